@@ -1,0 +1,234 @@
+"""Headline benchmark: transactions/s featurized + scored, and % of the HBM roofline.
+
+A step = one pass of the hot path over one batch already resident in HBM:
+  time flags -> re-key by CUSTOMER_ID -> customer 1/7/30-day windows -> re-key by
+  TERMINAL_ID -> terminal delayed-risk windows -> assemble the 15 input_features ->
+  StandardScaler + RandomForest(100 trees, depth 20) predict_proba.
+Workload per GPU (BASELINE.json configs[1]): 50k customers / 100k terminals / 183 days
+(~17.7M tx), synthetic data from the handbook distributions (fdx.synth), scored with the
+config-3 model (bench_assets/rf100_d20.npz, trained with sklearn on config-1 features).
+
+N GPUs (torch.distributed.run, one process per GPU): weak scaling, each rank owns its own
+50k customers; terminals are shared ids hashed to owner ranks and the terminal half runs
+after an RCCL all-to-all re-key (fdx.distributed).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
+
+METRIC = "transactions/sec featurized+scored (1/2/4/8 GPU) + % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# algorithmic bytes per row of one k_forest_chunk launch: scaled float32 features
+# (16 x 4 B slots) in + running float64 sum in + float64 sum/proba out
+FOREST_CHUNK_BYTES_PER_ROW = 64 + 8 + 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--customers", type=int, default=50_000)
+    ap.add_argument("--terminals", type=int, default=100_000)
+    ap.add_argument("--days", type=int, default=183)
+    ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-customers", type=int, default=2500)
+    ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
+    return ap.parse_args()
+
+
+def load_model(path):
+    import numpy as np
+
+    z = np.load(path)
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    return arrays, z["mean"], z["scale"], z["check_X"], z["check_proba"]
+
+
+def cpu_baseline(data, arrays, mean, scale, sample_customers):
+    """The CPU oracle (C port of the reference's pandas/sklearn arithmetic, 1 thread) on a
+    bounded sample: every transaction of customers [0, sample_customers)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+
+    m = data["customer"] < sample_customers
+    s = {k: v[m] for k, v in data.items()}
+    t0 = time.perf_counter()
+    f = oracle.featurize_arrays(s["ts"], s["customer"], s["terminal"], s["amount"], s["fraud"])
+    names = ["TX_DURING_WEEKEND", "TX_DURING_NIGHT"] + oracle.CUSTOMER_COLS + oracle.TERMINAL_COLS
+    X = np.column_stack([s["amount"]] + [f[k] for k in names])
+    oracle.forest_predict(X, arrays, mean, scale)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(s["ts"]) / dt, 1), "unit": "tx/s", "cores": 1, "kind": "port",
+            "sample": f"all {len(s['ts'])} tx of customers [0,{sample_customers}) of rank 0's batch: "
+                      f"flags + customer/terminal windows + scale + RF(100,d20) predict_proba, "
+                      f"C oracle (oracle/fdx_oracle.c), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from fdx import ops, synth
+    from fdx.pipeline import FraudPipeline
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    data = synth.generate(args.customers, args.terminals, args.days, seed=1234 + rank,
+                          customer_offset=rank * args.customers)
+    n_local = len(data["ts"])
+    arrays, mean, scale, check_X, check_proba = load_model(args.model)
+    forest = ops.Forest(arrays, 15, mean, scale)
+    T = lambda a, d: torch.from_numpy(np.ascontiguousarray(a)).to(dev, d)  # noqa: E731
+    # sanity: the GPU forest reproduces sklearn on the held-out sample saved with the model
+    got = forest.predict(T(check_X, torch.float64)).cpu().numpy()
+    if not np.array_equal(got, check_proba):
+        raise SystemExit("forest parity check against sklearn failed")
+
+    ts, cust, term = T(data["ts"], torch.int64), T(data["customer"], torch.int32), T(data["terminal"], torch.int32)
+    amt, fr = T(data["amount"], torch.float64), T(data["fraud"], torch.uint8)
+    pipe = FraudPipeline(forest=forest)
+    ws = ops.workspace(forest.workspace_size(n_local), dev)
+    proba = torch.empty(n_local, dtype=torch.float64, device=dev)
+    ev = []
+
+    if world > 1:
+        from fdx.distributed import ShardedPipeline
+
+        sp = ShardedPipeline(pipe, world, rank, args.terminals * world)
+        n_cust_total = args.customers * world
+
+        def step(record):
+            sp.run(ts, cust, term, amt, fr, n_cust_total, proba, ws, ev if record else None)
+    else:
+        def step(record):
+            f = pipe.featurize(ts, cust, term, amt, fr, args.customers, args.terminals)
+            ops.forest_prepare(forest, f.X, ws)
+            if record:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            ops.forest_traverse(forest, n_local, ws, proba)
+            if record:
+                b.record()
+                ev.append((a, b))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt, float(n_local)], dtype=torch.float64, device=dev)
+        dtm = t[:1].clone()
+        dist.all_reduce(dtm, op=dist.ReduceOp.MAX)
+        tot = t[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dt, n_total = float(dtm.item()), int(tot.item())
+    else:
+        n_total = n_local
+
+    trav_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    launch_ms = trav_ms / forest.n_chunks
+    achieved = FOREST_CHUNK_BYTES_PER_ROW * n_local / (launch_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(n_total * args.steps / dt, 1),
+        "unit": "tx/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: handbook-distribution generator (fdx.synth, seed 1234+rank), resident in HBM",
+        "config": {"workload": f"configs[1]: {args.customers} customers / {args.terminals} terminals / "
+                               f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
+                   "tx_per_gpu": n_local, "global_tx": n_total, "parallelism": f"customer-sharded x{world}",
+                   "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)"},
+        "roofline": {"kernel": "k_forest_chunk", "bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "avg_launch_ms": round(launch_ms, 4),
+                     "launches_per_step": forest.n_chunks,
+                     "bytes_per_row_per_launch": FOREST_CHUNK_BYTES_PER_ROW},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, args.cpu_sample_customers)
+    if args.breakdown and rank == 0:
+        print(json.dumps(stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba)),
+              file=sys.stderr)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
+    import torch
+
+    from fdx import ops
+
+    marks = []
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        marks.append((name, e))
+
+    n = ts.numel()
+    mark("start")
+    we, ni = ops.time_flags(ts)
+    mark("flags")
+    cperm, cseg, _ = ops.rekey(cust, args.customers)
+    mark("rekey_customer")
+    cts, camt = ops.gather(ts, cperm), ops.gather(amt, cperm)
+    mark("gather_customer")
+    cnb, cavg = ops.customer_windows(cts, camt, cseg)
+    mark("customer_windows")
+    tperm, tseg, _ = ops.rekey(term, args.terminals)
+    mark("rekey_terminal")
+    tts, tfr = ops.gather(ts, tperm), ops.gather(fr, tperm)
+    mark("gather_terminal")
+    tnb, trisk = ops.terminal_windows(tts, tfr, tseg)
+    mark("terminal_windows")
+    from fdx.pipeline import Features
+
+    X = pipe.assemble(Features(we, ni, cperm, cseg, cnb, cavg, tperm, tseg, tnb, trisk), amt)
+    mark("assemble")
+    ops.forest_prepare(forest, X, ws)
+    mark("forest_prepare")
+    ops.forest_traverse(forest, n, ws, proba)
+    mark("forest_traverse")
+    torch.cuda.synchronize()
+    return {"breakdown_ms": {marks[i][0]: round(marks[i - 1][1].elapsed_time(marks[i][1]), 4)
+                             for i in range(1, len(marks))}, "n": n}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/*
+ * fdx.h -- C ABI of the MI355X-native fraud-feature + scoring engine (libfdx.so).
+ *
+ * The reference (sauravtanwar786/Real-time_fraud_detection_system) has no FFI layer: its
+ * hot path is a set of Python functions called per group by pandas and a Spark pandas
+ * UDF.  Each entry point below replaces the arithmetic behind one of those calls for a
+ * WHOLE table (one call per table / Arrow batch, not per group); the Python drop-in
+ * (real-time_fraud_detection_system_amd/fdx) keeps the reference's names, signatures and
+ * DataFrame column contract on top of it.  See INTEGRATION.md for the bindings.
+ *
+ * Conventions
+ *   - Every pointer argument named *_d is DEVICE memory owned by the caller (e.g. a torch
+ *     tensor's data_ptr()); the library never frees caller memory and never allocates in
+ *     a compute call (scratch comes from a caller-passed workspace, see *_workspace_size).
+ *   - Host arrays (window lengths, tree descriptions) are read during the call only.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Every compute call is
+ *     stream-ordered and asynchronous; calls on different streams are independent.
+ *   - Return value: FDX_OK (0) or a negative FDX_E_* code; fdx_last_error() returns a
+ *     thread-local message for the last failing call on this thread.
+ *   - Timestamps are int64 nanoseconds since the Unix epoch (pandas datetime64[ns]).
+ *   - Grouped inputs: rows of key k occupy [seg_off_d[k], seg_off_d[k+1]) and are in
+ *     time order inside the segment (fdx_rekey produces exactly this layout).
+ */
+#ifndef FDX_H_
+#define FDX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDX_ABI_VERSION 1
+
+#define FDX_OK 0
+#define FDX_E_INVALID (-1)     /* bad argument (null pointer, size, unsupported shape) */
+#define FDX_E_HIP (-2)         /* a HIP runtime call failed */
+#define FDX_E_UNSUPPORTED (-3) /* input the engine does not implement (e.g. regressor forest) */
+#define FDX_E_WORKSPACE (-4)   /* workspace smaller than *_workspace_size() */
+
+#define FDX_MAX_WINDOWS 8
+#define FDX_MAX_FEATURES 32
+
+/* flag semantics: notebook (feature_transformation.ipynb:246-253, :294-301) or the Spark
+ * SQL of the streaming job (pyspark/scripts/fraud_detection.py:103-104). */
+#define FDX_FLAGS_NOTEBOOK 0 /* weekend = weekday()>=5 (Sat,Sun); night = hour<=6       */
+#define FDX_FLAGS_SPARK 1    /* weekend = dayofweek>=5 (Thu,Fri,Sat); night = hour>=20 (UTC) */
+
+const char *fdx_last_error(void);
+int fdx_abi_version(void);
+
+/* ---- a-1 / a-6: TX_DURING_WEEKEND, TX_DURING_NIGHT ------------------------------------
+ * Replaces `transactions_df.TX_DATETIME.apply(is_weekend|is_night)`
+ * (fraud_detection_model/feature_transformation.ipynb:278, :319) and the Spark SQL
+ * `if(dayofweek(tx_datetime) >= 5,1,0)`, `if(hour(tx_datetime) >= 20,1,0)`
+ * (pyspark/scripts/fraud_detection.py:103-104).  Outputs are 0/1 bytes, length n. */
+int fdx_time_flags(const int64_t *ts_ns_d, int64_t n, int32_t mode, uint8_t *weekend_d,
+                   uint8_t *night_d, void *stream);
+
+/* ---- a-2: customer spending-behaviour windows -----------------------------------------
+ * Replaces get_customer_spending_behaviour_features(customer_transactions,
+ * windows_size_in_days) (feature_transformation.ipynb:601-628) applied through
+ * `groupby('CUSTOMER_ID').apply(...)` (:1092), for all segments at once.
+ *   nb_d[w*n + i]  = rolling('{w}d').count()  (int32; the reference stores it as float64)
+ *   avg_d[w*n + i] = rolling('{w}d').sum() / count, bit-identical to pandas' Kahan
+ *                    add/remove roll_sum (exact emulation).
+ * window_ns: host array of n_windows window lengths in ns.  n = seg_off_d[n_seg]. */
+int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount_d, const int64_t *seg_off_d,
+                         int64_t n_seg, int64_t n, const int64_t *window_ns, int32_t n_windows,
+                         int32_t *nb_d, double *avg_d, void *stream);
+
+/* ---- a-3: terminal delayed-risk windows -----------------------------------------------
+ * Replaces get_count_risk_rolling_window(terminal_transactions, delay_period,
+ * windows_size_in_days, feature) (feature_transformation.ipynb:1495-1522) applied through
+ * `groupby('TERMINAL_ID').apply(...)` (:2435), for all segments at once.
+ *   nb_d[w*n+i]   = #rows of the segment with t in (t_i - delay - w, t_i - delay]
+ *   risk_d[w*n+i] = (#fraud rows in that window) / nb, or 0.0 when nb == 0 (fillna(0))
+ * fraud_d: 0/1 bytes. */
+int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int64_t *seg_off_d,
+                         int64_t n_seg, int64_t n, int64_t delay_ns, const int64_t *window_ns,
+                         int32_t n_windows, int32_t *nb_d, double *risk_d, void *stream);
+
+/* Assemble the 15-feature scoring matrix in the column order of `input_features`
+ * (model_training.ipynb:457-463 = pyspark/scripts/fraud_detection.py:126-132):
+ * X_d row r (leading dimension ld >= 3 + 4*n_windows, float64):
+ *   [TX_AMOUNT, TX_DURING_WEEKEND, TX_DURING_NIGHT,
+ *    CUSTOMER_ID_NB_TX_w, CUSTOMER_ID_AVG_AMOUNT_w (w = each window),
+ *    TERMINAL_ID_NB_TX_w, TERMINAL_ID_RISK_w (w = each window)]
+ * amount/weekend/night are in output row order; the grouped outputs of
+ * fdx_customer_windows / fdx_terminal_windows are scattered back through their perms. */
+int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
+                          const uint8_t *weekend_d, const uint8_t *night_d, const int32_t *cust_perm_d,
+                          const int32_t *cust_nb_d, const double *cust_avg_d, const int32_t *term_perm_d,
+                          const int32_t *term_nb_d, const double *term_risk_d, double *X_d, int64_t ld,
+                          void *stream);
+
+/* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
+ * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /
+ * groupby('TERMINAL_ID') (feature_transformation.ipynb:1092-1093, :2435-2436).
+ * keys_d[i] in [0, n_keys); key_bits = bits needed for n_keys-1 (<= 31).
+ * Outputs: perm_d[j] = input row placed at grouped position j (stable: equal keys keep
+ * input order), sorted_keys_d (optional, may be NULL), seg_off_d[0..n_keys] (CSR by key
+ * value; empty keys get empty segments). */
+size_t fdx_rekey_workspace_size(int64_t n, int32_t key_bits);
+int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, int32_t *perm_d,
+              int32_t *sorted_keys_d, int64_t *seg_off_d, void *workspace_d, size_t workspace_bytes,
+              void *stream);
+
+/* Stable argsort of int64 keys (e.g. TX_DATETIME ns): perm_d[j] = input row at sorted
+ * position j, ties keep input order.  Used when a caller's frame is not in time order
+ * (the reference sorts every group with sort_values('TX_DATETIME'),
+ * feature_transformation.ipynb:604, :1497). */
+size_t fdx_argsort_i64_workspace_size(int64_t n);
+int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *workspace_d,
+                    size_t workspace_bytes, void *stream);
+/* *flag_d = 1 if keys_d is non-decreasing, else 0 (stream-ordered). */
+int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream);
+
+/* dst[j] = src[perm[j]] for 1-, 2-, 4- or 8-byte elements (elem_bytes). */
+int fdx_gather(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n, void *dst_d,
+               void *stream);
+/* dst[perm[j]] = src[j]  (inverse of fdx_gather). */
+int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n, void *dst_d,
+                void *stream);
+
+/* ---- a-5 + a-7/a-8: StandardScaler + tree-ensemble predict_proba ----------------------
+ * Replaces `loaded_scaler.transform(features)` + `model.predict_proba(scaled)[:, 1]`
+ * (pyspark/scripts/fraud_detection.py:190-193) and the predict_proba inside
+ * fit_model_and_get_predictions (shared_functions.py:304-333 /
+ * model_training.ipynb:491-520) for sklearn DecisionTreeClassifier /
+ * RandomForestClassifier with 2 classes and one output.
+ *
+ * The forest is described with sklearn's own per-tree arrays concatenated over trees:
+ * tree t owns nodes [node_offsets[t], node_offsets[t+1]); child indices are tree-local
+ * (-1 = leaf), value1[i] = tree_.value[i, 0, 1] (class-1 fraction).  Scaler arrays are
+ * optional (NULL = no scaling). */
+/* StandardScaler.transform alone (shared_functions.py:114-120 scaleData):
+ * out[r,f] = (X[r,f] - mean[f]) / scale[f] in float64; mean_d/scale_d are device arrays
+ * (either may be NULL = skip that step).  Element (r, f) of X is X_d[r*row_stride +
+ * f*col_stride]; of out, out_d[r*out_row_stride + f*out_col_stride]. */
+int fdx_standard_scale(const double *X_d, int64_t n, int32_t n_features, int64_t row_stride,
+                       int64_t col_stride, const double *mean_d, const double *scale_d, double *out_d,
+                       int64_t out_row_stride, int64_t out_col_stride, void *stream);
+
+typedef struct fdx_forest_s *fdx_forest;
+
+typedef struct {
+    int32_t n_trees;
+    int32_t n_features;
+    const int64_t *node_offsets;   /* [n_trees+1] */
+    const int64_t *children_left;  /* [total nodes] */
+    const int64_t *children_right; /* [total nodes] */
+    const int64_t *feature;        /* [total nodes] */
+    const double *threshold;       /* [total nodes] */
+    const uint8_t *missing_go_to_left; /* [total nodes] (NULL = all 0) */
+    const double *value1;          /* [total nodes] */
+    const double *scaler_mean;     /* [n_features] or NULL */
+    const double *scaler_scale;    /* [n_features] or NULL */
+} fdx_forest_desc;
+
+int fdx_forest_create(const fdx_forest_desc *desc, fdx_forest *out, void *stream);
+/* Host-only: validate + pack the forest exactly as fdx_forest_create does (no GPU needed).
+ * nodes_out [total nodes] packed 8-byte nodes, orig_out [total] sklearn node id of each
+ * packed node, root_out [n_trees] packed position of each root. */
+int fdx_forest_pack(const fdx_forest_desc *desc, uint64_t *nodes_out, int32_t *orig_out,
+                    int32_t *root_out);
+int fdx_forest_destroy(fdx_forest forest);
+int fdx_forest_info(fdx_forest forest, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
+                    int32_t *n_chunks);
+size_t fdx_forest_workspace_size(fdx_forest forest, int64_t n_rows);
+/* X element (r, f) is X_d[r*row_stride + f*col_stride] (float64, raw unscaled features;
+ * NaN allowed = missing).  proba_d[r] = predict_proba(X)[r, 1]; leaf_d (optional) is
+ * [n][n_trees] int32 sklearn node ids (tree_.apply). */
+int fdx_forest_predict(fdx_forest forest, const double *X_d, int64_t n, int64_t row_stride,
+                       int64_t col_stride, double *proba_d, int32_t *leaf_d, void *workspace_d,
+                       size_t workspace_bytes, void *stream);
+
+/* The two halves of fdx_forest_predict, for callers that time or overlap them:
+ * prepare = scale + float32 cast into the workspace; traverse = the tree walk (one
+ * k_forest_chunk launch per LDS-sized chunk of trees) reading that workspace. */
+int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t row_stride,
+                       int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
+int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
+                        void *workspace_d, size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDX_H_ */

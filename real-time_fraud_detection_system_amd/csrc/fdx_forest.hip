@@ -1,0 +1,454 @@
+// fdx_forest.hip -- K3: StandardScaler + tree-ensemble predict_proba on gfx950.
+//
+// Replaces loaded_scaler.transform + model.predict_proba(...)[:, 1]
+// (pyspark/scripts/fraud_detection.py:190-193; shared_functions.py:304-333) for sklearn
+// DecisionTreeClassifier / RandomForestClassifier (2 classes, 1 output).
+//
+// Exactness recipe (bit-identical to sklearn 1.6/1.7 Tree._apply_dense + forest
+// accumulation):
+//   z64 = (x - mean) / scale                (float64, StandardScaler.transform)
+//   z32 = (float)z64                        (_validate_X_predict casts to float32, RNE)
+//   go left  <=>  isnan(z32) ? missing_go_to_left : (double)z32 <= thr64
+//           <=>  isnan(z32) ? missing_go_to_left : z32 <= thr32_down
+//   where thr32_down is the largest float <= thr64 (round toward -inf at load time)
+//   proba = (((0 + v_t0) + v_t1) + ...) / n_trees  in float64, trees in index order.
+//
+// Node format (8 bytes, trees re-laid out in pre-order so the left child is p+1):
+//   internal: hi = 0x80000000 | missing_left<<30 | feature<<25 | (right - p)  lo = thr32_down
+//   leaf    : the float64 class-1 value itself (sign bit 0, so hi bit 31 = 0)
+//
+// Kernel structure: trees are cut into chunks that fit the LDS budget; one launch per
+// chunk streams every row once: the block stages the chunk's nodes into LDS, each thread
+// stages its row's 16 scaled features into its own LDS column and walks G trees at once
+// (G independent dependency chains per lane hide the LDS latency).  The running float64
+// sum of a row crosses chunk launches through a workspace vector, preserving tree order.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "fdx_internal.h"
+
+struct fdx_forest_s {
+    int32_t n_trees = 0, n_features = 0, zstride = 16;
+    int64_t n_nodes = 0;
+    uint64_t *nodes_d = nullptr;   // packed nodes, all trees
+    int32_t *orig_d = nullptr;     // sklearn node id of each packed node
+    int32_t *root_d = nullptr;     // packed position of each tree root
+    double *mean_d = nullptr, *scale_d = nullptr;
+    struct Chunk {
+        int32_t t0, t1;
+        int64_t node_base, nodes;
+        bool in_lds;
+    };
+    std::vector<Chunk> chunks;
+};
+
+namespace fdx {
+namespace {
+
+constexpr int kFBlock = 512;
+constexpr int kG = 4;                          // trees walked concurrently per lane
+constexpr int kLdsNodeBytes16 = 120 * 1024;    // LDS for nodes when 16 feature slots
+constexpr int kLdsNodeBytes32 = 88 * 1024;     // LDS for nodes when 32 feature slots
+constexpr uint32_t kInternal = 0x80000000u;
+
+__device__ __forceinline__ double leaf_value(uint64_t nd) { return __longlong_as_double((long long)nd); }
+
+// z32[r][f] = (float)((x - mean[f]) / scale[f]); slots >= nf are 0.
+template <int FS>
+__global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, int64_t n, int64_t rs,
+                                                 int64_t cs, int32_t nf, const double *__restrict__ mean,
+                                                 const double *__restrict__ scale,
+                                                 float *__restrict__ z) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        float v[FS];
+#pragma unroll
+        for (int f = 0; f < FS; ++f) {
+            if (f < nf) {
+                double x = X[r * rs + (int64_t)f * cs];
+                if (mean) x = x - mean[f];
+                if (scale) x = x / scale[f];
+                v[f] = (float)x;
+            } else {
+                v[f] = 0.0f;
+            }
+        }
+        float4 *dst = reinterpret_cast<float4 *>(z + r * FS);
+#pragma unroll
+        for (int q = 0; q < FS / 4; ++q) dst[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+}
+
+// out = (X - mean) / scale elementwise in float64 (StandardScaler.transform), any strides.
+__global__ void __launch_bounds__(256) k_scale(const double *__restrict__ X, int64_t n, int32_t nf,
+                                               int64_t rs, int64_t cs, const double *__restrict__ mean,
+                                               const double *__restrict__ scale, double *__restrict__ out,
+                                               int64_t ors, int64_t ocs) {
+    const int64_t total = n * nf;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / nf;
+        const int f = (int)(e - r * nf);
+        double x = X[r * rs + (int64_t)f * cs];
+        if (mean) x = x - mean[f];
+        if (scale) x = x / scale[f];
+        out[r * ors + (int64_t)f * ocs] = x;
+    }
+}
+
+template <int FS, bool LDS>
+__global__ void __launch_bounds__(kFBlock) k_forest_chunk(
+    const uint64_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes,
+    const int32_t *__restrict__ root, int32_t t0, int32_t t1, const float *__restrict__ z, int64_t n,
+    double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
+    const int32_t *__restrict__ orig, int32_t n_trees, int first, int last) {
+    constexpr int kNodeCap = (LDS ? (FS == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) : 8) / 8;
+    __shared__ uint64_t s_nodes[kNodeCap];
+    __shared__ float s_x[FS][kFBlock];
+    const int tid = threadIdx.x;
+    const uint64_t *nb = nodes + node_base;
+    if (LDS) {
+        for (int i = tid; i < chunk_nodes; i += kFBlock) s_nodes[i] = nb[i];
+        __syncthreads();
+    }
+    for (int64_t row = (int64_t)blockIdx.x * kFBlock + tid; row < n;
+         row += (int64_t)gridDim.x * kFBlock) {
+        const float4 *src = reinterpret_cast<const float4 *>(z + row * FS);
+#pragma unroll
+        for (int q = 0; q < FS / 4; ++q) {
+            float4 v = src[q];
+            s_x[4 * q + 0][tid] = v.x;
+            s_x[4 * q + 1][tid] = v.y;
+            s_x[4 * q + 2][tid] = v.z;
+            s_x[4 * q + 3][tid] = v.w;
+        }
+        double a = first ? 0.0 : acc[row];
+        for (int t = t0; t < t1; t += kG) {
+            uint32_t p[kG];
+            uint64_t nd[kG];
+#pragma unroll
+            for (int g = 0; g < kG; ++g) {
+                const bool act = t + g < t1;
+                p[g] = act ? (uint32_t)(root[t + g] - node_base) : 0u;
+                nd[g] = act ? (LDS ? s_nodes[p[g]] : nb[p[g]]) : 0ull;
+            }
+            bool any = true;
+            while (any) {
+                any = false;
+#pragma unroll
+                for (int g = 0; g < kG; ++g) {
+                    const uint32_t hi = (uint32_t)(nd[g] >> 32);
+                    if (hi & kInternal) {
+                        const float x = s_x[(hi >> 25) & 31][tid];
+                        const float thr = __uint_as_float((uint32_t)nd[g]);
+                        const bool left = (x != x) ? ((hi >> 30) & 1u) : (x <= thr);
+                        p[g] = left ? p[g] + 1u : p[g] + (hi & 0x1FFFFFFu);
+                        nd[g] = LDS ? s_nodes[p[g]] : nb[p[g]];
+                        any = true;
+                    }
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < kG; ++g) {
+                if (t + g < t1) {
+                    a += leaf_value(nd[g]);
+                    if (leaf_out) leaf_out[row * n_trees + t + g] = orig[node_base + p[g]];
+                }
+            }
+        }
+        if (last)
+            proba[row] = a / (double)n_trees;
+        else
+            acc[row] = a;
+    }
+}
+
+float round_down_f32(double t) {
+    float f = (float)t;
+    if ((double)f > t) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+}  // namespace fdx
+
+using namespace fdx;
+
+namespace fdx {
+namespace {
+// Host-side validation + pre-order re-layout + 8-byte node packing (see header comment).
+int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::vector<int32_t> &orig,
+                std::vector<int32_t> &root) {
+    FDX_REQUIRE(d, "null pointer");
+    FDX_REQUIRE(d->n_trees >= 1, "n_trees must be >= 1");
+    FDX_REQUIRE(d->n_features >= 1 && d->n_features <= FDX_MAX_FEATURES, "n_features must be in [1, %d]",
+                FDX_MAX_FEATURES);
+    FDX_REQUIRE(d->node_offsets && d->children_left && d->children_right && d->feature && d->threshold &&
+                    d->value1,
+                "null tree array");
+    const int64_t total = d->node_offsets[d->n_trees];
+    FDX_REQUIRE(d->node_offsets[0] == 0 && total > 0 && total < (int64_t(1) << 31), "bad node_offsets");
+    packed.assign((size_t)total, 0);
+    orig.assign((size_t)total, 0);
+    root.assign((size_t)d->n_trees, 0);
+    std::vector<int64_t> stack;
+    for (int32_t t = 0; t < d->n_trees; ++t) {
+        const int64_t b = d->node_offsets[t], e = d->node_offsets[t + 1];
+        FDX_REQUIRE(e > b, "tree %d is empty", t);
+        const int64_t cnt = e - b;
+        // pre-order re-layout (identity for sklearn's depth-first builder)
+        std::vector<int64_t> pos((size_t)cnt, -1);
+        int64_t next = b;
+        stack.clear();
+        stack.push_back(0);
+        std::vector<int64_t> order;
+        order.reserve((size_t)cnt);
+        while (!stack.empty()) {
+            int64_t i = stack.back();
+            stack.pop_back();
+            FDX_REQUIRE(i >= 0 && i < cnt && pos[(size_t)i] < 0, "tree %d: malformed children", t);
+            pos[(size_t)i] = next++;
+            order.push_back(i);
+            int64_t l = d->children_left[b + i], r = d->children_right[b + i];
+            if (l != -1) {
+                FDX_REQUIRE(r != -1, "tree %d node %lld has one child", t, (long long)i);
+                stack.push_back(r);
+                stack.push_back(l);
+            }
+        }
+        FDX_REQUIRE(next == e, "tree %d: %lld unreachable nodes", t, (long long)(e - next));
+        root[(size_t)t] = (int32_t)b;
+        for (int64_t i : order) {
+            const int64_t p = pos[(size_t)i];
+            orig[(size_t)p] = (int32_t)i;
+            const int64_t l = d->children_left[b + i];
+            if (l == -1) {
+                double v = d->value1[b + i];
+                FDX_REQUIRE(!(v != v), "tree %d leaf %lld value is NaN", t, (long long)i);
+                if (v == 0.0) v = 0.0;  // normalise -0.0
+                uint64_t bits;
+                memcpy(&bits, &v, 8);
+                if (bits >> 63) {
+                    set_error("tree %d leaf %lld: negative leaf values are not supported", t, (long long)i);
+                    return FDX_E_UNSUPPORTED;
+                }
+                packed[(size_t)p] = bits;
+            } else {
+                const int64_t rp = pos[(size_t)d->children_right[b + i]];
+                FDX_REQUIRE(pos[(size_t)l] == p + 1, "tree %d: pre-order violated", t);
+                const int64_t rel = rp - p;
+                FDX_REQUIRE(rel > 0 && rel < (int64_t(1) << 25), "tree %d: subtree too large", t);
+                const int64_t f = d->feature[b + i];
+                FDX_REQUIRE(f >= 0 && f < d->n_features, "tree %d node %lld: feature %lld out of range", t,
+                            (long long)i, (long long)f);
+                const uint32_t ml = d->missing_go_to_left ? (d->missing_go_to_left[b + i] != 0) : 0u;
+                const float thr = round_down_f32(d->threshold[b + i]);
+                uint32_t lo;
+                memcpy(&lo, &thr, 4);
+                const uint32_t hi = kInternal | (ml << 30) | ((uint32_t)f << 25) | (uint32_t)rel;
+                packed[(size_t)p] = ((uint64_t)hi << 32) | lo;
+            }
+        }
+    }
+    return FDX_OK;
+}
+}  // namespace
+}  // namespace fdx
+
+extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, int32_t *orig_out,
+                               int32_t *root_out) {
+    std::vector<uint64_t> packed;
+    std::vector<int32_t> orig, root;
+    int rc = pack_forest(d, packed, orig, root);
+    if (rc) return rc;
+    FDX_REQUIRE(nodes_out && orig_out && root_out, "null output");
+    memcpy(nodes_out, packed.data(), packed.size() * 8);
+    memcpy(orig_out, orig.data(), orig.size() * 4);
+    memcpy(root_out, root.data(), root.size() * 4);
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void *stream) {
+    FDX_REQUIRE(d && out, "null pointer");
+    *out = nullptr;
+    std::vector<uint64_t> packed;
+    std::vector<int32_t> orig, root;
+    int rc = pack_forest(d, packed, orig, root);
+    if (rc) return rc;
+    const int64_t total = (int64_t)packed.size();
+    fdx_forest_s *F = new (std::nothrow) fdx_forest_s();
+    FDX_REQUIRE(F, "out of host memory");
+    F->n_trees = d->n_trees;
+    F->n_features = d->n_features;
+    F->zstride = d->n_features <= 16 ? 16 : 32;
+    F->n_nodes = total;
+    const int64_t cap_nodes = (F->zstride == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) / 8;
+    for (int32_t t = 0; t < d->n_trees;) {
+        fdx_forest_s::Chunk c;
+        c.t0 = t;
+        c.node_base = d->node_offsets[t];
+        int64_t sz = d->node_offsets[t + 1] - d->node_offsets[t];
+        if (sz > cap_nodes) {
+            c.t1 = t + 1;
+            c.in_lds = false;
+        } else {
+            int32_t u = t + 1;
+            while (u < d->n_trees && d->node_offsets[u + 1] - c.node_base <= cap_nodes) ++u;
+            c.t1 = u;
+            c.in_lds = true;
+        }
+        c.nodes = d->node_offsets[c.t1] - c.node_base;
+        F->chunks.push_back(c);
+        t = c.t1;
+    }
+    hipStream_t st = as_stream(stream);
+    auto fail = [&](hipError_t e, const char *what) {
+        set_error("%s failed: %s", what, hipGetErrorString(e));
+        fdx_forest_destroy(F);
+        return FDX_E_HIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&F->nodes_d, sizeof(uint64_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&F->root_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMemcpyAsync(F->nodes_d, packed.data(), sizeof(uint64_t) * total, hipMemcpyHostToDevice, st)))
+        return fail(e, "hipMemcpyAsync");
+    if ((e = hipMemcpyAsync(F->orig_d, orig.data(), sizeof(int32_t) * total, hipMemcpyHostToDevice, st)))
+        return fail(e, "hipMemcpyAsync");
+    if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
+        return fail(e, "hipMemcpyAsync");
+    if (d->scaler_mean) {
+        if ((e = hipMalloc(&F->mean_d, sizeof(double) * d->n_features))) return fail(e, "hipMalloc");
+        if ((e = hipMemcpyAsync(F->mean_d, d->scaler_mean, sizeof(double) * d->n_features,
+                                hipMemcpyHostToDevice, st)))
+            return fail(e, "hipMemcpyAsync");
+    }
+    if (d->scaler_scale) {
+        if ((e = hipMalloc(&F->scale_d, sizeof(double) * d->n_features))) return fail(e, "hipMalloc");
+        if ((e = hipMemcpyAsync(F->scale_d, d->scaler_scale, sizeof(double) * d->n_features,
+                                hipMemcpyHostToDevice, st)))
+            return fail(e, "hipMemcpyAsync");
+    }
+    // host vectors die at return: make the uploads complete first
+    if ((e = hipStreamSynchronize(st))) return fail(e, "hipStreamSynchronize");
+    *out = F;
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_destroy(fdx_forest F) {
+    if (!F) return FDX_OK;
+    (void)hipFree(F->nodes_d);
+    (void)hipFree(F->orig_d);
+    (void)hipFree(F->root_d);
+    (void)hipFree(F->mean_d);
+    (void)hipFree(F->scale_d);
+    delete F;
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_info(fdx_forest F, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
+                               int32_t *n_chunks) {
+    FDX_REQUIRE(F, "null forest");
+    if (n_trees) *n_trees = F->n_trees;
+    if (n_features) *n_features = F->n_features;
+    if (n_nodes) *n_nodes = F->n_nodes;
+    if (n_chunks) *n_chunks = (int32_t)F->chunks.size();
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows) {
+    if (!F || n_rows <= 0) return 256;
+    return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows);
+}
+
+static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, double **acc) {
+    size_t need = fdx_forest_workspace_size(F, n);
+    if (!ws || ws_bytes < need) {
+        set_error("forest workspace too small: %zu < %zu", ws_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    *z = reinterpret_cast<float *>(ws);
+    *acc = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) +
+                                      align_up(sizeof(float) * F->zstride * (size_t)n));
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, int64_t row_stride,
+                                  int64_t col_stride, void *ws, size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(X_d, "null pointer");
+    float *z;
+    double *acc;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    unsigned grid = stream_grid(n, 256);
+    if (F->zstride == 16)
+        hipLaunchKernelGGL(k_prepare<16>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
+                           F->n_features, F->mean_d, F->scale_d, z);
+    else
+        hipLaunchKernelGGL(k_prepare<32>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
+                           F->n_features, F->mean_d, F->scale_d, z);
+    FDX_LAUNCHED("k_prepare");
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int32_t *leaf_d, void *ws,
+                                   size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(proba_d, "null pointer");
+    float *z;
+    double *acc;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, kFBlock), 256 * 4);
+    const size_t nc = F->chunks.size();
+    for (size_t c = 0; c < nc; ++c) {
+        const auto &ch = F->chunks[c];
+        const int first = c == 0, last = c + 1 == nc;
+#define FDX_LAUNCH_CHUNK(FS, L)                                                                        \
+    hipLaunchKernelGGL((k_forest_chunk<FS, L>), dim3(grid), dim3(kFBlock), 0, st, F->nodes_d, ch.node_base, \
+                       (int32_t)ch.nodes, F->root_d, ch.t0, ch.t1, z, n, acc, proba_d, leaf_d, F->orig_d,    \
+                       F->n_trees, first, last)
+        if (F->zstride == 16) {
+            if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
+        } else {
+            if (ch.in_lds) FDX_LAUNCH_CHUNK(32, true); else FDX_LAUNCH_CHUNK(32, false);
+        }
+#undef FDX_LAUNCH_CHUNK
+        FDX_LAUNCHED("k_forest_chunk");
+    }
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_predict(fdx_forest F, const double *X_d, int64_t n, int64_t row_stride,
+                                  int64_t col_stride, double *proba_d, int32_t *leaf_d, void *ws,
+                                  size_t ws_bytes, void *stream) {
+    int rc = fdx_forest_prepare(F, X_d, n, row_stride, col_stride, ws, ws_bytes, stream);
+    if (rc) return rc;
+    return fdx_forest_traverse(F, n, proba_d, leaf_d, ws, ws_bytes, stream);
+}
+
+extern "C" int fdx_standard_scale(const double *X_d, int64_t n, int32_t n_features, int64_t row_stride,
+                                  int64_t col_stride, const double *mean_d, const double *scale_d,
+                                  double *out_d, int64_t out_row_stride, int64_t out_col_stride,
+                                  void *stream) {
+    FDX_REQUIRE(n >= 0 && n_features >= 1, "bad shape");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(X_d && out_d, "null pointer");
+    hipLaunchKernelGGL(k_scale, dim3(stream_grid(n * n_features, 256)), dim3(256), 0, as_stream(stream), X_d,
+                       n, n_features, row_stride, col_stride, mean_d, scale_d, out_d, out_row_stride,
+                       out_col_stride);
+    FDX_LAUNCHED("k_scale");
+    return FDX_OK;
+}

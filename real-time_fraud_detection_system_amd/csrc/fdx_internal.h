@@ -1,0 +1,59 @@
+// Internal helpers shared by the fdx HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "fdx.h"
+
+namespace fdx {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+void set_error(const char *fmt, ...);
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define FDX_REQUIRE(cond, ...)                     \
+    do {                                           \
+        if (!(cond)) {                             \
+            ::fdx::set_error(__VA_ARGS__);         \
+            return FDX_E_INVALID;                  \
+        }                                          \
+    } while (0)
+
+#define FDX_HIP(call)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            ::fdx::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),       \
+                             __FILE__, __LINE__);                                         \
+            return FDX_E_HIP;                                                             \
+        }                                                                                 \
+    } while (0)
+
+// Checks the launch that was just enqueued.
+#define FDX_LAUNCHED(name)                                                                \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess) {                                                           \
+            ::fdx::set_error("launch of %s failed: %s", name, hipGetErrorString(e_));      \
+            return FDX_E_HIP;                                                             \
+        }                                                                                 \
+    } while (0)
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid for a grid-stride streaming kernel: enough blocks to fill 256 CUs several times,
+// capped so launch overhead and tail stay small (cdna_hip_programming.md Guideline 11).
+inline unsigned stream_grid(int64_t n, int block, int64_t cap = 256 * 8) {
+    int64_t g = ceil_div(n, block);
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+}  // namespace fdx

@@ -1,0 +1,462 @@
+// fdx_rekey.hip -- K2: stable LSD radix key-sort + segment compaction (re-keying
+// CUSTOMER_ID -> TERMINAL_ID), plus permutation gather/scatter.
+//
+// Replaces the regrouping implied by pandas groupby('CUSTOMER_ID') -> sort_values
+// ('TX_DATETIME') -> groupby('TERMINAL_ID') (feature_transformation.ipynb:1092-1093,
+// :2435-2436).  Because the input table is already in time order, a STABLE sort on the key
+// alone yields per-key time order, which is what the window kernels need.
+//
+// Per pass (8-bit digit): hist (per-tile digit counts, LDS atomics) -> device-wide
+// exclusive scan over the digit-major [256][tiles] table -> scatter (wave ballot
+// multisplit gives the stable in-tile rank; the tile is re-ordered in LDS so that the
+// global writes are runs of consecutive addresses).  All traffic is HBM-streaming.
+#include <algorithm>
+
+#include "fdx_internal.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kRadixBits = 8;
+constexpr int kBins = 1 << kRadixBits;
+constexpr int kBlock = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kBlock * kItems;  // 4096 keys per tile
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---------------------------------------------------------------- device-wide scan
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanChunk = kScanBlock * kScanItems;
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t u = __shfl_up(v, d, kWave);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+// exclusive block scan of one value per thread; returns the block total via *total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t s_w[kScanBlock / kWave];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    uint32_t inc = wave_incl_scan_u32(v, lane);
+    if (lane == kWave - 1) s_w[wv] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kScanBlock / kWave; ++w) {
+        uint32_t x = s_w[w];
+        if (w < wv) base += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_partials(const uint32_t *__restrict__ in,
+                                                              int64_t m, uint32_t *__restrict__ part) {
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        int64_t i = base + (int64_t)k * kScanBlock + threadIdx.x;
+        if (i < m) s += in[i];
+    }
+    uint32_t tot;
+    block_excl_scan(s, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of part[0..P) in place
+__global__ void __launch_bounds__(kScanBlock) k_scan_single(uint32_t *__restrict__ part, int64_t P) {
+    uint32_t carry = 0;
+    for (int64_t c = 0; c < P; c += kScanBlock) {
+        int64_t i = c + threadIdx.x;
+        uint32_t v = i < P ? part[i] : 0u;
+        uint32_t tot;
+        uint32_t ex = block_excl_scan(v, &tot);
+        if (i < P) part[i] = ex + carry;
+        carry += tot;
+    }
+}
+
+// out = exclusive_scan(in) using the per-chunk bases in part (may alias in == out)
+__global__ void __launch_bounds__(kScanBlock) k_scan_apply(const uint32_t *in, int64_t m,
+                                                           const uint32_t *__restrict__ part,
+                                                           uint32_t *out) {
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        int64_t i = base + k;
+        v[k] = i < m ? in[i] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(s, &tot) + part[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        int64_t i = base + k;
+        if (i < m) out[i] = ex;
+        ex += v[k];
+    }
+}
+
+int64_t scan_partials_count(int64_t m) { return ceil_div(m, kScanChunk); }
+
+int exclusive_scan(uint32_t *data, int64_t m, uint32_t *part, hipStream_t st) {
+    if (m == 0) return FDX_OK;
+    const int64_t P = scan_partials_count(m);
+    hipLaunchKernelGGL(k_scan_partials, dim3((unsigned)P), dim3(kScanBlock), 0, st, data, m, part);
+    FDX_LAUNCHED("k_scan_partials");
+    hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(kScanBlock), 0, st, part, P);
+    FDX_LAUNCHED("k_scan_single");
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)P), dim3(kScanBlock), 0, st, data, m, part, data);
+    FDX_LAUNCHED("k_scan_apply");
+    return FDX_OK;
+}
+
+// ------------------------------------------------------------------- radix passes
+template <typename K>
+__device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
+    return (uint32_t)(((k ^ flip) >> shift) & (K)(kBins - 1));
+}
+
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ keys, int64_t n, int shift,
+                                                       K flip, int64_t n_tiles,
+                                                       uint32_t *__restrict__ hist) {
+    __shared__ uint32_t s_h[kBins];
+    for (int d = threadIdx.x; d < kBins; d += kBlock) s_h[d] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        int64_t i = base + (int64_t)k * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&s_h[digit_of(keys[i], shift, flip)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < kBins; d += kBlock) hist[(int64_t)d * n_tiles + blockIdx.x] = s_h[d];
+}
+
+// Stable scatter of one tile.  vals_in == nullptr means "the value is the row index".
+template <typename K>
+__global__ void __launch_bounds__(kBlock) k_radix_scatter(
+    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
+    int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out) {
+    __shared__ uint32_t s_run[kBins];                  // digit counts of earlier rounds
+    __shared__ uint32_t s_wcnt[kWavesPerBlock][kBins]; // this round's per-wave counts
+    __shared__ uint32_t s_start[kBins];                // tile-local digit starts
+    __shared__ K s_key[kTile];
+    __shared__ uint32_t s_val[kTile];
+
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    for (int d = tid; d < kBins; d += kBlock) {
+        s_run[d] = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) s_wcnt[w][d] = 0;
+    }
+    __syncthreads();
+
+    K key[kItems];
+    uint32_t val[kItems], rank[kItems];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + (int64_t)r * kBlock + tid;
+        const bool valid = i < n;
+        key[r] = valid ? keys_in[i] : (K)0;
+        val[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+        const uint32_t d = digit_of(key[r], shift, flip);
+        // peers: lanes of this wave holding the same digit (wave multisplit by ballots)
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t in_wave = (uint32_t)__popcll(peers & lt_mask);
+        if (valid && in_wave == 0) s_wcnt[wv][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = s_run[d];
+            for (int w = 0; w < wv; ++w) pre += s_wcnt[w][d];
+            rank[r] = pre + in_wave;
+        }
+        __syncthreads();
+        for (int dd = tid; dd < kBins; dd += kBlock) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                s += s_wcnt[w][dd];
+                s_wcnt[w][dd] = 0;
+            }
+            s_run[dd] += s;
+        }
+        __syncthreads();
+    }
+    // tile-local digit starts = exclusive scan of s_run over digits (kBins == kBlock)
+    {
+        uint32_t tot;
+        uint32_t ex = block_excl_scan(s_run[tid], &tot);
+        s_start[tid] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + (int64_t)r * kBlock + tid;
+        if (i < n) {
+            const uint32_t d = digit_of(key[r], shift, flip);
+            const uint32_t p = s_start[d] + rank[r];
+            s_key[p] = key[r];
+            s_val[p] = val[r];
+        }
+    }
+    __syncthreads();
+    const int64_t cnt = std::min<int64_t>(kTile, n - base);
+    for (int p = tid; p < cnt; p += kBlock) {
+        const K k = s_key[p];
+        const uint32_t d = digit_of(k, shift, flip);
+        const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
+        keys_out[dst] = k;
+        vals_out[dst] = s_val[p];
+    }
+}
+
+__global__ void k_iota(uint32_t *__restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)i;
+}
+
+__global__ void k_copy_u32(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+// seg_off[q] = first sorted position whose key >= q, for q in [0, n_keys]
+__global__ void k_seg_offsets(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys,
+                              int64_t *__restrict__ seg_off) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = (i == 0) ? 0 : (int64_t)sk[i - 1] + 1;     // first key value owned here
+        int64_t hi = (i == n) ? n_keys : (int64_t)sk[i];        // last key value owned here
+        if (hi > n_keys) hi = n_keys;
+        for (int64_t q = lo; q <= hi; ++q) seg_off[q] = i;
+    }
+}
+
+template <typename T>
+__global__ void k_gather(const T *__restrict__ src, const int32_t *__restrict__ perm, int64_t n,
+                         T *__restrict__ dst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[perm[i]];
+}
+
+template <typename T>
+__global__ void k_scatter(const T *__restrict__ src, const int32_t *__restrict__ perm, int64_t n,
+                          T *__restrict__ dst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        dst[perm[i]] = src[i];
+}
+
+__global__ void k_check_sorted_i64(const int64_t *__restrict__ k, int64_t n, int32_t *__restrict__ flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (k[i] < k[i - 1]) *flag = 0;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Workspace of one radix sort of n keys of type K: two ping-pong key/value buffers, the
+// digit histogram table and the scan partials.
+template <typename K>
+struct SortWs {
+    K *k0, *k1;
+    uint32_t *v0, *v1, *hist, *part;
+};
+
+template <typename K>
+size_t sort_ws(int64_t n, SortWs<K> *w, char *base) {
+    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kTile));
+    const int64_t hm = tiles * kBins;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char *p = base ? base + off : nullptr;
+        off += align_up(bytes);
+        return p;
+    };
+    SortWs<K> t;
+    t.k0 = reinterpret_cast<K *>(take(sizeof(K) * n));
+    t.k1 = reinterpret_cast<K *>(take(sizeof(K) * n));
+    t.v0 = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * n));
+    t.v1 = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * n));
+    t.hist = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * hm));
+    t.part = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * (scan_partials_count(hm) + 1)));
+    if (w) *w = t;
+    return off;
+}
+
+// Stable LSD radix sort of (key, row index) pairs over the low `bits` bits of (key ^ flip).
+// vals_out receives the input row index of each sorted position; keys_out (optional) the
+// sorted keys.  Returns the buffer that holds the sorted keys.
+template <typename K>
+int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t *vals_out,
+               const SortWs<K> &w, hipStream_t st, const K **sorted) {
+    const int64_t tiles = ceil_div(n, kTile);
+    const int passes = (bits + kRadixBits - 1) / kRadixBits;
+    const K *kin = keys;
+    const uint32_t *vin = nullptr;  // identity on the first pass
+    if (passes == 0) {
+        hipLaunchKernelGGL(k_iota, dim3(stream_grid(n, 256)), dim3(256), 0, st, vals_out, n);
+        FDX_LAUNCHED("k_iota");
+        *sorted = keys;
+        return FDX_OK;
+    }
+    for (int p = 0; p < passes; ++p) {
+        const int shift = p * kRadixBits;
+        const bool last = p == passes - 1;
+        K *kout = (p & 1) ? w.k1 : w.k0;
+        if (last && keys_out) kout = keys_out;
+        uint32_t *vout = last ? vals_out : ((p & 1) ? w.v1 : w.v0);
+        hipLaunchKernelGGL(k_radix_hist<K>, dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
+                           tiles, w.hist);
+        FDX_LAUNCHED("k_radix_hist");
+        int rc = exclusive_scan(w.hist, tiles * kBins, w.part, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_radix_scatter<K>, dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n, shift,
+                           flip, tiles, w.hist, kout, vout);
+        FDX_LAUNCHED("k_radix_scatter");
+        kin = kout;
+        vin = vout;
+    }
+    *sorted = kin;
+    return FDX_OK;
+}
+
+}  // namespace
+}  // namespace fdx
+
+using namespace fdx;
+
+extern "C" size_t fdx_rekey_workspace_size(int64_t n, int32_t key_bits) {
+    (void)key_bits;
+    if (n < 0) n = 0;
+    return sort_ws<uint32_t>(n, nullptr, nullptr);
+}
+
+extern "C" int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                         int32_t *perm_d, int32_t *sorted_keys_d, int64_t *seg_off_d,
+                         void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(key_bits >= 0 && key_bits <= 31, "key_bits must be in [0, 31]");
+    FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
+    FDX_REQUIRE(seg_off_d && perm_d, "null pointer");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
+        return FDX_OK;
+    }
+    FDX_REQUIRE(keys_d, "null keys");
+    SortWs<uint32_t> w;
+    size_t need = sort_ws<uint32_t>(n, &w, reinterpret_cast<char *>(workspace_d));
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("rekey workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    const uint32_t *sorted = nullptr;
+    int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u,
+                                  reinterpret_cast<uint32_t *>(sorted_keys_d),
+                                  reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted);
+    if (rc) return rc;
+    if (sorted_keys_d && sorted != reinterpret_cast<const uint32_t *>(sorted_keys_d)) {
+        hipLaunchKernelGGL(k_copy_u32, dim3(stream_grid(n, 256)), dim3(256), 0, st, sorted,
+                           reinterpret_cast<uint32_t *>(sorted_keys_d), n);
+        FDX_LAUNCHED("k_copy_u32");
+    }
+    hipLaunchKernelGGL(k_seg_offsets, dim3(stream_grid(n + 1, 256)), dim3(256), 0, st, sorted, n, n_keys,
+                       seg_off_d);
+    FDX_LAUNCHED("k_seg_offsets");
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_argsort_i64_workspace_size(int64_t n) {
+    if (n < 0) n = 0;
+    return sort_ws<uint64_t>(n, nullptr, nullptr);
+}
+
+extern "C" int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *workspace_d,
+                               size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(keys_d && perm_d, "null pointer");
+    SortWs<uint64_t> w;
+    size_t need = sort_ws<uint64_t>(n, &w, reinterpret_cast<char *>(workspace_d));
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("argsort workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    const uint64_t *sorted = nullptr;
+    // signed order: flip the sign bit so that negative keys sort first
+    return radix_sort<uint64_t>(reinterpret_cast<const uint64_t *>(keys_d), n, 64, 1ull << 63, nullptr,
+                                reinterpret_cast<uint32_t *>(perm_d), w, as_stream(stream), &sorted);
+}
+
+extern "C" int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream) {
+    FDX_REQUIRE(n >= 0 && flag_d, "bad argument");
+    hipStream_t st = as_stream(stream);
+    FDX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag_d), 1, 1, st));
+    if (n < 2) return FDX_OK;
+    FDX_REQUIRE(keys_d, "null keys");
+    hipLaunchKernelGGL(k_check_sorted_i64, dim3(stream_grid(n, 256)), dim3(256), 0, st, keys_d, n, flag_d);
+    FDX_LAUNCHED("k_check_sorted_i64");
+    return FDX_OK;
+}
+
+template <typename T>
+static int launch_perm(bool gather, const void *src, const int32_t *perm, int64_t n, void *dst,
+                       hipStream_t st) {
+    unsigned grid = stream_grid(n, 256);
+    if (gather)
+        hipLaunchKernelGGL(k_gather<T>, dim3(grid), dim3(256), 0, st, (const T *)src, perm, n, (T *)dst);
+    else
+        hipLaunchKernelGGL(k_scatter<T>, dim3(grid), dim3(256), 0, st, (const T *)src, perm, n, (T *)dst);
+    FDX_LAUNCHED(gather ? "k_gather" : "k_scatter");
+    return FDX_OK;
+}
+
+static int perm_op(bool gather, const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n,
+                   void *dst_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(src_d && perm_d && dst_d, "null pointer");
+    hipStream_t st = as_stream(stream);
+    switch (elem_bytes) {
+        case 1: return launch_perm<uint8_t>(gather, src_d, perm_d, n, dst_d, st);
+        case 2: return launch_perm<uint16_t>(gather, src_d, perm_d, n, dst_d, st);
+        case 4: return launch_perm<uint32_t>(gather, src_d, perm_d, n, dst_d, st);
+        case 8: return launch_perm<uint64_t>(gather, src_d, perm_d, n, dst_d, st);
+        default: set_error("elem_bytes must be 1, 2, 4 or 8"); return FDX_E_INVALID;
+    }
+}
+
+extern "C" int fdx_gather(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n,
+                          void *dst_d, void *stream) {
+    return perm_op(true, src_d, elem_bytes, perm_d, n, dst_d, stream);
+}
+
+extern "C" int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n,
+                           void *dst_d, void *stream) {
+    return perm_op(false, src_d, elem_bytes, perm_d, n, dst_d, stream);
+}

@@ -1,0 +1,381 @@
+// fdx_windows.hip -- K1: time flags, customer spending windows, terminal delayed-risk
+// windows on gfx950.  HBM-bound integer/FP64 scan work (no MFMA: nothing here is a
+// contraction).
+//
+// Reference behaviour (see include/fdx.h for the per-entry citations):
+//   flags     feature_transformation.ipynb:246-253, :294-301; fraud_detection.py:103-104
+//   customer  feature_transformation.ipynb:601-628 (pandas rolling('{w}d').sum()/count())
+//   terminal  feature_transformation.ipynb:1495-1522 (rolling(delay) vs rolling(delay+w))
+#include "fdx_internal.h"
+
+namespace fdx {
+namespace {
+
+constexpr int64_t kNsPerDay = 86400LL * 1000000000LL;
+constexpr int64_t kNsPerHour = 3600LL * 1000000000LL;
+
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// ----------------------------------------------------------------------------- flags
+// 8 rows per thread: 64 B of timestamps in, 8 B per flag array out (one u64 store each).
+__global__ void __launch_bounds__(256) k_time_flags(const int64_t *__restrict__ ts, int64_t n,
+                                                    int32_t mode, uint8_t *__restrict__ weekend,
+                                                    uint8_t *__restrict__ night) {
+    const int64_t n8 = n / 8;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n8; g += stride) {
+        const int64_t *p = ts + g * 8;
+        uint64_t we = 0, ni = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            int64_t t = p[k];
+            int64_t day = floor_div(t, kNsPerDay);
+            int64_t hour = (t - day * kNsPerDay) / kNsPerHour;
+            int64_t wd = (day + 3) % 7;  // Monday=0 (1970-01-01 was a Thursday); day may be < 0
+            if (wd < 0) wd += 7;
+            bool w, nt;
+            if (mode == FDX_FLAGS_NOTEBOOK) {
+                w = wd >= 5;
+                nt = hour <= 6;
+            } else {
+                int64_t dow = ((wd + 1) % 7) + 1;  // Spark dayofweek: Sunday=1 .. Saturday=7
+                w = dow >= 5;
+                nt = hour >= 20;
+            }
+            we |= (uint64_t)w << (8 * k);
+            ni |= (uint64_t)nt << (8 * k);
+        }
+        reinterpret_cast<uint64_t *>(weekend)[g] = we;
+        reinterpret_cast<uint64_t *>(night)[g] = ni;
+    }
+    // tail (< 8 rows) handled by block 0
+    if (blockIdx.x == 0 && threadIdx.x < (unsigned)(n - n8 * 8)) {
+        int64_t i = n8 * 8 + threadIdx.x;
+        int64_t t = ts[i];
+        int64_t day = floor_div(t, kNsPerDay);
+        int64_t hour = (t - day * kNsPerDay) / kNsPerHour;
+        int64_t wd = (day + 3) % 7;
+        if (wd < 0) wd += 7;
+        if (mode == FDX_FLAGS_NOTEBOOK) {
+            weekend[i] = wd >= 5;
+            night[i] = hour <= 6;
+        } else {
+            int64_t dow = ((wd + 1) % 7) + 1;
+            weekend[i] = dow >= 5;
+            night[i] = hour >= 20;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ customer windows
+struct WinArgs {
+    int64_t w[FDX_MAX_WINDOWS];
+};
+
+// pandas roll_sum state (aggregations.pyx add_sum/remove_sum/calc_sum), emulated exactly.
+struct RollSum {
+    double sum, c_add, c_rem, prev;
+    int32_t nobs, nsame;
+
+    __device__ __forceinline__ void reset(double first) {
+        sum = 0.0; c_add = 0.0; c_rem = 0.0; prev = first; nobs = 0; nsame = 0;
+    }
+    __device__ __forceinline__ void add(double v) {
+        if (v == v) {
+            nobs += 1;
+            double y = v - c_add;
+            double t = sum + y;
+            c_add = (t - sum) - y;
+            sum = t;
+            nsame = (v == prev) ? nsame + 1 : 1;
+            prev = v;
+        }
+    }
+    __device__ __forceinline__ void remove(double v) {
+        if (v == v) {
+            nobs -= 1;
+            double y = -v - c_rem;
+            double t = sum + y;
+            c_rem = (t - sum) - y;
+            sum = t;
+        }
+    }
+    // calc_sum with min_periods = 1 (offset windows)
+    __device__ __forceinline__ double value() const {
+        if (nobs >= 1) return (nsame >= nobs) ? prev * (double)nobs : sum;
+        return __builtin_nan("");
+    }
+};
+
+// One lane per (segment, window).  The lane walks its segment in time order with a tail
+// pointer, reproducing pandas' variable-window bounds (closed='right': rows j <= i with
+// t_j > t_i - w) and its add/remove/reset schedule, so the sums are bit-identical.
+// Lanes k*W .. k*W+W-1 share segment k, so their row loads hit the same cache lines.
+__global__ void __launch_bounds__(256) k_customer_exact(
+    const int64_t *__restrict__ ts, const double *__restrict__ amount,
+    const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, WinArgs win, int32_t n_win,
+    int32_t *__restrict__ nb_out, double *__restrict__ avg_out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t seg = gid / n_win;
+    if (seg >= n_seg) return;
+    const int wi = (int)(gid - seg * n_win);
+    const int64_t W = win.w[wi];
+    const int64_t b = seg_off[seg], e = seg_off[seg + 1];
+    int32_t *nb = nb_out + (int64_t)wi * n;
+    double *avg = avg_out + (int64_t)wi * n;
+
+    RollSum s;
+    int64_t tail = b;
+    for (int64_t i = b; i < e; ++i) {
+        const int64_t t = ts[i];
+        const double v = amount[i];
+        if (i == b) {
+            s.reset(v);
+            s.add(v);
+        } else {
+            const int64_t bound = t - W;
+            int64_t nt = tail;
+            while (nt < i && ts[nt] <= bound) ++nt;
+            if (nt >= i) {  // start[i] >= end[i-1]: pandas re-initialises the window
+                s.reset(v);
+                s.add(v);
+            } else {
+                for (int64_t j = tail; j < nt; ++j) s.remove(amount[j]);
+                s.add(v);
+            }
+            tail = nt;
+        }
+        const double sum = s.value();
+        nb[i] = s.nobs;
+        avg[i] = sum / (double)s.nobs;
+    }
+}
+
+// ------------------------------------------------------------------ terminal windows
+constexpr int kTermBlock = 256;
+constexpr int kTermWaves = kTermBlock / kWave;
+constexpr int kTermLdsRows = 1024;  // rows of one segment staged per wave (12 KB)
+
+// number of entries of a[lo, hi) that are <= x (a sorted ascending); returns index
+template <typename P>
+__device__ __forceinline__ int64_t upper_bound(P a, int64_t lo, int64_t hi, int64_t x) {
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        int u = __shfl_up(v, d, kWave);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+// One wave per segment (grid-stride over segments).  Closed form of the reference's
+// rolling(delay+w) - rolling(delay) (bitwise-identical, tie-order independent because
+// every counted row is strictly older than the current one):
+//   hi   = #rows with t <= t_i - delay,  lo_w = #rows with t <= t_i - delay - w
+//   NB_w = hi - lo_w,  FRAUD_w = F[hi] - F[lo_w]  (F = prefix count of fraud rows)
+//   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
+// Segments up to kTermLdsRows rows are staged in LDS (timestamps + prefix counts) with
+// coalesced loads; longer ones are searched in global memory (L2) instead.
+__global__ void __launch_bounds__(kTermBlock) k_terminal(
+    const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud,
+    const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
+    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out) {
+    __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
+    __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
+    const int64_t nwaves = (int64_t)gridDim.x * kTermWaves;
+    int64_t *lts = s_ts[wv];
+    int32_t *lf = s_f[wv];
+
+    for (int64_t seg = gwave; seg < n_seg; seg += nwaves) {
+        const int64_t b = seg_off[seg], e = seg_off[seg + 1];
+        const int64_t L = e - b;
+        if (L <= 0) continue;
+        if (L <= kTermLdsRows) {
+            int carry = 0;
+            if (lane == 0) lf[0] = 0;
+            for (int64_t c = 0; c < L; c += kWave) {
+                const int64_t j = c + lane;
+                int f = 0;
+                if (j < L) {
+                    lts[j] = ts[b + j];
+                    f = fraud[b + j] != 0;
+                }
+                int inc = wave_incl_scan(f, lane) + carry;
+                if (j < L) lf[j + 1] = inc;
+                carry = __shfl(inc, kWave - 1, kWave);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int64_t i = lane; i < L; i += kWave) {
+                const int64_t t = lts[i];
+                const int64_t hi = upper_bound(lts, 0, i, t - delay);
+                const int32_t fhi = lf[hi];
+                for (int w = 0; w < n_win; ++w) {
+                    const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
+                    const int32_t cnt = (int32_t)(hi - lo);
+                    const int32_t fr = fhi - lf[lo];
+                    nb_out[(int64_t)w * n + b + i] = cnt;
+                    risk_out[(int64_t)w * n + b + i] = cnt > 0 ? (double)fr / (double)cnt : 0.0;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            const int64_t *gts = ts + b;
+            const uint8_t *gf = fraud + b;
+            for (int64_t i = lane; i < L; i += kWave) {
+                const int64_t t = gts[i];
+                const int64_t hi = upper_bound(gts, 0, i, t - delay);
+                for (int w = 0; w < n_win; ++w) {
+                    const int64_t lo = upper_bound(gts, 0, hi, t - delay - win.w[w]);
+                    int32_t fr = 0;
+                    for (int64_t j = lo; j < hi; ++j) fr += gf[j] != 0;
+                    const int32_t cnt = (int32_t)(hi - lo);
+                    nb_out[(int64_t)w * n + b + i] = cnt;
+                    risk_out[(int64_t)w * n + b + i] = cnt > 0 ? (double)fr / (double)cnt : 0.0;
+                }
+            }
+        }
+    }
+}
+
+// X[r][0..2] = amount, weekend, night (rows already in output order)
+__global__ void __launch_bounds__(256) k_assemble_time(const double *__restrict__ amount,
+                                                       const uint8_t *__restrict__ weekend,
+                                                       const uint8_t *__restrict__ night, int64_t n,
+                                                       double *__restrict__ X, int64_t ld) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        double *x = X + r * ld;
+        x[0] = amount[r];
+        x[1] = (double)weekend[r];
+        x[2] = (double)night[r];
+    }
+}
+
+// X[perm[i]][col0 + 2w] = nb[w][i], X[perm[i]][col0 + 2w + 1] = val[w][i]
+__global__ void __launch_bounds__(256) k_assemble_group(const int32_t *__restrict__ perm,
+                                                        const int32_t *__restrict__ nb,
+                                                        const double *__restrict__ val, int64_t n,
+                                                        int32_t n_win, double *__restrict__ X, int64_t ld,
+                                                        int32_t col0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double *x = X + (int64_t)perm[i] * ld + col0;
+        for (int w = 0; w < n_win; ++w) {
+            x[2 * w] = (double)nb[(int64_t)w * n + i];
+            x[2 * w + 1] = val[(int64_t)w * n + i];
+        }
+    }
+}
+
+int check_windows(const int64_t *window_ns, int32_t n_windows, WinArgs *wa) {
+    FDX_REQUIRE(window_ns != nullptr, "window_ns is NULL");
+    FDX_REQUIRE(n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "n_windows must be in [1, %d]",
+                FDX_MAX_WINDOWS);
+    for (int i = 0; i < FDX_MAX_WINDOWS; ++i) wa->w[i] = 0;
+    for (int i = 0; i < n_windows; ++i) {
+        FDX_REQUIRE(window_ns[i] > 0, "window %d must be > 0 ns", i);
+        wa->w[i] = window_ns[i];
+    }
+    return FDX_OK;
+}
+
+}  // namespace
+}  // namespace fdx
+
+using namespace fdx;
+
+extern "C" int fdx_time_flags(const int64_t *ts_ns_d, int64_t n, int32_t mode, uint8_t *weekend_d,
+                              uint8_t *night_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    FDX_REQUIRE(mode == FDX_FLAGS_NOTEBOOK || mode == FDX_FLAGS_SPARK, "bad flags mode %d", mode);
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_ns_d && weekend_d && night_d, "null pointer");
+    FDX_REQUIRE(((uintptr_t)weekend_d % 8) == 0 && ((uintptr_t)night_d % 8) == 0,
+                "flag outputs must be 8-byte aligned");
+    const int block = 256;
+    unsigned grid = stream_grid(ceil_div(n, 8), block);
+    hipLaunchKernelGGL(k_time_flags, dim3(grid), dim3(block), 0, as_stream(stream), ts_ns_d, n, mode,
+                       weekend_d, night_d);
+    FDX_LAUNCHED("k_time_flags");
+    return FDX_OK;
+}
+
+extern "C" int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount_d,
+                                    const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                    const int64_t *window_ns, int32_t n_windows, int32_t *nb_d,
+                                    double *avg_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_ns_d && amount_d && seg_off_d && nb_d && avg_d, "null pointer");
+    const int block = 256;
+    const int64_t lanes = n_seg * n_windows;
+    hipLaunchKernelGGL(k_customer_exact, dim3((unsigned)ceil_div(lanes, block)), dim3(block), 0,
+                       as_stream(stream), ts_ns_d, amount_d, seg_off_d, n_seg, n, wa, n_windows,
+                       nb_d, avg_d);
+    FDX_LAUNCHED("k_customer_exact");
+    return FDX_OK;
+}
+
+extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                    const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                    int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
+                                    int32_t *nb_d, double *risk_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(delay_ns > 0, "delay must be > 0 ns");
+    FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
+    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
+    hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
+                       fraud_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d);
+    FDX_LAUNCHED("k_terminal");
+    return FDX_OK;
+}
+
+extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
+                                     const uint8_t *weekend_d, const uint8_t *night_d,
+                                     const int32_t *cust_perm_d, const int32_t *cust_nb_d,
+                                     const double *cust_avg_d, const int32_t *term_perm_d,
+                                     const int32_t *term_nb_d, const double *term_risk_d, double *X_d,
+                                     int64_t ld, void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    FDX_REQUIRE(n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad n_windows");
+    FDX_REQUIRE(ld >= 3 + 4 * n_windows, "ld too small");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(amount_d && weekend_d && night_d && cust_perm_d && cust_nb_d && cust_avg_d && term_perm_d &&
+                    term_nb_d && term_risk_d && X_d,
+                "null pointer");
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = stream_grid(n, 256);
+    hipLaunchKernelGGL(k_assemble_time, dim3(grid), dim3(256), 0, st, amount_d, weekend_d, night_d, n, X_d, ld);
+    FDX_LAUNCHED("k_assemble_time");
+    hipLaunchKernelGGL(k_assemble_group, dim3(grid), dim3(256), 0, st, cust_perm_d, cust_nb_d, cust_avg_d, n,
+                       n_windows, X_d, ld, 3);
+    FDX_LAUNCHED("k_assemble_group");
+    hipLaunchKernelGGL(k_assemble_group, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d, term_risk_d, n,
+                       n_windows, X_d, ld, 3 + 2 * n_windows);
+    FDX_LAUNCHED("k_assemble_group");
+    return FDX_OK;
+}

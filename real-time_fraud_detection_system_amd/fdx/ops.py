@@ -1,0 +1,259 @@
+"""Device-tensor wrappers over the libfdx C ABI.
+
+Every function takes / returns torch tensors resident on the GPU and enqueues work on
+torch's current HIP stream (``torch.cuda.current_stream().cuda_stream`` is the
+``hipStream_t`` passed to the C ABI).  PyTorch is used only for device memory and
+streams; all arithmetic happens in the HIP kernels of libfdx.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import FdxError, check
+
+NS_PER_DAY = 86_400 * 1_000_000_000
+
+
+def require_gpu() -> torch.device:
+    if not torch.cuda.is_available():
+        raise FdxError("fdx requires a ROCm GPU (MI355X); no CPU fallback exists")
+    _lib.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _s(stream=None) -> int:
+    return (stream or torch.cuda.current_stream()).cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _dev(t: torch.Tensor, dtype, name):
+    if t.device.type != "cuda":
+        raise FdxError(f"{name} must be a GPU tensor")
+    if t.dtype != dtype:
+        raise FdxError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise FdxError(f"{name} must be contiguous")
+    return t
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def key_bits_for(n_keys: int) -> int:
+    return max(int(n_keys) - 1, 0).bit_length()
+
+
+# ----------------------------------------------------------------------------- flags
+def time_flags(ts_ns: torch.Tensor, mode: int = _lib.FDX_FLAGS_NOTEBOOK, stream=None):
+    _dev(ts_ns, torch.int64, "ts_ns")
+    n = ts_ns.numel()
+    pad = (n + 7) // 8 * 8
+    we = torch.empty(pad, dtype=torch.uint8, device=ts_ns.device)
+    ni = torch.empty(pad, dtype=torch.uint8, device=ts_ns.device)
+    check(_lib.load().fdx_time_flags(_ptr(ts_ns), n, mode, _ptr(we), _ptr(ni), _s(stream)), "fdx_time_flags")
+    return we[:n], ni[:n]
+
+
+# ---------------------------------------------------------------------------- re-key
+def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool = False):
+    """Stable grouping by key: returns (perm int32, seg_off int64[n_keys+1], sorted_keys|None)."""
+    _dev(keys, torch.int32, "keys")
+    n = keys.numel()
+    kb = key_bits_for(n_keys)
+    dev = keys.device
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+    sk = torch.empty(n, dtype=torch.int32, device=dev) if want_sorted_keys else None
+    L = _lib.load()
+    ws = workspace(L.fdx_rekey_workspace_size(n, kb), dev)
+    check(L.fdx_rekey(_ptr(keys), n, kb, int(n_keys), _ptr(perm), _ptr(sk), _ptr(seg), _ptr(ws),
+                      ws.numel(), _s(stream)), "fdx_rekey")
+    return perm, seg, sk
+
+
+def argsort_i64(keys: torch.Tensor, stream=None) -> torch.Tensor:
+    _dev(keys, torch.int64, "keys")
+    n = keys.numel()
+    perm = torch.empty(n, dtype=torch.int32, device=keys.device)
+    L = _lib.load()
+    ws = workspace(L.fdx_argsort_i64_workspace_size(n), keys.device)
+    check(L.fdx_argsort_i64(_ptr(keys), n, _ptr(perm), _ptr(ws), ws.numel(), _s(stream)), "fdx_argsort_i64")
+    return perm
+
+
+def is_sorted_i64(keys: torch.Tensor, stream=None) -> bool:
+    """Host-synchronising check (reads one int back)."""
+    _dev(keys, torch.int64, "keys")
+    flag = torch.empty(1, dtype=torch.int32, device=keys.device)
+    check(_lib.load().fdx_is_sorted_i64(_ptr(keys), keys.numel(), _ptr(flag), _s(stream)), "fdx_is_sorted_i64")
+    return bool(flag.item())
+
+
+def gather(src: torch.Tensor, perm: torch.Tensor, stream=None) -> torch.Tensor:
+    _dev(perm, torch.int32, "perm")
+    if not src.is_contiguous():
+        raise FdxError("src must be contiguous")
+    out = torch.empty(perm.numel(), dtype=src.dtype, device=src.device)
+    check(_lib.load().fdx_gather(_ptr(src), src.element_size(), _ptr(perm), perm.numel(), _ptr(out),
+                                 _s(stream)), "fdx_gather")
+    return out
+
+
+def scatter(src: torch.Tensor, perm: torch.Tensor, out: torch.Tensor | None = None, stream=None):
+    _dev(perm, torch.int32, "perm")
+    if out is None:
+        out = torch.empty(perm.numel(), dtype=src.dtype, device=src.device)
+    check(_lib.load().fdx_scatter(_ptr(src), src.element_size(), _ptr(perm), perm.numel(), _ptr(out),
+                                  _s(stream)), "fdx_scatter")
+    return out
+
+
+# --------------------------------------------------------------------------- windows
+def _win_ns(days: Sequence[int]):
+    days = [int(d) for d in days]
+    if not 1 <= len(days) <= _lib.MAX_WINDOWS:
+        raise FdxError(f"1..{_lib.MAX_WINDOWS} windows supported")
+    return (ctypes.c_int64 * len(days))(*[d * NS_PER_DAY for d in days])
+
+
+def customer_windows(ts_ns, amount, seg_off, windows_days=(1, 7, 30), stream=None):
+    """Grouped rows -> (nb int32 [W, n], avg float64 [W, n])."""
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(amount, torch.float64, "amount"); _dev(seg_off, torch.int64, "seg_off")
+    n = ts_ns.numel()
+    W = len(windows_days)
+    nb = torch.empty((W, n), dtype=torch.int32, device=ts_ns.device)
+    avg = torch.empty((W, n), dtype=torch.float64, device=ts_ns.device)
+    check(_lib.load().fdx_customer_windows(_ptr(ts_ns), _ptr(amount), _ptr(seg_off), seg_off.numel() - 1, n,
+                                           _win_ns(windows_days), W, _ptr(nb), _ptr(avg), _s(stream)),
+          "fdx_customer_windows")
+    return nb, avg
+
+
+def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), stream=None):
+    """Grouped rows -> (nb int32 [W, n], risk float64 [W, n])."""
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
+    n = ts_ns.numel()
+    W = len(windows_days)
+    nb = torch.empty((W, n), dtype=torch.int32, device=ts_ns.device)
+    risk = torch.empty((W, n), dtype=torch.float64, device=ts_ns.device)
+    check(_lib.load().fdx_terminal_windows(_ptr(ts_ns), _ptr(fraud), _ptr(seg_off), seg_off.numel() - 1, n,
+                                           int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W, _ptr(nb),
+                                           _ptr(risk), _s(stream)), "fdx_terminal_windows")
+    return nb, risk
+
+
+# ----------------------------------------------------------------------------- scale
+def standard_scale(X: torch.Tensor, mean: torch.Tensor | None, scale: torch.Tensor | None, stream=None):
+    """(X - mean) / scale in float64; X is a 2-D float64 GPU tensor (any strides)."""
+    if X.dtype != torch.float64 or X.dim() != 2 or X.device.type != "cuda":
+        raise FdxError("X must be a 2-D float64 GPU tensor")
+    n, nf = X.shape
+    out = torch.empty((n, nf), dtype=torch.float64, device=X.device)
+    check(_lib.load().fdx_standard_scale(_ptr(X), n, nf, X.stride(0), X.stride(1), _ptr(mean), _ptr(scale),
+                                         _ptr(out), out.stride(0), out.stride(1), _s(stream)),
+          "fdx_standard_scale")
+    return out
+
+
+# ---------------------------------------------------------------------------- forest
+class Forest:
+    """A tree ensemble uploaded to the GPU (immutable; share it across streams)."""
+
+    def __init__(self, arrays: dict, n_features: int, mean=None, scale=None, stream=None):
+        require_gpu()
+        a = {
+            "node_offsets": np.ascontiguousarray(arrays["node_offsets"], np.int64),
+            "children_left": np.ascontiguousarray(arrays["left"], np.int64),
+            "children_right": np.ascontiguousarray(arrays["right"], np.int64),
+            "feature": np.ascontiguousarray(arrays["feature"], np.int64),
+            "threshold": np.ascontiguousarray(arrays["threshold"], np.float64),
+            "missing_go_to_left": np.ascontiguousarray(arrays["missing_left"], np.uint8),
+            "value1": np.ascontiguousarray(arrays["value1"], np.float64),
+        }
+        self._keep = a
+        self.n_trees = len(a["node_offsets"]) - 1
+        self.n_features = int(n_features)
+        m = None if mean is None else np.ascontiguousarray(mean, np.float64)
+        s = None if scale is None else np.ascontiguousarray(scale, np.float64)
+        self._keep_scaler = (m, s)
+        pp = lambda x: None if x is None else x.ctypes.data
+        desc = _lib.ForestDesc(self.n_trees, self.n_features, pp(a["node_offsets"]), pp(a["children_left"]),
+                               pp(a["children_right"]), pp(a["feature"]), pp(a["threshold"]),
+                               pp(a["missing_go_to_left"]), pp(a["value1"]), pp(m), pp(s))
+        h = ctypes.c_void_p()
+        L = _lib.load()
+        check(L.fdx_forest_create(ctypes.byref(desc), ctypes.byref(h), _s(stream)), "fdx_forest_create")
+        self._h = h
+        nt, nf, nn, nc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+        check(L.fdx_forest_info(h, ctypes.byref(nt), ctypes.byref(nf), ctypes.byref(nn), ctypes.byref(nc)))
+        self.n_nodes, self.n_chunks = nn.value, nc.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib._lib.fdx_forest_destroy(h)
+            self._h = None
+
+    def workspace_size(self, n: int) -> int:
+        return int(_lib.load().fdx_forest_workspace_size(self._h, int(n)))
+
+    def predict(self, X: torch.Tensor, want_leaves: bool = False, ws: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, stream=None):
+        """X: float64 GPU tensor [n, n_features] (any strides).  Returns proba (and leaves)."""
+        if X.dtype != torch.float64 or X.dim() != 2 or X.device.type != "cuda":
+            raise FdxError("X must be a 2-D float64 GPU tensor")
+        n, nf = X.shape
+        if nf != self.n_features:
+            raise FdxError(f"X has {nf} features, forest expects {self.n_features}")
+        proba = out if out is not None else torch.empty(n, dtype=torch.float64, device=X.device)
+        leaves = torch.empty((n, self.n_trees), dtype=torch.int32, device=X.device) if want_leaves else None
+        need = self.workspace_size(n)
+        if ws is None or ws.numel() < need:
+            ws = workspace(need, X.device)
+        check(_lib.load().fdx_forest_predict(self._h, _ptr(X), n, X.stride(0), X.stride(1), _ptr(proba),
+                                             _ptr(leaves), _ptr(ws), ws.numel(), _s(stream)),
+              "fdx_forest_predict")
+        return (proba, leaves) if want_leaves else proba
+
+
+def forest_prepare(forest: "Forest", X: torch.Tensor, ws: torch.Tensor, stream=None):
+    n = X.shape[0]
+    check(_lib.load().fdx_forest_prepare(forest._h, _ptr(X), n, X.stride(0), X.stride(1), _ptr(ws), ws.numel(),
+                                         _s(stream)), "fdx_forest_prepare")
+
+
+def forest_traverse(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, stream=None):
+    check(_lib.load().fdx_forest_traverse(forest._h, n, _ptr(out), None, _ptr(ws), ws.numel(), _s(stream)),
+          "fdx_forest_traverse")
+    return out
+
+
+def forest_arrays_from_sklearn(model) -> dict:
+    """sklearn DecisionTreeClassifier / RandomForestClassifier -> concatenated node arrays."""
+    ests = getattr(model, "estimators_", None)
+    if ests is None:
+        ests = [model]
+    left, right, feat, thr, ml, val, off = [], [], [], [], [], [], [0]
+    for e in ests:
+        t = e.tree_
+        if t.n_outputs != 1 or int(np.max(t.n_classes)) != 2:
+            raise _lib.FdxUnsupported("only single-output binary classifiers are supported")
+        left.append(t.children_left.astype(np.int64))
+        right.append(t.children_right.astype(np.int64))
+        feat.append(t.feature.astype(np.int64))
+        thr.append(t.threshold.astype(np.float64))
+        ml.append(np.asarray(t.missing_go_to_left, dtype=np.uint8))
+        val.append(np.ascontiguousarray(t.value[:, 0, 1], dtype=np.float64))
+        off.append(off[-1] + t.node_count)
+    return dict(left=np.concatenate(left), right=np.concatenate(right), feature=np.concatenate(feat),
+                threshold=np.concatenate(thr), missing_left=np.concatenate(ml), value1=np.concatenate(val),
+                node_offsets=np.asarray(off, np.int64))

@@ -1,0 +1,109 @@
+"""Whole-table featurize (+ score) pipeline on device tensors.
+
+One call replaces the notebook's whole featurization sequence
+(feature_transformation.ipynb:278, :319, :1092-1093, :2435-2436) and, with a forest, the
+scoring UDF body (pyspark/scripts/fraud_detection.py:183-195):
+
+    flags -> re-key by CUSTOMER_ID -> customer windows -> re-key by TERMINAL_ID
+          -> terminal windows -> assemble the 15 input_features -> scale + forest
+
+Input rows are in time order (the reference's order: read_from_files sorts by
+TRANSACTION_ID, which the generator assigns in TX_DATETIME order,
+shared_functions.py:74-90, data_generator.ipynb:1364-1369); ``time_sort=True`` first
+sorts them on the GPU.  All outputs are returned in input row order.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib, ops
+from ._lib import check
+
+
+@dataclass
+class Features:
+    weekend: torch.Tensor        # uint8 [n]
+    night: torch.Tensor          # uint8 [n]
+    cust_perm: torch.Tensor      # int32 [n] grouped position -> row
+    cust_seg: torch.Tensor       # int64 [n_customers+1]
+    cust_nb: torch.Tensor        # int32 [W, n] grouped order
+    cust_avg: torch.Tensor       # float64 [W, n] grouped order
+    term_perm: torch.Tensor
+    term_seg: torch.Tensor
+    term_nb: torch.Tensor        # int32 [W, n] grouped order
+    term_risk: torch.Tensor      # float64 [W, n] grouped order
+    X: Optional[torch.Tensor] = None  # float64 [n, ld] input_features in row order
+
+
+class FraudPipeline:
+    def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
+                 flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None):
+        self.windows_days = tuple(int(w) for w in windows_days)
+        self.delay_days = int(delay_days)
+        self.flags_mode = flags_mode
+        self.forest = forest
+        self.n_features = 3 + 4 * len(self.windows_days)
+        self._ws = None
+
+    def featurize(self, ts_ns, customer, terminal, amount, fraud, n_customers: int, n_terminals: int,
+                  assemble: bool = True, time_sort: bool = False, stream=None) -> Features:
+        """ts_ns int64, customer/terminal int32 (dense ids in [0, n_*)), amount float64,
+        fraud uint8 -- all GPU tensors of length n in time order (see time_sort)."""
+        if time_sort:
+            tperm = ops.argsort_i64(ts_ns, stream)
+            f = self.featurize(ops.gather(ts_ns, tperm, stream), ops.gather(customer, tperm, stream),
+                               ops.gather(terminal, tperm, stream), ops.gather(amount, tperm, stream),
+                               ops.gather(fraud, tperm, stream), n_customers, n_terminals, False,
+                               False, stream)
+            f = _to_caller_order(f, tperm, stream)
+            if assemble:
+                f.X = self.assemble(f, amount, stream)
+            return f
+        n = ts_ns.numel()
+        we, ni = ops.time_flags(ts_ns, self.flags_mode, stream)
+        cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
+        cnb, cavg = ops.customer_windows(ops.gather(ts_ns, cperm, stream), ops.gather(amount, cperm, stream),
+                                         cseg, self.windows_days, stream)
+        tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
+        tnb, trisk = ops.terminal_windows(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
+                                          tseg, self.delay_days, self.windows_days, stream)
+        f = Features(we, ni, cperm, cseg, cnb, cavg, tperm, tseg, tnb, trisk)
+        if assemble:
+            f.X = self.assemble(f, amount, stream)
+        return f
+
+    def assemble(self, f: Features, amount: torch.Tensor, stream=None) -> torch.Tensor:
+        n = amount.numel()
+        ld = 16 if self.n_features <= 16 else self.n_features
+        X = torch.empty((n, ld), dtype=torch.float64, device=amount.device)
+        W = len(self.windows_days)
+        p = ops._ptr
+        check(_lib.load().fdx_assemble_features(n, W, p(amount), p(f.weekend), p(f.night), p(f.cust_perm),
+                                                p(f.cust_nb), p(f.cust_avg), p(f.term_perm), p(f.term_nb),
+                                                p(f.term_risk), p(X), ld, ops._s(stream)),
+              "fdx_assemble_features")
+        return X[:, : self.n_features]
+
+    def score(self, X: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        if self.forest is None:
+            raise _lib.FdxError("FraudPipeline has no forest")
+        need = self.forest.workspace_size(X.shape[0])
+        if self._ws is None or self._ws.numel() < need or self._ws.device != X.device:
+            self._ws = ops.workspace(need, X.device)
+        return self.forest.predict(X, ws=self._ws, out=out, stream=stream)
+
+    def run(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, stream=None):
+        f = self.featurize(ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, True,
+                           False, stream)
+        return f, self.score(f.X, stream=stream)
+
+
+def _to_caller_order(f: Features, tperm: torch.Tensor, stream) -> Features:
+    """Outputs computed on time-sorted rows -> the caller's row order (tperm[j] = caller row
+    of sorted row j).  Grouped outputs keep their order; only the perms are composed."""
+    return Features(ops.scatter(f.weekend, tperm, stream=stream), ops.scatter(f.night, tperm, stream=stream),
+                    ops.gather(tperm, f.cust_perm, stream), f.cust_seg, f.cust_nb, f.cust_avg,
+                    ops.gather(tperm, f.term_perm, stream), f.term_seg, f.term_nb, f.term_risk)

@@ -1,0 +1,122 @@
+"""The C ABI surface (no GPU): libfdx.so loads, exports exactly what include/fdx.h
+declares, the ctypes signatures cover every declaration, and host-only entry points work."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "fdx.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fdx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("fdx_customer_windows", "fdx_terminal_windows", "fdx_rekey", "fdx_forest_predict",
+                 "fdx_time_flags", "fdx_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from fdx import _lib
+
+    L = _lib.load()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert set(_lib.SIGNATURES) == set(declared_functions())
+    assert L.fdx_abi_version() == 1
+
+
+def test_error_path_without_gpu():
+    from fdx import _lib
+
+    L = _lib.load()
+    rc = L.fdx_customer_windows(None, None, None, 1, 1, None, 0, None, None, None)
+    assert rc == -1
+    assert b"window" in L.fdx_last_error()
+    assert L.fdx_rekey_workspace_size(1000, 16) > 0
+
+
+def _pack(z):
+    from fdx import _lib
+
+    L = _lib.load()
+    a = {k: np.ascontiguousarray(z[k]) for k in ("node_offsets", "left", "right", "feature", "threshold",
+                                                  "missing_left", "value1")}
+    nt = len(a["node_offsets"]) - 1
+    total = int(a["node_offsets"][-1])
+    desc = _lib.ForestDesc(nt, 15, a["node_offsets"].ctypes.data, a["left"].ctypes.data,
+                           a["right"].ctypes.data, a["feature"].ctypes.data, a["threshold"].ctypes.data,
+                           a["missing_left"].ctypes.data, a["value1"].ctypes.data, None, None)
+    nodes = np.zeros(total, np.uint64)
+    orig = np.zeros(total, np.int32)
+    root = np.zeros(nt, np.int32)
+    rc = L.fdx_forest_pack(ctypes.byref(desc), nodes.ctypes.data, orig.ctypes.data, root.ctypes.data)
+    assert rc == 0, L.fdx_last_error()
+    return nodes, orig, root
+
+
+def _walk_packed(nodes, orig, root, z32):
+    """numpy model of the kernel's traversal over the packed nodes (float32 compares)."""
+    n, nt = z32.shape[0], len(root)
+    acc = np.zeros(n)
+    leaves = np.zeros((n, nt), np.int32)
+    hi = (nodes >> np.uint64(32)).astype(np.uint32)
+    thr = (nodes & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32)
+    vals = nodes.view(np.float64)
+    for t in range(nt):
+        p = np.full(n, root[t], np.int64)
+        while True:
+            h = hi[p]
+            internal = (h & 0x80000000) != 0
+            if not internal.any():
+                break
+            f = ((h >> 25) & 31).astype(np.int64)
+            x = z32[np.arange(n), np.minimum(f, z32.shape[1] - 1)]
+            left = np.where(np.isnan(x), (h >> 30) & 1, x <= thr[p]).astype(bool)
+            rel = (h & 0x1FFFFFF).astype(np.int64)
+            p = np.where(internal, np.where(left, p + 1, p + rel), p)
+        acc = acc + vals[p]
+        leaves[:, t] = orig[p]
+    return acc / nt, leaves
+
+
+@pytest.mark.parametrize("name", ["forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"])
+def test_forest_packing_reproduces_sklearn(golden, name):
+    """Round-toward--inf float32 thresholds + packed pre-order layout give sklearn's exact
+    leaves and probabilities (checked on the host with a numpy walk of the packed nodes)."""
+    z = golden(name)
+    nodes, orig, root = _pack(z)
+    z32 = ((z["X"] - z["mean"]) / z["scale"]).astype(np.float32)
+    proba, leaves = _walk_packed(nodes, orig, root, z32)
+    np.testing.assert_array_equal(leaves, z["leaves"])
+    np.testing.assert_array_equal(proba, z["proba"])
+
+
+def test_threshold_round_down_edge_cases():
+    """x32 <= thr64  <=>  x32 <= round_down_f32(thr64) for thresholds between floats."""
+    from fdx import _lib
+
+    thr = np.array([0.1, -0.1, 1e-40, -1e-40, 3.4e38, 1.0, 0.5 + 2**-30, -2.5 - 2**-40], np.float64)
+    n = len(thr)
+    z = dict(node_offsets=np.arange(0, 3 * n + 1, 3, dtype=np.int64),
+             left=np.tile(np.array([1, -1, -1], np.int64), n), right=np.tile(np.array([2, -1, -1], np.int64), n),
+             feature=np.zeros(3 * n, np.int64), threshold=np.repeat(thr, 3), missing_left=np.zeros(3 * n, np.uint8),
+             value1=np.tile(np.array([0.0, 1.0, 0.0]), n))
+    nodes, orig, root = _pack(z)
+    cand = np.concatenate([np.nextafter(thr.astype(np.float32), np.float32(np.inf)), thr.astype(np.float32),
+                           np.nextafter(thr.astype(np.float32), np.float32(-np.inf))])
+    z32 = np.zeros((len(cand), 15), np.float32)
+    z32[:, 0] = cand
+    proba, leaves = _walk_packed(nodes, orig, root, z32)
+    expect = np.stack([(cand.astype(np.float64) <= t) for t in thr], axis=1)  # left leaf = node 1
+    np.testing.assert_array_equal(leaves == 1, expect)
+    _ = _lib

@@ -1,0 +1,260 @@
+"""HIP kernels (through the C ABI) vs the CPU oracle and the reference's golden vectors.
+
+Bar: bit-exact for counts, flags, permutations, leaf ids; float64 averages / risks /
+probabilities are also required bit-exact here (the kernels emulate pandas' Kahan
+roll_sum and sklearn's float32 traversal exactly), which is stricter than the 1e-6
+relative tolerance north_star allows.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from fdx import ops
+from fdx.pipeline import FraudPipeline
+
+pytestmark = pytest.mark.gpu
+
+DAY = 86_400 * 10**9
+HOUR = 3600 * 10**9
+
+
+def T(a, dtype, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device=dev, dtype=dtype)
+
+
+# ----------------------------------------------------------------------------- flags
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 1000, 100_003])
+def test_time_flags(dev, n):
+    rng = np.random.default_rng(n)
+    ts = rng.integers(-400 * DAY, 20_000 * DAY, size=n, dtype=np.int64)
+    if n >= 8:  # hour / day boundaries
+        ts[:4] = [0, 7 * HOUR - 1, 7 * HOUR, 20 * HOUR]
+        ts[4:8] = [-1, -DAY, 6 * HOUR + 59 * 60 * 10**9, DAY - 1]
+    for mode, wf, nf in ((0, oracle.weekend_flag, oracle.night_flag),
+                         (1, oracle.spark_weekend_flag, oracle.spark_night_flag)):
+        we, ni = ops.time_flags(T(ts, torch.int64, dev), mode)
+        np.testing.assert_array_equal(we.cpu().numpy(), wf(ts))
+        np.testing.assert_array_equal(ni.cpu().numpy(), nf(ts))
+
+
+# ---------------------------------------------------------------------------- re-key
+@pytest.mark.parametrize("n,n_keys", [(0, 5), (1, 1), (5000, 1), (4096, 256), (4097, 257),
+                                      (100_000, 50_000), (300_001, 100_000), (2_000_000, 1 << 21)])
+def test_rekey_stable(dev, n, n_keys):
+    rng = np.random.default_rng(n + n_keys)
+    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
+    perm, seg, sk = ops.rekey(T(keys, torch.int32, dev), n_keys, want_sorted_keys=True)
+    ref = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(perm.cpu().numpy(), ref)
+    np.testing.assert_array_equal(sk.cpu().numpy(), keys[ref])
+    np.testing.assert_array_equal(seg.cpu().numpy(), np.r_[0, np.cumsum(np.bincount(keys, minlength=n_keys))])
+
+
+def test_argsort_i64_and_perm_ops(dev):
+    rng = np.random.default_rng(3)
+    k = rng.integers(-(1 << 62), 1 << 62, size=200_001, dtype=np.int64)
+    k[::7] = k[0]  # ties
+    perm = ops.argsort_i64(T(k, torch.int64, dev)).cpu().numpy()
+    np.testing.assert_array_equal(perm, np.argsort(k, kind="stable"))
+    assert not ops.is_sorted_i64(T(k, torch.int64, dev))
+    assert ops.is_sorted_i64(T(np.sort(k), torch.int64, dev))
+    p = rng.permutation(len(k)).astype(np.int32)
+    for dt, tdt in ((np.int64, torch.int64), (np.int32, torch.int32), (np.uint8, torch.uint8)):
+        src = k.astype(dt)
+        g = ops.gather(T(src, tdt, dev), T(p, torch.int32, dev)).cpu().numpy()
+        np.testing.assert_array_equal(g, src[p])
+        s = ops.scatter(T(src, tdt, dev), T(p, torch.int32, dev)).cpu().numpy()
+        exp = np.empty_like(src)
+        exp[p] = src
+        np.testing.assert_array_equal(s, exp)
+
+
+# --------------------------------------------------------------------------- windows
+def _gpu_customer(dev, ts, amount, seg, windows=(1, 7, 30)):
+    nb, avg = ops.customer_windows(T(ts, torch.int64, dev), T(amount, torch.float64, dev),
+                                   T(seg, torch.int64, dev), windows)
+    return nb.cpu().numpy(), avg.cpu().numpy()
+
+
+def _gpu_terminal(dev, ts, fraud, seg, delay=7, windows=(1, 7, 30)):
+    nb, risk = ops.terminal_windows(T(ts, torch.int64, dev), T(fraud, torch.uint8, dev),
+                                    T(seg, torch.int64, dev), delay, windows)
+    return nb.cpu().numpy(), risk.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["tiny_a.npz", "tiny_b.npz"])
+def test_windows_match_reference_golden(dev, golden, name):
+    z = golden(name)
+    o = np.argsort(z["TRANSACTION_ID"], kind="stable")
+    cols = {k: z[k][o] for k in z.files}
+    order, seg = oracle.group_order(cols["CUSTOMER_ID"], cols["TX_DATETIME"])
+    nb, avg = _gpu_customer(dev, cols["TX_DATETIME"][order], cols["TX_AMOUNT"][order], seg)
+    for k, w in enumerate((1, 7, 30)):
+        np.testing.assert_array_equal(nb[k], cols[f"CUSTOMER_ID_NB_TX_{w}DAY_WINDOW"][order])
+        np.testing.assert_array_equal(avg[k], cols[f"CUSTOMER_ID_AVG_AMOUNT_{w}DAY_WINDOW"][order])
+    order, seg = oracle.group_order(cols["TERMINAL_ID"], cols["TX_DATETIME"])
+    nb, risk = _gpu_terminal(dev, cols["TX_DATETIME"][order], cols["TX_FRAUD"][order].astype(np.uint8), seg)
+    for k, w in enumerate((1, 7, 30)):
+        np.testing.assert_array_equal(nb[k], cols[f"TERMINAL_ID_NB_TX_{w}DAY_WINDOW"][order])
+        np.testing.assert_array_equal(risk[k], cols[f"TERMINAL_ID_RISK_{w}DAY_WINDOW"][order])
+
+
+def test_customer_windows_ties_reference_order(dev, golden):
+    z = golden("ties.npz")
+    order = np.lexsort((z["CUSTOMER_ID_NB_TX_1DAY_WINDOW"], z["TX_DATETIME"], z["CUSTOMER_ID"]))
+    sk = z["CUSTOMER_ID"][order]
+    seg = np.r_[np.flatnonzero(np.r_[True, sk[1:] != sk[:-1]]), len(sk)]
+    nb, avg = _gpu_customer(dev, z["TX_DATETIME"][order], z["TX_AMOUNT"][order], seg)
+    for k, w in enumerate((1, 7, 30)):
+        np.testing.assert_array_equal(nb[k], z[f"CUSTOMER_ID_NB_TX_{w}DAY_WINDOW"][order])
+        np.testing.assert_array_equal(avg[k], z[f"CUSTOMER_ID_AVG_AMOUNT_{w}DAY_WINDOW"][order])
+
+
+def _edge_segments(rng, n_seg, max_len):
+    """Segments with ties, gaps exactly equal to the windows, repeated amounts, empties."""
+    ts_all, amt_all, fr_all, seg = [], [], [], [0]
+    for s in range(n_seg):
+        L = int(rng.integers(0, max_len + 1)) if s % 17 else (0 if s % 2 else 1)
+        t0 = int(rng.integers(0, 400)) * DAY
+        steps = rng.choice([0, 1, HOUR, DAY, 7 * DAY, 8 * DAY, 14 * DAY, 30 * DAY, 37 * DAY,
+                            int(rng.integers(1, 3 * DAY))], size=L, p=[.1, .02, .1, .1, .05, .03, .03,
+                                                                        .03, .04, .5])
+        ts = t0 + np.cumsum(steps)
+        amt = np.round(rng.gamma(2.0, 40.0, size=L), 2)
+        if s % 5 == 0:
+            amt[:] = 12.34  # n-consecutive-equal-values branch of roll_sum
+        elif s % 5 == 1:
+            amt[rng.random(L) < 0.5] = 7.0
+        ts_all.append(ts); amt_all.append(amt); fr_all.append((rng.random(L) < 0.3).astype(np.uint8))
+        seg.append(seg[-1] + L)
+    return (np.concatenate(ts_all).astype(np.int64), np.concatenate(amt_all), np.concatenate(fr_all),
+            np.asarray(seg, np.int64))
+
+
+@pytest.mark.parametrize("max_len", [3, 300, 2500])
+def test_windows_random_edge_cases(dev, max_len):
+    rng = np.random.default_rng(max_len)
+    ts, amt, fr, seg = _edge_segments(rng, 400 if max_len < 1000 else 40, max_len)
+    for windows in ((1, 7, 30), (2, 5)):
+        nb, avg = _gpu_customer(dev, ts, amt, seg, windows)
+        onb, oavg = oracle.customer_windows(ts, amt, seg, windows)
+        np.testing.assert_array_equal(nb, onb)
+        np.testing.assert_array_equal(avg, oavg)
+        nb, risk = _gpu_terminal(dev, ts, fr, seg, 7, windows)
+        onb, orisk = oracle.terminal_windows(ts, fr, seg, 7, windows)
+        np.testing.assert_array_equal(nb, onb)
+        np.testing.assert_array_equal(risk, orisk)
+
+
+# ---------------------------------------------------------------------------- forest
+def _forest(golden_z):
+    return {k: golden_z[k] for k in ("left", "right", "feature", "threshold", "missing_left", "value1",
+                                     "node_offsets")}
+
+
+@pytest.mark.parametrize("name", ["forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"])
+def test_forest_matches_sklearn_golden(dev, golden, name):
+    z = golden(name)
+    f = ops.Forest(_forest(z), 15, z["mean"], z["scale"])
+    proba, leaves = f.predict(T(z["X"], torch.float64, dev), want_leaves=True)
+    np.testing.assert_array_equal(leaves.cpu().numpy(), z["leaves"])
+    np.testing.assert_array_equal(proba.cpu().numpy(), z["proba"])
+    # column-major input (Spark columns) gives the same answer
+    Xc = T(np.asfortranarray(z["X"]).T.copy(), torch.float64, dev).t()
+    np.testing.assert_array_equal(f.predict(Xc).cpu().numpy(), z["proba"])
+
+
+def random_forest(rng, n_trees, depth, n_feat=15, p_leaf=0.15):
+    """Random sklearn-layout trees (pre-order, -1 leaves) for chunking / global-path tests."""
+    L, R, F, TH, ML, V, off = [], [], [], [], [], [], [0]
+    for _ in range(n_trees):
+        left, right, feat, thr, ml, val = [], [], [], [], [], []
+
+        def build(d):
+            i = len(left)
+            left.append(-1); right.append(-1); feat.append(-2); thr.append(-2.0); ml.append(0)
+            val.append(float(rng.integers(0, 1000)) / 999.0)
+            if d < depth and (d < 2 or rng.random() > p_leaf):
+                feat[i] = int(rng.integers(0, n_feat)); thr[i] = float(rng.normal()) * 1.3
+                ml[i] = int(rng.random() < 0.5)
+                left[i] = build(d + 1)
+                right[i] = build(d + 1)
+            return i
+
+        build(0)
+        L += left; R += right; F += feat; TH += thr; ML += ml; V += val
+        off.append(off[-1] + len(left))
+    return dict(left=np.array(L, np.int64), right=np.array(R, np.int64), feature=np.array(F, np.int64),
+                threshold=np.array(TH), missing_left=np.array(ML, np.uint8), value1=np.array(V),
+                node_offsets=np.array(off, np.int64))
+
+
+@pytest.mark.parametrize("n_trees,depth", [(60, 10), (2, 15)])
+def test_forest_chunks_and_global_path(dev, n_trees, depth):
+    rng = np.random.default_rng(depth)
+    arr = random_forest(rng, n_trees, depth)
+    X = rng.normal(size=(20_000, 15))
+    X[rng.random(X.shape) < 0.01] = np.nan
+    mean, scale = rng.normal(size=15) * 0.1, rng.uniform(0.5, 2.0, size=15)
+    f = ops.Forest(arr, 15, mean, scale)
+    assert f.n_chunks >= 2
+    proba, leaves = f.predict(T(X, torch.float64, dev), want_leaves=True)
+    op, ol = oracle.forest_predict(X, arr, mean, scale, want_leaves=True)
+    np.testing.assert_array_equal(leaves.cpu().numpy(), ol)
+    np.testing.assert_array_equal(proba.cpu().numpy(), op)
+
+
+def test_standard_scale(dev, golden):
+    z = golden("forest_rf5d8.npz")
+    X = z["X"]
+    out = ops.standard_scale(T(X, torch.float64, dev), T(z["mean"], torch.float64, dev),
+                             T(z["scale"], torch.float64, dev)).cpu().numpy()
+    np.testing.assert_array_equal(out, (X - z["mean"]) / z["scale"])
+
+
+# -------------------------------------------------------------------------- pipeline
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_pipeline_matches_reference_golden(dev, golden, shuffle):
+    z = golden("tiny_a.npz")
+    o = np.argsort(z["TRANSACTION_ID"], kind="stable")
+    if shuffle:
+        o = np.random.default_rng(0).permutation(o)
+    cols = {k: z[k][o] for k in z.files}
+    pipe = FraudPipeline()
+    f = pipe.featurize(T(cols["TX_DATETIME"], torch.int64, dev), T(cols["CUSTOMER_ID"], torch.int32, dev),
+                       T(cols["TERMINAL_ID"], torch.int32, dev), T(cols["TX_AMOUNT"], torch.float64, dev),
+                       T(cols["TX_FRAUD"], torch.uint8, dev), int(cols["CUSTOMER_ID"].max()) + 1,
+                       int(cols["TERMINAL_ID"].max()) + 1, time_sort=shuffle)
+    X = f.X.cpu().numpy()
+    feats = ["TX_AMOUNT", "TX_DURING_WEEKEND", "TX_DURING_NIGHT"] + oracle.CUSTOMER_COLS + oracle.TERMINAL_COLS
+    for j, c in enumerate(feats):
+        np.testing.assert_array_equal(X[:, j], cols[c].astype(np.float64), err_msg=c)
+
+
+def test_pipeline_large_sampled_segments(dev):
+    """Full-size run (synthetic config-2-shaped data); every customer and terminal segment of
+    a random sample is re-computed by the oracle and must match bit for bit, and global
+    invariants hold for all rows."""
+    from fdx import synth
+
+    data = synth.generate(n_customers=20_000, n_terminals=40_000, nb_days=183, seed=5)
+    n = len(data["ts"])
+    pipe = FraudPipeline()
+    f = pipe.featurize(T(data["ts"], torch.int64, dev), T(data["customer"], torch.int32, dev),
+                       T(data["terminal"], torch.int32, dev), T(data["amount"], torch.float64, dev),
+                       T(data["fraud"], torch.uint8, dev), 20_000, 40_000)
+    X = f.X.cpu().numpy()
+    assert X.shape == (n, 15)
+    # invariants: every row counts itself in its customer windows; nb grows with w
+    assert (X[:, 3] >= 1).all() and (X[:, 5] >= X[:, 3]).all() and (X[:, 7] >= X[:, 5]).all()
+    assert ((X[:, 10] >= 0) & (X[:, 10] <= 1)).all()
+    rng = np.random.default_rng(1)
+    for key, cols in (("customer", slice(3, 9)), ("terminal", slice(9, 15))):
+        ids = rng.choice(int(data[key].max()) + 1, size=50, replace=False)
+        m = np.flatnonzero(np.isin(data[key], ids))
+        sub = {k: v[m] for k, v in data.items()}
+        of = oracle.featurize_arrays(sub["ts"], sub["customer"], sub["terminal"], sub["amount"], sub["fraud"])
+        names = oracle.CUSTOMER_COLS if key == "customer" else oracle.TERMINAL_COLS
+        exp = np.stack([of[c] for c in names], axis=1)
+        np.testing.assert_array_equal(X[m][:, cols], exp)
