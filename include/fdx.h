@@ -88,7 +88,9 @@ int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d, const i
  *    CUSTOMER_ID_NB_TX_w, CUSTOMER_ID_AVG_AMOUNT_w (w = each window),
  *    TERMINAL_ID_NB_TX_w, TERMINAL_ID_RISK_w (w = each window)]
  * amount/weekend/night are in output row order; the grouped outputs of
- * fdx_customer_windows / fdx_terminal_windows are scattered back through their perms. */
+ * fdx_customer_windows / fdx_terminal_windows are scattered back through their perms.
+ * The three term_* pointers may all be NULL (the multi-GPU path fills those columns with
+ * fdx_reply_assemble after the return exchange). */
 int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
                           const uint8_t *weekend_d, const uint8_t *night_d, const int32_t *cust_perm_d,
                           const int32_t *cust_nb_d, const double *cust_avg_d, const int32_t *term_perm_d,
@@ -123,6 +125,28 @@ int fdx_gather(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int
 /* dst[perm[j]] = src[j]  (inverse of fdx_gather). */
 int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n, void *dst_d,
                 void *stream);
+
+/* ---- multi-GPU re-key exchange ------------------------------------
+ * Rows are sharded by customer; the terminal windows need every row of a terminal on its
+ * owner rank, owner(t) = t % world.  Per step: fdx_key_map(MOD) -> fdx_rekey(owner) ->
+ * fdx_exchange_pack -> RCCL all-to-all (16 B/row) -> fdx_exchange_unpack (local terminal
+ * id = t / world) -> time sort + fdx_rekey -> fdx_terminal_windows -> fdx_reply_pack
+ * (records indexed by receive position) -> RCCL all-to-all back -> fdx_reply_assemble.
+ * Record layouts: exchange rec[j] = {ts, term<<32 | fraud<<31 | source row}; reply rows
+ * are ceil(W/2) words of packed int32 counts followed by W float64 risks. */
+#define FDX_KEY_MOD 0 /* out = key % param  (owner rank of a terminal)          */
+#define FDX_KEY_DIV 1 /* out = key / param  (owner-local terminal id)           */
+#define FDX_KEY_SUB 2 /* out = key - param  (shard-local customer id)           */
+int fdx_key_map(const int32_t *keys_d, int64_t n, int32_t op, int32_t param, int32_t *out_d,
+                void *stream);
+int fdx_exchange_pack(const int64_t *ts_d, const int32_t *term_d, const uint8_t *fraud_d,
+                      const int32_t *perm_d, int64_t n, int64_t *rec_d, void *stream);
+int fdx_exchange_unpack(const int64_t *rec_d, int64_t m, int32_t world, int64_t *ts_d,
+                        int32_t *term_local_d, uint8_t *fraud_d, void *stream);
+int fdx_reply_pack(const int32_t *nb_d, const double *risk_d, const int32_t *perm_d, int64_t m,
+                   int32_t n_windows, int64_t *reply_d, void *stream);
+int fdx_reply_assemble(const int64_t *reply_d, const int32_t *perm_d, int64_t n, int32_t n_windows,
+                       double *X_d, int64_t ld, int32_t col0, void *stream);
 
 /* ---- a-5 + a-7/a-8: StandardScaler + tree-ensemble predict_proba ----------------------
  * Replaces `loaded_scaler.transform(features)` + `model.predict_proba(scaled)[:, 1]`

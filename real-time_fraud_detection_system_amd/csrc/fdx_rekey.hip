@@ -362,13 +362,13 @@ extern "C" int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     FDX_REQUIRE(key_bits >= 0 && key_bits <= 31, "key_bits must be in [0, 31]");
     FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
-    FDX_REQUIRE(seg_off_d && perm_d, "null pointer");
+    FDX_REQUIRE(seg_off_d, "null seg_off");
     hipStream_t st = as_stream(stream);
     if (n == 0) {
         FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
         return FDX_OK;
     }
-    FDX_REQUIRE(keys_d, "null keys");
+    FDX_REQUIRE(keys_d && perm_d, "null keys/perm");
     SortWs<uint32_t> w;
     size_t need = sort_ws<uint32_t>(n, &w, reinterpret_cast<char *>(workspace_d));
     if (!workspace_d || workspace_bytes < need) {
@@ -424,6 +424,73 @@ extern "C" int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag
     return FDX_OK;
 }
 
+// ---- multi-GPU terminal exchange (fdx.distributed) ----------------------------------
+__global__ void k_key_map(const int32_t *__restrict__ in, int64_t n, int32_t op, int32_t param,
+                          int32_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k = in[i];
+        out[i] = op == FDX_KEY_MOD ? k % param : (op == FDX_KEY_DIV ? k / param : k - param);
+    }
+}
+
+// rec[j] = {ts[r], term[r] << 32 | fraud[r] << 31 | r}, r = perm[j] (destination-grouped)
+__global__ void k_exchange_pack(const int64_t *__restrict__ ts, const int32_t *__restrict__ term,
+                                const uint8_t *__restrict__ fraud, const int32_t *__restrict__ perm,
+                                int64_t n, int64_t *__restrict__ rec) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = perm[j];
+        rec[2 * j] = ts[r];
+        rec[2 * j + 1] = ((int64_t)term[r] << 32) | ((int64_t)(fraud[r] != 0) << 31) | (int64_t)r;
+    }
+}
+
+__global__ void k_exchange_unpack(const int64_t *__restrict__ rec, int64_t m, int32_t world,
+                                  int64_t *__restrict__ ts, int32_t *__restrict__ term_local,
+                                  uint8_t *__restrict__ fraud) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w = rec[2 * j + 1];
+        ts[j] = rec[2 * j];
+        term_local[j] = (int32_t)(w >> 32) / world;
+        fraud[j] = (uint8_t)((w >> 31) & 1);
+    }
+}
+
+// reply[perm[j]] = {nb[0..W) packed 2 per word, risk bits[0..W)}
+__global__ void k_reply_pack(const int32_t *__restrict__ nb, const double *__restrict__ risk,
+                             const int32_t *__restrict__ perm, int64_t m, int32_t W,
+                             int64_t *__restrict__ reply) {
+    const int words = (W + 1) / 2 + W;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        int64_t *o = reply + (int64_t)perm[j] * words;
+        for (int w = 0; w < W; w += 2) {
+            uint64_t lo = (uint32_t)nb[(int64_t)w * m + j];
+            uint64_t hi = (w + 1 < W) ? (uint32_t)nb[(int64_t)(w + 1) * m + j] : 0u;
+            o[w / 2] = (int64_t)(lo | (hi << 32));
+        }
+        for (int w = 0; w < W; ++w) o[(W + 1) / 2 + w] = __double_as_longlong(risk[(int64_t)w * m + j]);
+    }
+}
+
+// X[perm[j]][col0 + 2w] = nb_w, X[perm[j]][col0 + 2w + 1] = risk_w from reply records
+__global__ void k_reply_assemble(const int64_t *__restrict__ reply, const int32_t *__restrict__ perm,
+                                 int64_t n, int32_t W, double *__restrict__ X, int64_t ld, int32_t col0) {
+    const int words = (W + 1) / 2 + W;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t *r = reply + j * words;
+        double *x = X + (int64_t)perm[j] * ld + col0;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t p = (uint64_t)r[w / 2];
+            x[2 * w] = (double)(int32_t)((w & 1) ? (p >> 32) : (p & 0xFFFFFFFFu));
+            x[2 * w + 1] = __longlong_as_double(r[(W + 1) / 2 + w]);
+        }
+    }
+}
+
 template <typename T>
 static int launch_perm(bool gather, const void *src, const int32_t *perm, int64_t n, void *dst,
                        hipStream_t st) {
@@ -459,4 +526,62 @@ extern "C" int fdx_gather(const void *src_d, int32_t elem_bytes, const int32_t *
 extern "C" int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n,
                            void *dst_d, void *stream) {
     return perm_op(false, src_d, elem_bytes, perm_d, n, dst_d, stream);
+}
+
+extern "C" int fdx_key_map(const int32_t *keys_d, int64_t n, int32_t op, int32_t param, int32_t *out_d,
+                           void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    FDX_REQUIRE(op == FDX_KEY_MOD || op == FDX_KEY_DIV || op == FDX_KEY_SUB, "bad op %d", op);
+    FDX_REQUIRE(op == FDX_KEY_SUB || param >= 1, "param must be >= 1");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(keys_d && out_d, "null pointer");
+    hipLaunchKernelGGL(k_key_map, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), keys_d, n, op,
+                       param, out_d);
+    FDX_LAUNCHED("k_key_map");
+    return FDX_OK;
+}
+
+extern "C" int fdx_exchange_pack(const int64_t *ts_d, const int32_t *term_d, const uint8_t *fraud_d,
+                                 const int32_t *perm_d, int64_t n, int64_t *rec_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_d && term_d && fraud_d && perm_d && rec_d, "null pointer");
+    hipLaunchKernelGGL(k_exchange_pack, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), ts_d,
+                       term_d, fraud_d, perm_d, n, rec_d);
+    FDX_LAUNCHED("k_exchange_pack");
+    return FDX_OK;
+}
+
+extern "C" int fdx_exchange_unpack(const int64_t *rec_d, int64_t m, int32_t world, int64_t *ts_d,
+                                   int32_t *term_local_d, uint8_t *fraud_d, void *stream) {
+    FDX_REQUIRE(m >= 0 && world >= 1, "bad argument");
+    if (m == 0) return FDX_OK;
+    FDX_REQUIRE(rec_d && ts_d && term_local_d && fraud_d, "null pointer");
+    hipLaunchKernelGGL(k_exchange_unpack, dim3(stream_grid(m, 256)), dim3(256), 0, as_stream(stream), rec_d,
+                       m, world, ts_d, term_local_d, fraud_d);
+    FDX_LAUNCHED("k_exchange_unpack");
+    return FDX_OK;
+}
+
+extern "C" int fdx_reply_pack(const int32_t *nb_d, const double *risk_d, const int32_t *perm_d, int64_t m,
+                              int32_t n_windows, int64_t *reply_d, void *stream) {
+    FDX_REQUIRE(m >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
+    if (m == 0) return FDX_OK;
+    FDX_REQUIRE(nb_d && risk_d && perm_d && reply_d, "null pointer");
+    hipLaunchKernelGGL(k_reply_pack, dim3(stream_grid(m, 256)), dim3(256), 0, as_stream(stream), nb_d, risk_d,
+                       perm_d, m, n_windows, reply_d);
+    FDX_LAUNCHED("k_reply_pack");
+    return FDX_OK;
+}
+
+extern "C" int fdx_reply_assemble(const int64_t *reply_d, const int32_t *perm_d, int64_t n, int32_t n_windows,
+                                  double *X_d, int64_t ld, int32_t col0, void *stream) {
+    FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
+    FDX_REQUIRE(col0 >= 0 && col0 + 2 * n_windows <= ld, "columns out of range");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(reply_d && perm_d && X_d, "null pointer");
+    hipLaunchKernelGGL(k_reply_assemble, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), reply_d,
+                       perm_d, n, n_windows, X_d, ld, col0);
+    FDX_LAUNCHED("k_reply_assemble");
+    return FDX_OK;
 }

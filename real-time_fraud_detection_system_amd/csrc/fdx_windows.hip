@@ -364,8 +364,7 @@ extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double 
     FDX_REQUIRE(n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad n_windows");
     FDX_REQUIRE(ld >= 3 + 4 * n_windows, "ld too small");
     if (n == 0) return FDX_OK;
-    FDX_REQUIRE(amount_d && weekend_d && night_d && cust_perm_d && cust_nb_d && cust_avg_d && term_perm_d &&
-                    term_nb_d && term_risk_d && X_d,
+    FDX_REQUIRE(amount_d && weekend_d && night_d && cust_perm_d && cust_nb_d && cust_avg_d && X_d,
                 "null pointer");
     hipStream_t st = as_stream(stream);
     const unsigned grid = stream_grid(n, 256);
@@ -374,8 +373,10 @@ extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double 
     hipLaunchKernelGGL(k_assemble_group, dim3(grid), dim3(256), 0, st, cust_perm_d, cust_nb_d, cust_avg_d, n,
                        n_windows, X_d, ld, 3);
     FDX_LAUNCHED("k_assemble_group");
-    hipLaunchKernelGGL(k_assemble_group, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d, term_risk_d, n,
-                       n_windows, X_d, ld, 3 + 2 * n_windows);
-    FDX_LAUNCHED("k_assemble_group");
+    if (term_perm_d && term_nb_d && term_risk_d) {  // NULL: filled later (multi-GPU reply path)
+        hipLaunchKernelGGL(k_assemble_group, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d, term_risk_d,
+                           n, n_windows, X_d, ld, 3 + 2 * n_windows);
+        FDX_LAUNCHED("k_assemble_group");
+    }
     return FDX_OK;
 }

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libfdx.so")
 FDX_OK = 0
 FDX_FLAGS_NOTEBOOK = 0
 FDX_FLAGS_SPARK = 1
+FDX_KEY_MOD, FDX_KEY_DIV, FDX_KEY_SUB = 0, 1, 2
 MAX_WINDOWS = 8
 MAX_FEATURES = 32
 
@@ -54,6 +55,11 @@ SIGNATURES = {
     "fdx_is_sorted_i64": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_gather": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),
     "fdx_scatter": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),
+    "fdx_key_map": (ctypes.c_int, [P, c_i64, c_i32, c_i32, P, P]),
+    "fdx_exchange_pack": (ctypes.c_int, [P, P, P, P, c_i64, P, P]),
+    "fdx_exchange_unpack": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P]),
+    "fdx_reply_pack": (ctypes.c_int, [P, P, P, c_i64, c_i32, P, P]),
+    "fdx_reply_assemble": (ctypes.c_int, [P, P, c_i64, c_i32, P, c_i64, c_i32, P]),
     "fdx_standard_scale": (ctypes.c_int, [P, c_i64, c_i32, c_i64, c_i64, P, P, P, c_i64, c_i64, P]),
     "fdx_forest_create": (ctypes.c_int, [ctypes.POINTER(ForestDesc), ctypes.POINTER(P), P]),
     "fdx_forest_pack": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P]),

@@ -1,0 +1,145 @@
+"""Multi-GPU featurize + score: customer-sharded rows, one RCCL all-to-all re-key per step.
+
+SURVEY.md §8(e).  One process per GPU (torch.distributed, backend "nccl" = RCCL over
+xGMI).  Each rank owns a contiguous range of CUSTOMER_IDs and all their transactions, so
+the flags and the customer windows need no communication.  The terminal windows need all
+rows of a terminal on one rank: owner(t) = t % world.  Per step
+
+  owner keys -> stable re-key by owner -> pack {ts, term|fraud|row} (16 B/row)
+  -> all_to_all_single (splits exchanged first, 8 B per peer)
+  -> owner: unpack, time sort + re-key by local terminal id, terminal windows,
+     reply records (ceil(W/2)+W words/row) indexed by receive position
+  -> all_to_all_single back (splits mirrored) -> scatter into the local feature matrix
+  -> scale + forest locally.
+
+Ring collectives are the wrong primitive on xGMI's point-to-point links; the all-to-all
+sends 1/world of the rows to each peer over its own link.  Results are bitwise identical
+to the 1-GPU pipeline (terminal features are tie-order independent, the customer windows
+never leave their rank).
+
+The routing logic is written once against a small kernel interface so that the same code
+runs with the HIP kernels (GpuKernels, product) and -- in the CPU gloo tests only -- with
+numpy stand-ins supplied by the test.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib, ops
+from ._lib import check
+
+
+class GpuKernels:
+    """The libfdx entry points the exchange uses, on the current HIP stream."""
+
+    owner_keys = staticmethod(lambda term, world: ops.key_map(term, _lib.FDX_KEY_MOD, world))
+
+    rekey = staticmethod(lambda keys, n_keys: ops.rekey(keys, n_keys)[:2])
+    gather = staticmethod(ops.gather)
+    argsort_i64 = staticmethod(ops.argsort_i64)
+
+    @staticmethod
+    def exchange_pack(ts, term, fraud, perm):
+        rec = torch.empty((perm.numel(), 2), dtype=torch.int64, device=ts.device)
+        check(_lib.load().fdx_exchange_pack(ops._ptr(ts), ops._ptr(term), ops._ptr(fraud), ops._ptr(perm),
+                                            perm.numel(), ops._ptr(rec), ops._s()), "fdx_exchange_pack")
+        return rec
+
+    @staticmethod
+    def exchange_unpack(rec, world):
+        m = rec.shape[0]
+        ts = torch.empty(m, dtype=torch.int64, device=rec.device)
+        tl = torch.empty(m, dtype=torch.int32, device=rec.device)
+        fr = torch.empty(m, dtype=torch.uint8, device=rec.device)
+        check(_lib.load().fdx_exchange_unpack(ops._ptr(rec), m, world, ops._ptr(ts), ops._ptr(tl), ops._ptr(fr),
+                                              ops._s()), "fdx_exchange_unpack")
+        return ts, tl, fr
+
+    terminal_windows = staticmethod(ops.terminal_windows)
+
+    @staticmethod
+    def reply_pack(nb, risk, perm, W):
+        m = perm.numel()
+        words = (W + 1) // 2 + W
+        rep = torch.empty((m, words), dtype=torch.int64, device=nb.device)
+        check(_lib.load().fdx_reply_pack(ops._ptr(nb), ops._ptr(risk), ops._ptr(perm), m, W, ops._ptr(rep),
+                                         ops._s()), "fdx_reply_pack")
+        return rep
+
+    @staticmethod
+    def reply_assemble(reply, perm, W, X, col0):
+        check(_lib.load().fdx_reply_assemble(ops._ptr(reply), ops._ptr(perm), perm.numel(), W, ops._ptr(X),
+                                             X.stride(0), col0, ops._s()), "fdx_reply_assemble")
+
+
+def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
+                               delay_days=7, group=None):
+    """Runs the re-key exchange and the owner-side terminal windows.  Returns
+    (reply [n_local, words] in send order, send_perm [n_local] send position -> local row)."""
+    W = len(windows_days)
+    owner = K.owner_keys(term, world)
+    send_perm, send_seg = K.rekey(owner, world)
+    send_counts = (send_seg[1:] - send_seg[:-1]).to(torch.int64)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
+    rec = K.exchange_pack(ts, term, fraud, send_perm)
+    recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
+    dist.all_to_all_single(recv, rec, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    rts, rterm, rfr = K.exchange_unpack(recv, world)
+    n_local_terms = (n_terminals_total + world - 1) // world
+    tperm = K.argsort_i64(rts)                                  # time order (stable)
+    gperm, gseg = K.rekey(K.gather(rterm, tperm), n_local_terms)  # then by terminal (stable)
+    perm = K.gather(tperm, gperm)                               # grouped position -> receive index
+    nb, risk = K.terminal_windows(K.gather(rts, perm), K.gather(rfr, perm), gseg, delay_days, windows_days)
+    reply = K.reply_pack(nb, risk, perm, W)
+    back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
+    dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
+    return back, send_perm
+
+
+class ShardedPipeline:
+    """FraudPipeline over `world` GPUs (this process = `rank`)."""
+
+    def __init__(self, pipe, world: int, rank: int, n_terminals_total: int, customer_base: int | None = None,
+                 group=None):
+        self.pipe, self.world, self.rank = pipe, world, rank
+        self.n_terminals_total = n_terminals_total
+        self.customer_base = customer_base
+        self.group = group
+
+    def featurize(self, ts, customer, terminal, amount, fraud, n_customers_local: int):
+        """customer: global ids of this rank's customers, dense in
+        [customer_base, customer_base + n_customers_local)."""
+        p = self.pipe
+        W = len(p.windows_days)
+        we, ni = ops.time_flags(ts, p.flags_mode)
+        base = self.rank * n_customers_local if self.customer_base is None else self.customer_base
+        cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
+        cperm, cseg, _ = ops.rekey(cust, n_customers_local)
+        cnb, cavg = ops.customer_windows(ops.gather(ts, cperm), ops.gather(amount, cperm), cseg, p.windows_days)
+        n = ts.numel()
+        ld = 16 if p.n_features <= 16 else p.n_features
+        X = torch.empty((n, ld), dtype=torch.float64, device=ts.device)
+        P = ops._ptr
+        check(_lib.load().fdx_assemble_features(n, W, P(amount), P(we), P(ni), P(cperm), P(cnb), P(cavg), None,
+                                                None, None, P(X), ld, ops._s()), "fdx_assemble_features")
+        back, send_perm = exchange_terminal_features(GpuKernels, ts, terminal, fraud, self.world,
+                                                     self.n_terminals_total, p.windows_days, p.delay_days,
+                                                     self.group)
+        GpuKernels.reply_assemble(back, send_perm, W, X, 3 + 2 * W)
+        return X[:, : p.n_features]
+
+    def run(self, ts, customer, terminal, amount, fraud, n_customers_total, proba, ws, events=None):
+        n_local = n_customers_total // self.world
+        X = self.featurize(ts, customer, terminal, amount, fraud, n_local)
+        ops.forest_prepare(self.pipe.forest, X, ws)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+        ops.forest_traverse(self.pipe.forest, ts.numel(), ws, proba)
+        if events is not None:
+            b.record()
+            events.append((a, b))
+        return proba

@@ -80,6 +80,15 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
     return perm, seg, sk
 
 
+def key_map(keys: torch.Tensor, op: int, param: int, stream=None) -> torch.Tensor:
+    """MOD: key % param, DIV: key / param, SUB: key - param (int32, on the GPU)."""
+    _dev(keys, torch.int32, "keys")
+    out = torch.empty_like(keys)
+    check(_lib.load().fdx_key_map(_ptr(keys), keys.numel(), int(op), int(param), _ptr(out), _s(stream)),
+          "fdx_key_map")
+    return out
+
+
 def argsort_i64(keys: torch.Tensor, stream=None) -> torch.Tensor:
     _dev(keys, torch.int64, "keys")
     n = keys.numel()
