@@ -64,6 +64,7 @@ def main():
     # a small held-out sample with sklearn's own answers, for the bench's sanity check
     Xs = feat[feats].values[-4096:].astype(np.float64)
     Zs = scaler.transform(pd.DataFrame(Xs, columns=feats))
+    rf.set_params(n_jobs=1)  # tree-order float64 accumulation (threads add in completion order)
     np.savez_compressed(
         os.path.join(HERE, "rf100_d20.npz"),
         node_offsets=off,

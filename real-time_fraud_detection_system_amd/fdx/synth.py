@@ -16,19 +16,42 @@ START_NS = np.datetime64("2024-06-01T00:00:00", "ns").astype(np.int64)
 NS = 1_000_000_000
 
 
-def _terminals_within(cx, cy, tx, ty, r):
-    """CSR lists of terminal ids within radius r of each customer (scipy KD-tree)."""
-    from scipy.spatial import cKDTree
+class _TerminalSampler:
+    """Uniform choice among the terminals within radius r of a customer
+    (get_list_terminals_within_radius + random.choice, data_generator.ipynb:420-437, :821)
+    without materialising the per-customer lists: draw uniformly from the terminals whose x
+    lies in [cx - r, cx + r] (a contiguous range of the x-sorted terminals) and reject the
+    draws outside the disk.  Exact in distribution; scales to millions of terminals."""
 
-    tree = cKDTree(np.stack([tx, ty], axis=1))
-    lists = tree.query_ball_point(np.stack([cx, cy], axis=1), r=r - 1e-12, workers=-1)
-    lens = np.fromiter((len(x) for x in lists), dtype=np.int64, count=len(lists))
-    flat = np.fromiter((t for x in lists for t in sorted(x)), dtype=np.int64, count=int(lens.sum()))
-    return np.r_[0, np.cumsum(lens)], flat
+    def __init__(self, tx, ty, r):
+        self.order = np.argsort(tx, kind="stable")
+        self.xs, self.ys = tx[self.order], ty[self.order]
+        self.r = r
+
+    def count(self, cx, cy):
+        from scipy.spatial import cKDTree
+
+        tree = cKDTree(np.stack([self.xs, self.ys], axis=1))
+        return tree.query_ball_point(np.stack([cx, cy], axis=1), r=self.r - 1e-12, return_length=True,
+                                     workers=-1)
+
+    def sample(self, rng, px, py):
+        lo = np.searchsorted(self.xs, px - self.r, side="left")
+        hi = np.searchsorted(self.xs, px + self.r, side="right")
+        out = np.full(len(px), -1, np.int64)
+        pending = np.arange(len(px))
+        while len(pending):
+            span = hi[pending] - lo[pending]
+            cand = lo[pending] + (rng.random(len(pending)) * span).astype(np.int64)
+            dx, dy = self.xs[cand] - px[pending], self.ys[cand] - py[pending]
+            ok = np.sqrt(dx * dx + dy * dy) < self.r
+            out[pending[ok]] = self.order[cand[ok]]
+            pending = pending[~ok]
+        return out
 
 
 def generate(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, seed=0, customer_offset=0,
-             frauds=True):
+             frauds=True, terminal_seed=10_000):
     """Returns a dict of numpy arrays in global time order:
     ts (int64 ns), customer (int32), terminal (int32), amount (f64), fraud (u8), tid (int64)."""
     rng = np.random.default_rng(seed)
@@ -36,10 +59,10 @@ def generate(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, seed=0, cu
     mean_amount = rng.uniform(5, 100, n_customers)
     std_amount = mean_amount / 2
     mean_nb = rng.uniform(0, 4, n_customers)
-    trng = np.random.default_rng(10_000 + seed if customer_offset == 0 else 10_000)
+    trng = np.random.default_rng(terminal_seed)  # shared by all ranks: one terminal map
     tx, ty = trng.uniform(0, 100, n_terminals), trng.uniform(0, 100, n_terminals)
-    off, flat = _terminals_within(cx, cy, tx, ty, r)
-    has_term = (off[1:] - off[:-1]) > 0
+    sampler = _TerminalSampler(tx, ty, r)
+    has_term = sampler.count(cx, cy) > 0
 
     counts = rng.poisson(np.broadcast_to(mean_nb, (nb_days, n_customers)))  # [day, customer]
     day_idx, cust_idx = np.nonzero(counts)
@@ -53,8 +76,7 @@ def generate(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, seed=0, cu
     amount = np.round(amount, 2)
     keep = (t > 0) & (t < 86400) & has_term[cust]
     day, cust, t, amount = day[keep], cust[keep], t[keep], amount[keep]
-    nterm = off[cust + 1] - off[cust]
-    term = flat[off[cust] + (rng.random(len(cust)) * nterm).astype(np.int64)]
+    term = sampler.sample(rng, cx[cust], cy[cust])
     secs = t + day * 86400
     order = np.argsort(secs, kind="stable")
     secs, day, cust, term, amount = secs[order], day[order], cust[order], term[order], amount[order]

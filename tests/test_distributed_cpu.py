@@ -1,0 +1,140 @@
+"""World-size-2 gloo test of the multi-GPU routing (fdx.distributed) on CPU.
+
+The exchange code (owner keys, split exchange, all-to-all there and back, reply
+reassembly) runs unchanged; only the per-rank kernels are replaced by numpy/oracle
+stand-ins with the same record formats, so the test checks the distributed algorithm:
+every rank's terminal features must equal the single-process oracle over the union of
+all shards.  The HIP versions of the same kernels are covered by tests/test_gpu_*.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+
+
+class CpuKernels:
+    @staticmethod
+    def owner_keys(term, world):
+        return term % world
+
+    @staticmethod
+    def rekey(keys, n_keys):
+        k = keys.numpy()
+        perm = np.argsort(k, kind="stable").astype(np.int32)
+        seg = np.r_[0, np.cumsum(np.bincount(k, minlength=n_keys))].astype(np.int64)
+        return torch.from_numpy(perm), torch.from_numpy(seg)
+
+    @staticmethod
+    def gather(src, perm):
+        return src[perm.long()]
+
+    @staticmethod
+    def argsort_i64(keys):
+        return torch.from_numpy(np.argsort(keys.numpy(), kind="stable").astype(np.int32))
+
+    @staticmethod
+    def exchange_pack(ts, term, fraud, perm):
+        p = perm.long()
+        rec = torch.empty((len(p), 2), dtype=torch.int64)
+        rec[:, 0] = ts[p]
+        rec[:, 1] = (term[p].long() << 32) | ((fraud[p] != 0).long() << 31) | p
+        return rec
+
+    @staticmethod
+    def exchange_unpack(rec, world):
+        w = rec[:, 1]
+        return rec[:, 0].clone(), ((w >> 32).int() // world).int(), ((w >> 31) & 1).to(torch.uint8)
+
+    @staticmethod
+    def terminal_windows(ts, fraud, seg, delay_days, windows_days):
+        nb, risk = oracle.terminal_windows(ts.numpy(), fraud.numpy(), seg.numpy(), delay_days, windows_days)
+        return torch.from_numpy(nb.astype(np.int32)), torch.from_numpy(risk)
+
+    @staticmethod
+    def reply_pack(nb, risk, perm, W):
+        words = (W + 1) // 2 + W
+        rep = np.zeros((perm.numel(), words), np.int64)
+        nbn = nb.numpy().astype(np.int64) & 0xFFFFFFFF
+        for w in range(0, W, 2):
+            hi = nbn[w + 1] if w + 1 < W else 0
+            rep[perm.numpy(), w // 2] = nbn[w] | (hi << 32)
+        rep[perm.numpy(), (W + 1) // 2:] = risk.numpy().T.view(np.int64)
+        return torch.from_numpy(rep)
+
+    @staticmethod
+    def unpack_reply(back, W):
+        b = back.numpy()
+        nb = np.zeros((len(b), W))
+        for w in range(W):
+            word = b[:, w // 2]
+            nb[:, w] = ((word >> 32) if w % 2 else word) & 0xFFFFFFFF
+        risk = np.ascontiguousarray(b[:, (W + 1) // 2:]).view(np.float64)
+        return nb, risk
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, shards, n_terms, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fdx.distributed import exchange_terminal_features
+
+    d = shards[rank]
+    back, send_perm = exchange_terminal_features(
+        CpuKernels, torch.from_numpy(d["ts"]), torch.from_numpy(d["terminal"]), torch.from_numpy(d["fraud"]),
+        world, n_terms)
+    nb, risk = CpuKernels.unpack_reply(back, 3)
+    rows = send_perm.numpy()
+    out_nb = np.zeros_like(nb); out_risk = np.zeros_like(risk)
+    out_nb[rows] = nb; out_risk[rows] = risk
+    q.put((rank, out_nb, out_risk))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_terminal_exchange_matches_single_process(world):
+    from fdx import synth
+
+    n_terms = 150
+    shards = [synth.generate(n_customers=120, n_terminals=n_terms, nb_days=60, r=30, seed=11 + r,
+                             customer_offset=120 * r) for r in range(world)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, n_terms, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, nb, risk = q.get(timeout=120)
+        res[r] = (nb, risk)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allc = {k: np.concatenate([s[k] for s in shards]) for k in shards[0]}
+    order = np.argsort(allc["ts"], kind="stable")
+    g = {k: v[order] for k, v in allc.items()}
+    f = oracle.featurize_arrays(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
+    inv = np.empty_like(order); inv[order] = np.arange(len(order))
+    start = 0
+    for r in range(world):
+        n = len(shards[r]["ts"])
+        idx = inv[start:start + n]
+        start += n
+        nb, risk = res[r]
+        for k, w in enumerate((1, 7, 30)):
+            np.testing.assert_array_equal(nb[:, k], f[f"TERMINAL_ID_NB_TX_{w}DAY_WINDOW"][idx])
+            np.testing.assert_array_equal(risk[:, k], f[f"TERMINAL_ID_RISK_{w}DAY_WINDOW"][idx])

@@ -1,0 +1,47 @@
+"""The multi-GPU path's HIP kernels and RCCL calls on one GPU (world_size 1): the sharded
+pipeline (owner keys, exchange pack/unpack, all-to-all to self, reply pack/assemble) must
+give the same feature matrix, bit for bit, as the single-GPU pipeline.  world > 1 routing
+is covered on CPU by tests/test_distributed_cpu.py (gloo, world 2 and 3)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from fdx import ops, synth
+from fdx.distributed import ShardedPipeline
+from fdx.pipeline import FraudPipeline
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_pipeline_world1_matches_single(dev):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        d = synth.generate(n_customers=3000, n_terminals=5000, nb_days=90, seed=3, customer_offset=0)
+        T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+        args = (T(d["ts"], torch.int64), T(d["customer"], torch.int32), T(d["terminal"], torch.int32),
+                T(d["amount"], torch.float64), T(d["fraud"], torch.uint8))
+        pipe = FraudPipeline()
+        ref = pipe.featurize(*args, 3000, 5000).X.cpu().numpy()
+        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=5000)
+        got = sp.featurize(*args, 3000).cpu().numpy()
+        np.testing.assert_array_equal(got, ref)
+        # exchange kernels with world > 1 semantics (owner = t % 4, local id = t / 4)
+        own = ops.key_map(args[2], 0, 4).cpu().numpy()
+        np.testing.assert_array_equal(own, d["terminal"] % 4)
+        np.testing.assert_array_equal(ops.key_map(args[2], 1, 4).cpu().numpy(), d["terminal"] // 4)
+        np.testing.assert_array_equal(ops.key_map(args[1], 2, 7).cpu().numpy(), d["customer"] - 7)
+    finally:
+        dist.destroy_process_group()
