@@ -208,6 +208,22 @@ int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t 
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
                         void *workspace_d, size_t workspace_bytes, void *stream);
 
+/* Fused assemble + scale for the scoring pipeline: writes the forest's float32 feature
+ * rows in the workspace straight from the window kernels' grouped outputs (same columns
+ * and arithmetic as fdx_assemble_features followed by fdx_forest_prepare), so
+ * fdx_forest_traverse can follow.  term_* may be NULL (filled by fdx_forest_prepare_reply
+ * in the multi-GPU path, col0 = 3 + 2*n_windows). */
+int fdx_forest_prepare_features(fdx_forest forest, int64_t n, int32_t n_windows,
+                                const double *amount_d, const uint8_t *weekend_d,
+                                const uint8_t *night_d, const int32_t *cust_perm_d,
+                                const int32_t *cust_nb_d, const double *cust_avg_d,
+                                const int32_t *term_perm_d, const int32_t *term_nb_d,
+                                const double *term_risk_d, void *workspace_d,
+                                size_t workspace_bytes, void *stream);
+int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const int32_t *perm_d,
+                             int64_t n, int32_t n_windows, int32_t col0, void *workspace_d,
+                             size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

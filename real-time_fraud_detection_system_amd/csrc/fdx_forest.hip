@@ -24,6 +24,7 @@
 // sum of a row crosses chunk launches through a workspace vector, preserving tree order.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -99,22 +100,93 @@ __global__ void __launch_bounds__(256) k_scale(const double *__restrict__ X, int
     }
 }
 
+__device__ __forceinline__ float zval(double x, const double *mean, const double *scale, int f) {
+    if (mean) x = x - mean[f];
+    if (scale) x = x / scale[f];
+    return (float)x;
+}
+
+// Fused assemble + scale: the scoring pipeline writes the forest's float32 feature rows
+// directly (no float64 feature matrix round trip).  Columns follow input_features.
+template <int FS>
+__global__ void __launch_bounds__(256) k_zfill_time(const double *__restrict__ amount,
+                                                   const uint8_t *__restrict__ weekend,
+                                                   const uint8_t *__restrict__ night, int64_t n,
+                                                   const double *__restrict__ mean,
+                                                   const double *__restrict__ scale, float *__restrict__ z) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        float *o = z + r * FS;
+        o[0] = zval(amount[r], mean, scale, 0);
+        o[1] = zval((double)weekend[r], mean, scale, 1);
+        o[2] = zval((double)night[r], mean, scale, 2);
+    }
+}
+
+template <int FS>
+__global__ void __launch_bounds__(256) k_zfill_group(const int32_t *__restrict__ perm,
+                                                    const int32_t *__restrict__ nb,
+                                                    const double *__restrict__ val, int64_t n, int32_t W,
+                                                    int32_t col0, const double *__restrict__ mean,
+                                                    const double *__restrict__ scale, float *__restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float *o = z + (int64_t)perm[i] * FS + col0;
+        for (int w = 0; w < W; ++w) {
+            o[2 * w] = zval((double)nb[(int64_t)w * n + i], mean, scale, col0 + 2 * w);
+            o[2 * w + 1] = zval(val[(int64_t)w * n + i], mean, scale, col0 + 2 * w + 1);
+        }
+    }
+}
+
+// same, from the multi-GPU reply records (fdx_reply_pack layout), row j -> perm[j]
+template <int FS>
+__global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__ reply,
+                                                    const int32_t *__restrict__ perm, int64_t n, int32_t W,
+                                                    int32_t col0, const double *__restrict__ mean,
+                                                    const double *__restrict__ scale, float *__restrict__ z) {
+    const int words = (W + 1) / 2 + W;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t *r = reply + j * words;
+        float *o = z + (int64_t)perm[j] * FS + col0;
+        for (int w = 0; w < W; ++w) {
+            const uint64_t pk = (uint64_t)r[w / 2];
+            const int32_t cnt = (int32_t)((w & 1) ? (pk >> 32) : (pk & 0xFFFFFFFFu));
+            o[2 * w] = zval((double)cnt, mean, scale, col0 + 2 * w);
+            o[2 * w + 1] = zval(__longlong_as_double(r[(W + 1) / 2 + w]), mean, scale, col0 + 2 * w + 1);
+        }
+    }
+}
+
+template <bool LDS>
+__device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char *gbase, uint32_t byte_off) {
+    if (LDS) return *reinterpret_cast<const uint64_t *>(reinterpret_cast<const char *>(s_nodes) + byte_off);
+    return *reinterpret_cast<const uint64_t *>(gbase + byte_off);
+}
+
+// One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Inner loop is phased so
+// that the G walks of a lane keep G LDS reads in flight at once: feature reads for all
+// walks, then the branch-free step for all walks, then node reads for all walks.  A walk
+// that reached its leaf keeps re-reading it (a no-op step) until every walk of the lane
+// is done; the loop is wave-uniform through the exec mask.
 template <int FS, bool LDS>
 __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
     const uint64_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes,
-    const int32_t *__restrict__ root, int32_t t0, int32_t t1, const float *__restrict__ z, int64_t n,
-    double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
+    const int32_t *__restrict__ root, int32_t t0, int32_t t1, const float *__restrict__ z, int64_t r0,
+    int64_t r1, double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
     const int32_t *__restrict__ orig, int32_t n_trees, int first, int last) {
     constexpr int kNodeCap = (LDS ? (FS == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) : 8) / 8;
     __shared__ uint64_t s_nodes[kNodeCap];
     __shared__ float s_x[FS][kFBlock];
     const int tid = threadIdx.x;
     const uint64_t *nb = nodes + node_base;
+    const char *gbase = reinterpret_cast<const char *>(nb);
     if (LDS) {
         for (int i = tid; i < chunk_nodes; i += kFBlock) s_nodes[i] = nb[i];
         __syncthreads();
     }
-    for (int64_t row = (int64_t)blockIdx.x * kFBlock + tid; row < n;
+    for (int64_t row = r0 + (int64_t)blockIdx.x * kFBlock + tid; row < r1;
          row += (int64_t)gridDim.x * kFBlock) {
         const float4 *src = reinterpret_cast<const float4 *>(z + row * FS);
 #pragma unroll
@@ -131,31 +203,35 @@ __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
             uint64_t nd[kG];
 #pragma unroll
             for (int g = 0; g < kG; ++g) {
+                // inactive walk slots sit on a leaf-like 0 word (never stepped)
                 const bool act = t + g < t1;
-                p[g] = act ? (uint32_t)(root[t + g] - node_base) : 0u;
-                nd[g] = act ? (LDS ? s_nodes[p[g]] : nb[p[g]]) : 0ull;
+                p[g] = act ? (uint32_t)(root[t + g] - node_base) * 8u : 0u;
+                nd[g] = act ? node_at<LDS>(s_nodes, gbase, p[g]) : 0ull;
             }
-            bool any = true;
-            while (any) {
-                any = false;
+            while (true) {
+                uint32_t live = 0;
+#pragma unroll
+                for (int g = 0; g < kG; ++g) live |= (uint32_t)(nd[g] >> 32);
+                if (!(live & kInternal)) break;
+                float x[kG];
+#pragma unroll
+                for (int g = 0; g < kG; ++g) x[g] = s_x[((uint32_t)(nd[g] >> 32) >> 25) & (FS - 1)][tid];
 #pragma unroll
                 for (int g = 0; g < kG; ++g) {
                     const uint32_t hi = (uint32_t)(nd[g] >> 32);
-                    if (hi & kInternal) {
-                        const float x = s_x[(hi >> 25) & 31][tid];
-                        const float thr = __uint_as_float((uint32_t)nd[g]);
-                        const bool left = (x != x) ? ((hi >> 30) & 1u) : (x <= thr);
-                        p[g] = left ? p[g] + 1u : p[g] + (hi & 0x1FFFFFFu);
-                        nd[g] = LDS ? s_nodes[p[g]] : nb[p[g]];
-                        any = true;
-                    }
+                    const float thr = __uint_as_float((uint32_t)nd[g]);
+                    const bool left = (x[g] <= thr) | ((x[g] != x[g]) & ((hi >> 30) & 1u));
+                    const uint32_t step = left ? 8u : (hi & 0x1FFFFFFu) * 8u;
+                    p[g] += (hi & kInternal) ? step : 0u;
                 }
+#pragma unroll
+                for (int g = 0; g < kG; ++g) nd[g] = node_at<LDS>(s_nodes, gbase, p[g]);
             }
 #pragma unroll
             for (int g = 0; g < kG; ++g) {
                 if (t + g < t1) {
                     a += leaf_value(nd[g]);
-                    if (leaf_out) leaf_out[row * n_trees + t + g] = orig[node_base + p[g]];
+                    if (leaf_out) leaf_out[row * n_trees + t + g] = orig[node_base + (p[g] >> 3)];
                 }
             }
         }
@@ -164,6 +240,15 @@ __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
         else
             acc[row] = a;
     }
+}
+
+int64_t forest_slab_rows() {
+    static int64_t v = [] {
+        const char *e = getenv("FDX_FOREST_SLAB_ROWS");
+        int64_t x = e ? atoll(e) : 0;
+        return x > 0 ? x : int64_t(2) << 20;
+    }();
+    return v;
 }
 
 float round_down_f32(double t) {
@@ -411,22 +496,28 @@ extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int
     int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
-    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, kFBlock), 256 * 4);
+    // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
+    // features and running sums stay in the 256 MiB Infinity Cache.
+    const int64_t slab = forest_slab_rows();
     const size_t nc = F->chunks.size();
-    for (size_t c = 0; c < nc; ++c) {
-        const auto &ch = F->chunks[c];
-        const int first = c == 0, last = c + 1 == nc;
+    for (int64_t s0 = 0; s0 < n; s0 += slab) {
+        const int64_t s1 = std::min<int64_t>(n, s0 + slab);
+        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, kFBlock), 256 * 4);
+        for (size_t c = 0; c < nc; ++c) {
+            const auto &ch = F->chunks[c];
+            const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_CHUNK(FS, L)                                                                        \
     hipLaunchKernelGGL((k_forest_chunk<FS, L>), dim3(grid), dim3(kFBlock), 0, st, F->nodes_d, ch.node_base, \
-                       (int32_t)ch.nodes, F->root_d, ch.t0, ch.t1, z, n, acc, proba_d, leaf_d, F->orig_d,    \
-                       F->n_trees, first, last)
-        if (F->zstride == 16) {
-            if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
-        } else {
-            if (ch.in_lds) FDX_LAUNCH_CHUNK(32, true); else FDX_LAUNCH_CHUNK(32, false);
-        }
+                       (int32_t)ch.nodes, F->root_d, ch.t0, ch.t1, z, s0, s1, acc, proba_d, leaf_d,          \
+                       F->orig_d, F->n_trees, first, last)
+            if (F->zstride == 16) {
+                if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
+            } else {
+                if (ch.in_lds) FDX_LAUNCH_CHUNK(32, true); else FDX_LAUNCH_CHUNK(32, false);
+            }
 #undef FDX_LAUNCH_CHUNK
-        FDX_LAUNCHED("k_forest_chunk");
+            FDX_LAUNCHED("k_forest_chunk");
+        }
     }
     return FDX_OK;
 }
@@ -450,5 +541,62 @@ extern "C" int fdx_standard_scale(const double *X_d, int64_t n, int32_t n_featur
                        n, n_features, row_stride, col_stride, mean_d, scale_d, out_d, out_row_stride,
                        out_col_stride);
     FDX_LAUNCHED("k_scale");
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_windows, const double *amount_d,
+                                           const uint8_t *weekend_d, const uint8_t *night_d,
+                                           const int32_t *cust_perm_d, const int32_t *cust_nb_d,
+                                           const double *cust_avg_d, const int32_t *term_perm_d,
+                                           const int32_t *term_nb_d, const double *term_risk_d, void *ws,
+                                           size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
+    FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
+                3 + 4 * n_windows);
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(amount_d && weekend_d && night_d && cust_perm_d && cust_nb_d && cust_avg_d, "null pointer");
+    float *z;
+    double *acc;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = stream_grid(n, 256);
+#define FDX_ZFILL(FS)                                                                                       \
+    do {                                                                                                    \
+        hipLaunchKernelGGL(k_zfill_time<FS>, dim3(grid), dim3(256), 0, st, amount_d, weekend_d, night_d, n,   \
+                           F->mean_d, F->scale_d, z);                                                       \
+        hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, cust_perm_d, cust_nb_d,          \
+                           cust_avg_d, n, n_windows, 3, F->mean_d, F->scale_d, z);                          \
+        if (term_perm_d && term_nb_d && term_risk_d)                                                       \
+            hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d,      \
+                               term_risk_d, n, n_windows, 3 + 2 * n_windows, F->mean_d, F->scale_d, z);     \
+    } while (0)
+    if (F->zstride == 16) FDX_ZFILL(16); else FDX_ZFILL(32);
+#undef FDX_ZFILL
+    FDX_LAUNCHED("k_zfill");
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, const int32_t *perm_d, int64_t n,
+                                        int32_t n_windows, int32_t col0, void *ws, size_t ws_bytes,
+                                        void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
+    FDX_REQUIRE(col0 >= 0 && col0 + 2 * n_windows <= F->n_features, "columns out of range");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(reply_d && perm_d, "null pointer");
+    float *z;
+    double *acc;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    if (rc) return rc;
+    const unsigned grid = stream_grid(n, 256);
+    if (F->zstride == 16)
+        hipLaunchKernelGGL(k_zfill_reply<16>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
+                           n_windows, col0, F->mean_d, F->scale_d, z);
+    else
+        hipLaunchKernelGGL(k_zfill_reply<32>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
+                           n_windows, col0, F->mean_d, F->scale_d, z);
+    FDX_LAUNCHED("k_zfill_reply");
     return FDX_OK;
 }

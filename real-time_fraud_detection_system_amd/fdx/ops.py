@@ -240,6 +240,24 @@ def forest_prepare(forest: "Forest", X: torch.Tensor, ws: torch.Tensor, stream=N
                                          _s(stream)), "fdx_forest_prepare")
 
 
+def forest_prepare_features(forest: "Forest", f, amount: torch.Tensor, ws: torch.Tensor, W: int,
+                            with_terminal: bool = True, stream=None):
+    """Fused assemble + scale into the forest workspace (float32 rows) from a
+    pipeline.Features; with_terminal=False leaves the terminal columns for the reply path."""
+    n = amount.numel()
+    t = with_terminal
+    check(_lib.load().fdx_forest_prepare_features(
+        forest._h, n, W, _ptr(amount), _ptr(f.weekend), _ptr(f.night), _ptr(f.cust_perm), _ptr(f.cust_nb),
+        _ptr(f.cust_avg), _ptr(f.term_perm) if t else None, _ptr(f.term_nb) if t else None,
+        _ptr(f.term_risk) if t else None, _ptr(ws), ws.numel(), _s(stream)), "fdx_forest_prepare_features")
+
+
+def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tensor, W: int, col0: int,
+                         ws: torch.Tensor, stream=None):
+    check(_lib.load().fdx_forest_prepare_reply(forest._h, _ptr(reply), _ptr(perm), perm.numel(), W, col0,
+                                               _ptr(ws), ws.numel(), _s(stream)), "fdx_forest_prepare_reply")
+
+
 def forest_traverse(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, stream=None):
     check(_lib.load().fdx_forest_traverse(forest._h, n, _ptr(out), None, _ptr(ws), ws.numel(), _s(stream)),
           "fdx_forest_traverse")

@@ -96,9 +96,24 @@ class FraudPipeline:
         return self.forest.predict(X, ws=self._ws, out=out, stream=stream)
 
     def run(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, stream=None):
+        """featurize (with the float64 feature matrix) + score; returns (Features, proba)."""
         f = self.featurize(ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, True,
                            False, stream)
         return f, self.score(f.X, stream=stream)
+
+    def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
+                  proba: torch.Tensor, ws: torch.Tensor, stream=None, on_traverse=None):
+        """The scoring path without the float64 feature matrix: window outputs are scaled
+        straight into the forest's float32 rows (fdx_forest_prepare_features)."""
+        f = self.featurize(ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, False,
+                           False, stream)
+        ops.forest_prepare_features(self.forest, f, amount, ws, len(self.windows_days), True, stream)
+        if on_traverse:
+            on_traverse(0)
+        ops.forest_traverse(self.forest, amount.numel(), ws, proba, stream)
+        if on_traverse:
+            on_traverse(1)
+        return proba
 
 
 def _to_caller_order(f: Features, tperm: torch.Tensor, stream) -> Features:

@@ -45,3 +45,32 @@ def test_sharded_pipeline_world1_matches_single(dev):
         np.testing.assert_array_equal(ops.key_map(args[1], 2, 7).cpu().numpy(), d["customer"] - 7)
     finally:
         dist.destroy_process_group()
+
+
+def test_fused_scoring_paths_agree(dev, golden):
+    """run_fused (z32 written by the window outputs) == featurize + float64 X + predict, and
+    the sharded run (world 1) gives the same probabilities."""
+    z = golden("forest_rf5d8.npz")
+    arrays = {k: z[k] for k in ("left", "right", "feature", "threshold", "missing_left", "value1",
+                                "node_offsets")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    d = synth.generate(n_customers=2000, n_terminals=4000, nb_days=60, seed=9)
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    args = (T(d["ts"], torch.int64), T(d["customer"], torch.int32), T(d["terminal"], torch.int32),
+            T(d["amount"], torch.float64), T(d["fraud"], torch.uint8))
+    n = len(d["ts"])
+    pipe = FraudPipeline(forest=forest)
+    _, p_ref = pipe.run(*args, 2000, 4000)
+    ws = ops.workspace(forest.workspace_size(n), dev)
+    p1 = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 2000, 4000, p1, ws)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p_ref.cpu().numpy())
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=4000)
+        p2 = torch.zeros(n, dtype=torch.float64, device=dev)
+        sp.run(*args, 2000, p2, ws)
+        np.testing.assert_array_equal(p2.cpu().numpy(), p_ref.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
