@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-customers", type=int, default=2500)
     ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
+    ap.add_argument("--slab-rows", type=int, default=0, help="forest traversal slab rows (0 = all rows)")
+    ap.add_argument("--sweep-slab", default="", help="comma list of slab sizes to time (stderr)")
     return ap.parse_args()
 
 
@@ -96,6 +98,7 @@ def main():
     n_local = len(data["ts"])
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
+    forest.set_slab_rows(args.slab_rows)
     T = lambda a, d: torch.from_numpy(np.ascontiguousarray(a)).to(dev, d)  # noqa: E731
     # sanity: the GPU forest reproduces sklearn on the held-out sample saved with the model
     got = forest.predict(T(check_X, torch.float64)).cpu().numpy()
@@ -159,7 +162,7 @@ def main():
         n_total = n_local
 
     trav_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
-    slab = int(os.environ.get("FDX_FOREST_SLAB_ROWS", str(2 << 20)))
+    slab = args.slab_rows if args.slab_rows > 0 else n_local
     launches = forest.n_chunks * -(-n_local // slab)
     launch_ms = trav_ms / launches
     # every launch streams its slab's rows once: total algorithmic bytes / total time
@@ -190,6 +193,20 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, args.cpu_sample_customers)
+    if args.sweep_slab and rank == 0:
+        res = {}
+        for sr in [int(x) for x in args.sweep_slab.split(",")]:
+            forest.set_slab_rows(sr)
+            ops.forest_traverse(forest, n_local, ws, proba)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(3):
+                ops.forest_traverse(forest, n_local, ws, proba)
+            b.record()
+            torch.cuda.synchronize()
+            res[sr] = round(a.elapsed_time(b) / 3, 3)
+        forest.set_slab_rows(args.slab_rows)
+        print(json.dumps({"slab_sweep_traverse_ms": res}), file=sys.stderr)
     if args.breakdown and rank == 0:
         print(json.dumps(stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba)),
               file=sys.stderr)

@@ -207,6 +207,9 @@ int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t 
                        int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
                         void *workspace_d, size_t workspace_bytes, void *stream);
+/* Rows per traversal slab (all chunks run over one slab before the next, so that the
+ * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
+int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
 
 /* Fused assemble + scale for the scoring pipeline: writes the forest's float32 feature
  * rows in the workspace straight from the window kernels' grouped outputs (same columns

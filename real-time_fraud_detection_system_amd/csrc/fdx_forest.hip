@@ -14,8 +14,10 @@
 //   proba = (((0 + v_t0) + v_t1) + ...) / n_trees  in float64, trees in index order.
 //
 // Node format (8 bytes, trees re-laid out in pre-order so the left child is p+1):
-//   internal: hi = 0x80000000 | missing_left<<30 | feature<<25 | (right - p)  lo = thr32_down
+//   internal: hi = 0x80000000 | missing_left<<30 | feature<<24 | 8*(right - p)   lo = thr32_down
 //   leaf    : the float64 class-1 value itself (sign bit 0, so hi bit 31 = 0)
+// A leaf is a fixed point of the step (its step is masked to 0 by the sign of hi), so every
+// walk runs exactly depth(tree group) steps with no per-step leaf test.
 //
 // Kernel structure: trees are cut into chunks that fit the LDS budget; one launch per
 // chunk streams every row once: the block stages the chunk's nodes into LDS, each thread
@@ -37,6 +39,7 @@ struct fdx_forest_s {
     uint64_t *nodes_d = nullptr;   // packed nodes, all trees
     int32_t *orig_d = nullptr;     // sklearn node id of each packed node
     int32_t *root_d = nullptr;     // packed position of each tree root
+    int32_t *depth_d = nullptr;    // max leaf depth of each tree (steps to reach any leaf)
     double *mean_d = nullptr, *scale_d = nullptr;
     struct Chunk {
         int32_t t0, t1;
@@ -44,6 +47,7 @@ struct fdx_forest_s {
         bool in_lds;
     };
     std::vector<Chunk> chunks;
+    int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or 2M rows)
 };
 
 namespace fdx {
@@ -62,10 +66,11 @@ template <int FS>
 __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, int64_t n, int64_t rs,
                                                  int64_t cs, int32_t nf, const double *__restrict__ mean,
                                                  const double *__restrict__ scale,
-                                                 float *__restrict__ z) {
+                                                 float *__restrict__ z, int32_t *__restrict__ nan_flag) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
+        bool nan = false;
 #pragma unroll
         for (int f = 0; f < FS; ++f) {
             if (f < nf) {
@@ -73,10 +78,12 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
                 if (mean) x = x - mean[f];
                 if (scale) x = x / scale[f];
                 v[f] = (float)x;
+                nan |= x != x;
             } else {
                 v[f] = 0.0f;
             }
         }
+        if (nan) *nan_flag = 1;  // routes the traversal through the NaN-aware step
         float4 *dst = reinterpret_cast<float4 *>(z + r * FS);
 #pragma unroll
         for (int q = 0; q < FS / 4; ++q) dst[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
@@ -113,13 +120,16 @@ __global__ void __launch_bounds__(256) k_zfill_time(const double *__restrict__ a
                                                    const uint8_t *__restrict__ weekend,
                                                    const uint8_t *__restrict__ night, int64_t n,
                                                    const double *__restrict__ mean,
-                                                   const double *__restrict__ scale, float *__restrict__ z) {
+                                                   const double *__restrict__ scale, float *__restrict__ z,
+                                                   int32_t *__restrict__ nan_flag) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         float *o = z + r * FS;
-        o[0] = zval(amount[r], mean, scale, 0);
+        const float a = zval(amount[r], mean, scale, 0);
+        o[0] = a;
         o[1] = zval((double)weekend[r], mean, scale, 1);
         o[2] = zval((double)night[r], mean, scale, 2);
+        if (a != a) *nan_flag = 1;
     }
 }
 
@@ -128,14 +138,19 @@ __global__ void __launch_bounds__(256) k_zfill_group(const int32_t *__restrict__
                                                     const int32_t *__restrict__ nb,
                                                     const double *__restrict__ val, int64_t n, int32_t W,
                                                     int32_t col0, const double *__restrict__ mean,
-                                                    const double *__restrict__ scale, float *__restrict__ z) {
+                                                    const double *__restrict__ scale, float *__restrict__ z,
+                                                    int32_t *__restrict__ nan_flag) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float *o = z + (int64_t)perm[i] * FS + col0;
+        bool nan = false;
         for (int w = 0; w < W; ++w) {
             o[2 * w] = zval((double)nb[(int64_t)w * n + i], mean, scale, col0 + 2 * w);
-            o[2 * w + 1] = zval(val[(int64_t)w * n + i], mean, scale, col0 + 2 * w + 1);
+            const float v = zval(val[(int64_t)w * n + i], mean, scale, col0 + 2 * w + 1);
+            o[2 * w + 1] = v;
+            nan |= v != v;
         }
+        if (nan) *nan_flag = 1;
     }
 }
 
@@ -144,18 +159,23 @@ template <int FS>
 __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__ reply,
                                                     const int32_t *__restrict__ perm, int64_t n, int32_t W,
                                                     int32_t col0, const double *__restrict__ mean,
-                                                    const double *__restrict__ scale, float *__restrict__ z) {
+                                                    const double *__restrict__ scale, float *__restrict__ z,
+                                                    int32_t *__restrict__ nan_flag) {
     const int words = (W + 1) / 2 + W;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t *r = reply + j * words;
         float *o = z + (int64_t)perm[j] * FS + col0;
+        bool nan = false;
         for (int w = 0; w < W; ++w) {
             const uint64_t pk = (uint64_t)r[w / 2];
             const int32_t cnt = (int32_t)((w & 1) ? (pk >> 32) : (pk & 0xFFFFFFFFu));
             o[2 * w] = zval((double)cnt, mean, scale, col0 + 2 * w);
-            o[2 * w + 1] = zval(__longlong_as_double(r[(W + 1) / 2 + w]), mean, scale, col0 + 2 * w + 1);
+            const float v = zval(__longlong_as_double(r[(W + 1) / 2 + w]), mean, scale, col0 + 2 * w + 1);
+            o[2 * w + 1] = v;
+            nan |= v != v;
         }
+        if (nan) *nan_flag = 1;
     }
 }
 
@@ -165,16 +185,41 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
     return *reinterpret_cast<const uint64_t *>(gbase + byte_off);
 }
 
-// One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Inner loop is phased so
-// that the G walks of a lane keep G LDS reads in flight at once: feature reads for all
-// walks, then the branch-free step for all walks, then node reads for all walks.  A walk
-// that reached its leaf keeps re-reading it (a no-op step) until every walk of the lane
-// is done; the loop is wave-uniform through the exec mask.
+// One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Each lane walks G trees of
+// one row at once.  A step is branch-free (leaves are fixed points), all G feature reads are
+// issued together, then all G node reads, so a lane keeps G LDS reads in flight; a group
+// of G trees runs exactly max(depth) steps, so the loop is uniform across the wave.
+// NaN routing (missing_go_to_left) costs 3 extra VALU per step: it is compiled in a second
+// loop that runs only when the prepare step saw a NaN feature (*nan_flag != 0).
+template <bool NAN_AWARE, bool LDS>
+__device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *s_xcol,
+                                           uint32_t (&p)[kG], uint64_t (&nd)[kG], int depth) {
+    for (int d = 0; d < depth; ++d) {
+        float x[kG];
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            const uint32_t hi = (uint32_t)(nd[g] >> 32);
+            x[g] = s_xcol[((hi >> 24) & 63u) * kFBlock];
+        }
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            const uint32_t hi = (uint32_t)(nd[g] >> 32);
+            bool left = x[g] <= __uint_as_float((uint32_t)nd[g]);
+            if (NAN_AWARE) left = left | ((x[g] != x[g]) & ((hi >> 30) & 1u));
+            const uint32_t step = left ? 8u : (hi & 0xFFFFFFu);
+            p[g] += step & (uint32_t)((int32_t)hi >> 31);
+        }
+#pragma unroll
+        for (int g = 0; g < kG; ++g) nd[g] = node_at<LDS>(s_nodes, gbase, p[g]);
+    }
+}
+
 template <int FS, bool LDS>
 __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
     const uint64_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes,
-    const int32_t *__restrict__ root, int32_t t0, int32_t t1, const float *__restrict__ z, int64_t r0,
-    int64_t r1, double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
+    const int32_t *__restrict__ root, const int32_t *__restrict__ depth, int32_t t0, int32_t t1,
+    const float *__restrict__ z, const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1,
+    double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
     const int32_t *__restrict__ orig, int32_t n_trees, int first, int last) {
     constexpr int kNodeCap = (LDS ? (FS == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) : 8) / 8;
     __shared__ uint64_t s_nodes[kNodeCap];
@@ -182,10 +227,12 @@ __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
     const int tid = threadIdx.x;
     const uint64_t *nb = nodes + node_base;
     const char *gbase = reinterpret_cast<const char *>(nb);
+    const bool any_nan = *nan_flag != 0;  // uniform
     if (LDS) {
         for (int i = tid; i < chunk_nodes; i += kFBlock) s_nodes[i] = nb[i];
         __syncthreads();
     }
+    const float *s_xcol = &s_x[0][tid];
     for (int64_t row = r0 + (int64_t)blockIdx.x * kFBlock + tid; row < r1;
          row += (int64_t)gridDim.x * kFBlock) {
         const float4 *src = reinterpret_cast<const float4 *>(z + row * FS);
@@ -201,32 +248,19 @@ __global__ void __launch_bounds__(kFBlock) k_forest_chunk(
         for (int t = t0; t < t1; t += kG) {
             uint32_t p[kG];
             uint64_t nd[kG];
+            int dmax = 0;
 #pragma unroll
             for (int g = 0; g < kG; ++g) {
-                // inactive walk slots sit on a leaf-like 0 word (never stepped)
+                // inactive walk slots sit on a leaf-like 0 word (a fixed point)
                 const bool act = t + g < t1;
                 p[g] = act ? (uint32_t)(root[t + g] - node_base) * 8u : 0u;
                 nd[g] = act ? node_at<LDS>(s_nodes, gbase, p[g]) : 0ull;
+                dmax = act ? max(dmax, depth[t + g]) : dmax;
             }
-            while (true) {
-                uint32_t live = 0;
-#pragma unroll
-                for (int g = 0; g < kG; ++g) live |= (uint32_t)(nd[g] >> 32);
-                if (!(live & kInternal)) break;
-                float x[kG];
-#pragma unroll
-                for (int g = 0; g < kG; ++g) x[g] = s_x[((uint32_t)(nd[g] >> 32) >> 25) & (FS - 1)][tid];
-#pragma unroll
-                for (int g = 0; g < kG; ++g) {
-                    const uint32_t hi = (uint32_t)(nd[g] >> 32);
-                    const float thr = __uint_as_float((uint32_t)nd[g]);
-                    const bool left = (x[g] <= thr) | ((x[g] != x[g]) & ((hi >> 30) & 1u));
-                    const uint32_t step = left ? 8u : (hi & 0x1FFFFFFu) * 8u;
-                    p[g] += (hi & kInternal) ? step : 0u;
-                }
-#pragma unroll
-                for (int g = 0; g < kG; ++g) nd[g] = node_at<LDS>(s_nodes, gbase, p[g]);
-            }
+            if (any_nan)
+                walk_group<true, LDS>(s_nodes, gbase, s_xcol, p, nd, dmax);
+            else
+                walk_group<false, LDS>(s_nodes, gbase, s_xcol, p, nd, dmax);
 #pragma unroll
             for (int g = 0; g < kG; ++g) {
                 if (t + g < t1) {
@@ -246,7 +280,7 @@ int64_t forest_slab_rows() {
     static int64_t v = [] {
         const char *e = getenv("FDX_FOREST_SLAB_ROWS");
         int64_t x = e ? atoll(e) : 0;
-        return x > 0 ? x : int64_t(2) << 20;
+        return x > 0 ? x : INT64_MAX;  // measured: slabbing for Infinity-Cache reuse did not pay (r01)
     }();
     return v;
 }
@@ -268,7 +302,7 @@ namespace fdx {
 namespace {
 // Host-side validation + pre-order re-layout + 8-byte node packing (see header comment).
 int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::vector<int32_t> &orig,
-                std::vector<int32_t> &root) {
+                std::vector<int32_t> &root, std::vector<int32_t> &depth) {
     FDX_REQUIRE(d, "null pointer");
     FDX_REQUIRE(d->n_trees >= 1, "n_trees must be >= 1");
     FDX_REQUIRE(d->n_features >= 1 && d->n_features <= FDX_MAX_FEATURES, "n_features must be in [1, %d]",
@@ -280,6 +314,7 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
     FDX_REQUIRE(d->node_offsets[0] == 0 && total > 0 && total < (int64_t(1) << 31), "bad node_offsets");
     packed.assign((size_t)total, 0);
     orig.assign((size_t)total, 0);
+    depth.assign((size_t)d->n_trees, 0);
     root.assign((size_t)d->n_trees, 0);
     std::vector<int64_t> stack;
     for (int32_t t = 0; t < d->n_trees; ++t) {
@@ -308,6 +343,20 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
         }
         FDX_REQUIRE(next == e, "tree %d: %lld unreachable nodes", t, (long long)(e - next));
         root[(size_t)t] = (int32_t)b;
+        {   // max leaf depth = number of steps a walk of this tree takes
+            std::vector<int32_t> dep((size_t)cnt, 0);
+            int32_t dm = 0;
+            for (int64_t i : order) {  // pre-order: parents before children
+                const int64_t l = d->children_left[b + i];
+                if (l != -1) {
+                    dep[(size_t)l] = dep[(size_t)i] + 1;
+                    dep[(size_t)d->children_right[b + i]] = dep[(size_t)i] + 1;
+                } else if (dep[(size_t)i] > dm) {
+                    dm = dep[(size_t)i];
+                }
+            }
+            depth[(size_t)t] = dm;
+        }
         for (int64_t i : order) {
             const int64_t p = pos[(size_t)i];
             orig[(size_t)p] = (int32_t)i;
@@ -327,7 +376,7 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
                 const int64_t rp = pos[(size_t)d->children_right[b + i]];
                 FDX_REQUIRE(pos[(size_t)l] == p + 1, "tree %d: pre-order violated", t);
                 const int64_t rel = rp - p;
-                FDX_REQUIRE(rel > 0 && rel < (int64_t(1) << 25), "tree %d: subtree too large", t);
+                FDX_REQUIRE(rel > 0 && rel < (int64_t(1) << 21), "tree %d: subtree too large", t);
                 const int64_t f = d->feature[b + i];
                 FDX_REQUIRE(f >= 0 && f < d->n_features, "tree %d node %lld: feature %lld out of range", t,
                             (long long)i, (long long)f);
@@ -335,7 +384,7 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
                 const float thr = round_down_f32(d->threshold[b + i]);
                 uint32_t lo;
                 memcpy(&lo, &thr, 4);
-                const uint32_t hi = kInternal | (ml << 30) | ((uint32_t)f << 25) | (uint32_t)rel;
+                const uint32_t hi = kInternal | (ml << 30) | ((uint32_t)f << 24) | (uint32_t)(rel * 8);
                 packed[(size_t)p] = ((uint64_t)hi << 32) | lo;
             }
         }
@@ -348,8 +397,8 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
 extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, int32_t *orig_out,
                                int32_t *root_out) {
     std::vector<uint64_t> packed;
-    std::vector<int32_t> orig, root;
-    int rc = pack_forest(d, packed, orig, root);
+    std::vector<int32_t> orig, root, depth;
+    int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
     FDX_REQUIRE(nodes_out && orig_out && root_out, "null output");
     memcpy(nodes_out, packed.data(), packed.size() * 8);
@@ -362,8 +411,8 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     FDX_REQUIRE(d && out, "null pointer");
     *out = nullptr;
     std::vector<uint64_t> packed;
-    std::vector<int32_t> orig, root;
-    int rc = pack_forest(d, packed, orig, root);
+    std::vector<int32_t> orig, root, depth;
+    int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
     const int64_t total = (int64_t)packed.size();
     fdx_forest_s *F = new (std::nothrow) fdx_forest_s();
@@ -384,6 +433,8 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         } else {
             int32_t u = t + 1;
             while (u < d->n_trees && d->node_offsets[u + 1] - c.node_base <= cap_nodes) ++u;
+            // keep whole groups of kG trees (a partial group idles walk slots)
+            if (u - t > kG && (u - t) % kG) u -= (u - t) % kG;
             c.t1 = u;
             c.in_lds = true;
         }
@@ -401,6 +452,9 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     if ((e = hipMalloc(&F->nodes_d, sizeof(uint64_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->root_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&F->depth_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMemcpyAsync(F->depth_d, depth.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
+        return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->nodes_d, packed.data(), sizeof(uint64_t) * total, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->orig_d, orig.data(), sizeof(int32_t) * total, hipMemcpyHostToDevice, st)))
@@ -430,6 +484,7 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->nodes_d);
     (void)hipFree(F->orig_d);
     (void)hipFree(F->root_d);
+    (void)hipFree(F->depth_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
     delete F;
@@ -448,10 +503,12 @@ extern "C" int fdx_forest_info(fdx_forest F, int32_t *n_trees, int32_t *n_featur
 
 extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows) {
     if (!F || n_rows <= 0) return 256;
-    return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows);
+    return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows) +
+           256;  // + NaN flag word
 }
 
-static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, double **acc) {
+static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, double **acc,
+                     int32_t **nan_flag = nullptr) {
     size_t need = fdx_forest_workspace_size(F, n);
     if (!ws || ws_bytes < need) {
         set_error("forest workspace too small: %zu < %zu", ws_bytes, need);
@@ -460,6 +517,8 @@ static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float *
     *z = reinterpret_cast<float *>(ws);
     *acc = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) +
                                       align_up(sizeof(float) * F->zstride * (size_t)n));
+    if (nan_flag)
+        *nan_flag = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(*acc) + align_up(sizeof(double) * (size_t)n));
     return FDX_OK;
 }
 
@@ -471,16 +530,18 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     FDX_REQUIRE(X_d, "null pointer");
     float *z;
     double *acc;
-    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
+    FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
     if (F->zstride == 16)
         hipLaunchKernelGGL(k_prepare<16>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
-                           F->n_features, F->mean_d, F->scale_d, z);
+                           F->n_features, F->mean_d, F->scale_d, z, flag);
     else
         hipLaunchKernelGGL(k_prepare<32>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
-                           F->n_features, F->mean_d, F->scale_d, z);
+                           F->n_features, F->mean_d, F->scale_d, z, flag);
     FDX_LAUNCHED("k_prepare");
     return FDX_OK;
 }
@@ -493,12 +554,13 @@ extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int
     FDX_REQUIRE(proba_d, "null pointer");
     float *z;
     double *acc;
-    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
     // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
     // features and running sums stay in the 256 MiB Infinity Cache.
-    const int64_t slab = forest_slab_rows();
+    const int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
     const size_t nc = F->chunks.size();
     for (int64_t s0 = 0; s0 < n; s0 += slab) {
         const int64_t s1 = std::min<int64_t>(n, s0 + slab);
@@ -508,8 +570,8 @@ extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int
             const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_CHUNK(FS, L)                                                                        \
     hipLaunchKernelGGL((k_forest_chunk<FS, L>), dim3(grid), dim3(kFBlock), 0, st, F->nodes_d, ch.node_base, \
-                       (int32_t)ch.nodes, F->root_d, ch.t0, ch.t1, z, s0, s1, acc, proba_d, leaf_d,          \
-                       F->orig_d, F->n_trees, first, last)
+                       (int32_t)ch.nodes, F->root_d, F->depth_d, ch.t0, ch.t1, z, flag, s0, s1, acc, proba_d, \
+                       leaf_d, F->orig_d, F->n_trees, first, last)
             if (F->zstride == 16) {
                 if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
             } else {
@@ -558,19 +620,21 @@ extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_wi
     FDX_REQUIRE(amount_d && weekend_d && night_d && cust_perm_d && cust_nb_d && cust_avg_d, "null pointer");
     float *z;
     double *acc;
-    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
+    FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
 #define FDX_ZFILL(FS)                                                                                       \
     do {                                                                                                    \
         hipLaunchKernelGGL(k_zfill_time<FS>, dim3(grid), dim3(256), 0, st, amount_d, weekend_d, night_d, n,   \
-                           F->mean_d, F->scale_d, z);                                                       \
+                           F->mean_d, F->scale_d, z, flag);                                                 \
         hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, cust_perm_d, cust_nb_d,          \
-                           cust_avg_d, n, n_windows, 3, F->mean_d, F->scale_d, z);                          \
+                           cust_avg_d, n, n_windows, 3, F->mean_d, F->scale_d, z, flag);                    \
         if (term_perm_d && term_nb_d && term_risk_d)                                                       \
             hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d,      \
-                               term_risk_d, n, n_windows, 3 + 2 * n_windows, F->mean_d, F->scale_d, z);     \
+                               term_risk_d, n, n_windows, 3 + 2 * n_windows, F->mean_d, F->scale_d, z, flag); \
     } while (0)
     if (F->zstride == 16) FDX_ZFILL(16); else FDX_ZFILL(32);
 #undef FDX_ZFILL
@@ -588,15 +652,23 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
     FDX_REQUIRE(reply_d && perm_d, "null pointer");
     float *z;
     double *acc;
-    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc);
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     const unsigned grid = stream_grid(n, 256);
     if (F->zstride == 16)
         hipLaunchKernelGGL(k_zfill_reply<16>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
-                           n_windows, col0, F->mean_d, F->scale_d, z);
+                           n_windows, col0, F->mean_d, F->scale_d, z, flag);
     else
         hipLaunchKernelGGL(k_zfill_reply<32>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
-                           n_windows, col0, F->mean_d, F->scale_d, z);
+                           n_windows, col0, F->mean_d, F->scale_d, z, flag);
     FDX_LAUNCHED("k_zfill_reply");
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_set_slab_rows(fdx_forest F, int64_t rows) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(rows >= 0, "rows < 0");
+    F->slab_rows = rows;
     return FDX_OK;
 }

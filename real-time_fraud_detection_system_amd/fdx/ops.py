@@ -212,6 +212,10 @@ class Forest:
             _lib._lib.fdx_forest_destroy(h)
             self._h = None
 
+    def set_slab_rows(self, rows: int) -> None:
+        check(_lib.load().fdx_forest_set_slab_rows(self._h, int(rows)), "fdx_forest_set_slab_rows")
+        self.slab_rows = int(rows)
+
     def workspace_size(self, n: int) -> int:
         return int(_lib.load().fdx_forest_workspace_size(self._h, int(n)))
 

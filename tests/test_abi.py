@@ -79,10 +79,10 @@ def _walk_packed(nodes, orig, root, z32):
             internal = (h & 0x80000000) != 0
             if not internal.any():
                 break
-            f = ((h >> 25) & 31).astype(np.int64)
+            f = ((h >> 24) & 63).astype(np.int64)
             x = z32[np.arange(n), np.minimum(f, z32.shape[1] - 1)]
             left = np.where(np.isnan(x), (h >> 30) & 1, x <= thr[p]).astype(bool)
-            rel = (h & 0x1FFFFFF).astype(np.int64)
+            rel = (h & 0xFFFFFF).astype(np.int64) // 8
             p = np.where(internal, np.where(left, p + 1, p + rel), p)
         acc = acc + vals[p]
         leaves[:, t] = orig[p]
