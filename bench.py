@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
     ap.add_argument("--slab-rows", type=int, default=0, help="forest traversal slab rows (0 = all rows)")
     ap.add_argument("--sweep-slab", default="", help="comma list of slab sizes to time (stderr)")
+    ap.add_argument("--forest-variant", type=int, default=0, help="traversal kernel shape (fdx_forest_set_variant)")
+    ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     return ap.parse_args()
 
 
@@ -99,6 +101,7 @@ def main():
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
     forest.set_slab_rows(args.slab_rows)
+    forest.set_variant(args.forest_variant)
     T = lambda a, d: torch.from_numpy(np.ascontiguousarray(a)).to(dev, d)  # noqa: E731
     # sanity: the GPU forest reproduces sklearn on the held-out sample saved with the model
     got = forest.predict(T(check_X, torch.float64)).cpu().numpy()
@@ -207,6 +210,24 @@ def main():
             res[sr] = round(a.elapsed_time(b) / 3, 3)
         forest.set_slab_rows(args.slab_rows)
         print(json.dumps({"slab_sweep_traverse_ms": res}), file=sys.stderr)
+    if args.sweep_variant and rank == 0:
+        res = {}
+        ref = proba.clone()
+        ops.forest_traverse(forest, n_local, ws, ref)
+        for v in [int(x) for x in args.sweep_variant.split(",")]:
+            forest.set_variant(v)
+            out = torch.empty_like(proba)
+            ops.forest_traverse(forest, n_local, ws, out)
+            same = bool(torch.equal(out, ref))
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(3):
+                ops.forest_traverse(forest, n_local, ws, out)
+            b.record()
+            torch.cuda.synchronize()
+            res[v] = {"ms": round(a.elapsed_time(b) / 3, 3), "chunks": forest.n_chunks, "bit_equal": same}
+        forest.set_variant(args.forest_variant)
+        print(json.dumps({"variant_sweep_traverse": res}), file=sys.stderr)
     if args.breakdown and rank == 0:
         print(json.dumps(stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba)),
               file=sys.stderr)
@@ -230,8 +251,6 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
 
     n = ts.numel()
     mark("start")
-    we, ni = ops.time_flags(ts)
-    mark("flags")
     cperm, cseg, _ = ops.rekey(cust, args.customers)
     mark("rekey_customer")
     cts, camt = ops.gather(ts, cperm), ops.gather(amt, cperm)
@@ -242,14 +261,13 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("rekey_terminal")
     tts, tfr = ops.gather(ts, tperm), ops.gather(fr, tperm)
     mark("gather_terminal")
-    tnb, trisk = ops.terminal_windows(tts, tfr, tseg)
+    trec = ops.terminal_windows_packed(tts, tfr, tseg)
     mark("terminal_windows")
-    from fdx.pipeline import Features
-
-    ops.forest_prepare_features(forest, Features(we, ni, cperm, cseg, cnb, cavg, tperm, tseg, tnb, trisk), amt,
-                                ws, 3)
+    tinv = ops.invert_perm(tperm)
+    mark("invert_terminal_perm")
+    ops.forest_prepare_grouped(forest, 0, cts, camt, cnb, cavg, cperm, tinv, trec, ws)
     mark("assemble_scale_z32")
-    ops.forest_traverse(forest, n, ws, proba)
+    ops.forest_traverse_perm(forest, n, ws, proba, cperm)
     mark("forest_traverse")
     torch.cuda.synchronize()
     return {"breakdown_ms": {marks[i][0]: round(marks[i - 1][1].elapsed_time(marks[i][1]), 4)

@@ -97,6 +97,14 @@ int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
                           const int32_t *term_nb_d, const double *term_risk_d, double *X_d, int64_t ld,
                           void *stream);
 
+/* Same as fdx_terminal_windows, but one packed record per row (grouped order):
+ * ceil(W/2) 8-byte words of int32 counts, then W float64 risks (rec_d: [n][ceil(W/2)+W]
+ * int64).  The record is what fdx_forest_prepare_grouped reads. */
+int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
+                                void *stream);
+
 /* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
  * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /
  * groupby('TERMINAL_ID') (feature_transformation.ipynb:1092-1093, :2435-2436).
@@ -118,6 +126,9 @@ int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *wor
                     size_t workspace_bytes, void *stream);
 /* *flag_d = 1 if keys_d is non-decreasing, else 0 (stream-ordered). */
 int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream);
+
+/* inv_d[perm_d[i]] = i */
+int fdx_invert_perm(const int32_t *perm_d, int64_t n, int32_t *inv_d, void *stream);
 
 /* dst[j] = src[perm[j]] for 1-, 2-, 4- or 8-byte elements (elem_bytes). */
 int fdx_gather(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, int64_t n, void *dst_d,
@@ -210,6 +221,10 @@ int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *
 /* Rows per traversal slab (all chunks run over one slab before the next, so that the
  * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
 int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
+/* Traversal kernel shape: 0 = 512 threads x 1 row x 4 trees per lane (default), 1 = 1024 x 1
+ * x 4, 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4 (variants > 0 need <= 16 features).
+ * Re-cuts the LDS chunks; results are identical for every variant. */
+int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
 
 /* Fused assemble + scale for the scoring pipeline: writes the forest's float32 feature
  * rows in the workspace straight from the window kernels' grouped outputs (same columns
@@ -226,6 +241,23 @@ int fdx_forest_prepare_features(fdx_forest forest, int64_t n, int32_t n_windows,
 int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const int32_t *perm_d,
                              int64_t n, int32_t n_windows, int32_t col0, void *workspace_d,
                              size_t workspace_bytes, void *stream);
+
+/* The scoring rows in CUSTOMER-grouped order, each written whole (coalesced): row i is
+ * transaction r = cust_perm[i]; cust_ts/cust_amount/cust_nb/cust_avg are the customer-grouped
+ * copies and outputs (flags are derived from cust_ts with flags_mode), the terminal half
+ * is the packed record term_rec[term_inv[r]] (fdx_terminal_windows_packed output with
+ * term_inv = inverse of the terminal perm, or the multi-GPU reply records with term_inv =
+ * inverse of the send perm).  Follow with fdx_forest_traverse_perm(out_perm = cust_perm)
+ * so that proba lands in row order. */
+int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
+                               const int64_t *cust_ts_d, const double *cust_amount_d,
+                               const int32_t *cust_nb_d, const double *cust_avg_d,
+                               const int32_t *cust_perm_d, const int32_t *term_inv_d,
+                               const int64_t *term_rec_d, void *workspace_d, size_t workspace_bytes,
+                               void *stream);
+/* fdx_forest_traverse writing proba_d[out_perm_d[row]] (and leaf rows likewise). */
+int fdx_forest_traverse_perm(fdx_forest forest, int64_t n, double *proba_d, const int32_t *out_perm_d,
+                             int32_t *leaf_d, void *workspace_d, size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

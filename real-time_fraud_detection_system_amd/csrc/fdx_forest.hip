@@ -47,16 +47,14 @@ struct fdx_forest_s {
         bool in_lds;
     };
     std::vector<Chunk> chunks;
-    int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or 2M rows)
+    int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or all rows)
+    int variant = 0;        // index into kVariants
+    std::vector<int64_t> node_offsets;  // host copy (chunking)
 };
 
 namespace fdx {
 namespace {
 
-constexpr int kFBlock = 512;
-constexpr int kG = 4;                          // trees walked concurrently per lane
-constexpr int kLdsNodeBytes16 = 120 * 1024;    // LDS for nodes when 16 feature slots
-constexpr int kLdsNodeBytes32 = 88 * 1024;     // LDS for nodes when 32 feature slots
 constexpr uint32_t kInternal = 0x80000000u;
 
 __device__ __forceinline__ double leaf_value(uint64_t nd) { return __longlong_as_double((long long)nd); }
@@ -179,100 +177,188 @@ __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__
     }
 }
 
+// Scoring rows in CUSTOMER-grouped order, written whole (64-byte coalesced rows): row i
+// holds the transaction r = cust_perm[i]; amount / time flags / customer windows are
+// already in this order, the terminal half is one packed record read from
+// term_rec[term_inv[r]] (term_inv: row -> terminal-grouped or send position).
+template <int FS>
+__global__ void __launch_bounds__(256) k_zfill_grouped(
+    const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
+    const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
+    const int64_t *__restrict__ term_rec, int64_t n, int32_t W, int32_t flags_mode,
+    const double *__restrict__ mean, const double *__restrict__ scale, float *__restrict__ z,
+    int32_t *__restrict__ nan_flag) {
+    constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
+    const int words = (W + 1) / 2 + W;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float v[FS];
+#pragma unroll
+        for (int f = 0; f < FS; ++f) v[f] = 0.0f;
+        const int64_t t = cts[i];
+        int64_t day = t / kDay;
+        if (t % kDay != 0 && t < 0) --day;
+        const int64_t hour = (t - day * kDay) / kHour;
+        int64_t wd = (day + 3) % 7;
+        if (wd < 0) wd += 7;
+        const bool we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
+        const bool ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+        v[0] = zval(camt[i], mean, scale, 0);
+        v[1] = zval((double)we, mean, scale, 1);
+        v[2] = zval((double)ni, mean, scale, 2);
+        bool nan = v[0] != v[0];
+        const int64_t q = term_inv[cust_perm[i]];
+        const int64_t *rec = term_rec + q * words;
+        const int32_t *r32 = reinterpret_cast<const int32_t *>(rec);
+#pragma unroll
+        for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+            if (w < W) {
+                v[3 + 2 * w] = zval((double)cnb[(int64_t)w * n + i], mean, scale, 3 + 2 * w);
+                v[4 + 2 * w] = zval(cval[(int64_t)w * n + i], mean, scale, 4 + 2 * w);
+                v[3 + 2 * W + 2 * w] = zval((double)r32[w], mean, scale, 3 + 2 * W + 2 * w);
+                v[4 + 2 * W + 2 * w] = zval(__longlong_as_double(rec[(W + 1) / 2 + w]), mean, scale, 4 + 2 * W + 2 * w);
+                nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
+            }
+        }
+        if (nan) *nan_flag = 1;
+        float4 *dst = reinterpret_cast<float4 *>(z + i * FS);
+#pragma unroll
+        for (int qd = 0; qd < FS / 4; ++qd) dst[qd] = make_float4(v[4 * qd], v[4 * qd + 1], v[4 * qd + 2], v[4 * qd + 3]);
+    }
+}
+
 template <bool LDS>
 __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char *gbase, uint32_t byte_off) {
     if (LDS) return *reinterpret_cast<const uint64_t *>(reinterpret_cast<const char *>(s_nodes) + byte_off);
     return *reinterpret_cast<const uint64_t *>(gbase + byte_off);
 }
 
-// One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Each lane walks G trees of
-// one row at once.  A step is branch-free (leaves are fixed points), all G feature reads are
-// issued together, then all G node reads, so a lane keeps G LDS reads in flight; a group
-// of G trees runs exactly max(depth) steps, so the loop is uniform across the wave.
-// NaN routing (missing_go_to_left) costs 3 extra VALU per step: it is compiled in a second
-// loop that runs only when the prepare step saw a NaN feature (*nan_flag != 0).
-template <bool NAN_AWARE, bool LDS>
-__device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *s_xcol,
-                                           uint32_t (&p)[kG], uint64_t (&nd)[kG], int depth) {
+// Kernel variants (block size, rows per lane R, trees per walk group G).  LDS holds the
+// row features [FS][BLOCK*R] float32 and, in the rest of the 160 KiB, the chunk's nodes.
+struct Variant {
+    int block, rows, group;
+};
+constexpr Variant kVariants[] = {{512, 1, 4}, {1024, 1, 4}, {512, 2, 4}, {512, 2, 2}, {256, 2, 4}};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
+
+constexpr int lds_node_bytes(int fs, int block, int rows) { return kLdsTotal - fs * block * rows * 4; }
+
+// One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Each lane walks G trees
+// for each of its R rows at once (R*G independent chains).  A step is branch-free (leaves
+// are fixed points); all feature reads of a step are issued together, then all node reads,
+// so a lane keeps R*G LDS reads in flight; a walk group runs exactly max(depth) steps, so
+// the loop is uniform across the wave.  NaN routing (missing_go_to_left) costs 3 extra
+// VALU per step: it is compiled in a second loop that runs only when the prepare step saw
+// a NaN feature (*nan_flag != 0).
+template <bool NAN_AWARE, bool LDS, int BLOCK, int K>
+__device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
+                                           uint32_t (&p)[K], uint64_t (&nd)[K], int depth) {
     for (int d = 0; d < depth; ++d) {
-        float x[kG];
+        float x[K];
 #pragma unroll
-        for (int g = 0; g < kG; ++g) {
-            const uint32_t hi = (uint32_t)(nd[g] >> 32);
-            x[g] = s_xcol[((hi >> 24) & 63u) * kFBlock];
+        for (int k = 0; k < K; ++k) {
+            const uint32_t hi = (uint32_t)(nd[k] >> 32);
+            x[k] = xcol[k][((hi >> 24) & 63u) * (BLOCK * (K > 0 ? 1 : 1))];
         }
 #pragma unroll
-        for (int g = 0; g < kG; ++g) {
-            const uint32_t hi = (uint32_t)(nd[g] >> 32);
-            bool left = x[g] <= __uint_as_float((uint32_t)nd[g]);
-            if (NAN_AWARE) left = left | ((x[g] != x[g]) & ((hi >> 30) & 1u));
+        for (int k = 0; k < K; ++k) {
+            const uint32_t hi = (uint32_t)(nd[k] >> 32);
+            bool left = x[k] <= __uint_as_float((uint32_t)nd[k]);
+            if (NAN_AWARE) left = left | ((x[k] != x[k]) & ((hi >> 30) & 1u));
             const uint32_t step = left ? 8u : (hi & 0xFFFFFFu);
-            p[g] += step & (uint32_t)((int32_t)hi >> 31);
+            p[k] += step & (uint32_t)((int32_t)hi >> 31);
         }
 #pragma unroll
-        for (int g = 0; g < kG; ++g) nd[g] = node_at<LDS>(s_nodes, gbase, p[g]);
+        for (int k = 0; k < K; ++k) nd[k] = node_at<LDS>(s_nodes, gbase, p[k]);
     }
 }
 
-template <int FS, bool LDS>
-__global__ void __launch_bounds__(kFBlock) k_forest_chunk(
+template <int FS, bool LDS, int BLOCK, int R, int G>
+__global__ void __launch_bounds__(BLOCK) k_forest_chunk(
     const uint64_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes,
     const int32_t *__restrict__ root, const int32_t *__restrict__ depth, int32_t t0, int32_t t1,
     const float *__restrict__ z, const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1,
-    double *__restrict__ acc, double *__restrict__ proba, int32_t *__restrict__ leaf_out,
-    const int32_t *__restrict__ orig, int32_t n_trees, int first, int last) {
-    constexpr int kNodeCap = (LDS ? (FS == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) : 8) / 8;
+    double *__restrict__ acc, double *__restrict__ proba, const int32_t *__restrict__ out_perm,
+    int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig, int32_t n_trees, int first, int last) {
+    constexpr int kNodeCap = LDS ? lds_node_bytes(FS, BLOCK, R) / 8 : 1;
+    constexpr int K = R * G;
+    constexpr int kRowsPerBlock = BLOCK * R;
     __shared__ uint64_t s_nodes[kNodeCap];
-    __shared__ float s_x[FS][kFBlock];
+    __shared__ float s_x[FS][kRowsPerBlock];
     const int tid = threadIdx.x;
     const uint64_t *nb = nodes + node_base;
     const char *gbase = reinterpret_cast<const char *>(nb);
     const bool any_nan = *nan_flag != 0;  // uniform
     if (LDS) {
-        for (int i = tid; i < chunk_nodes; i += kFBlock) s_nodes[i] = nb[i];
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_nodes[i] = nb[i];
         __syncthreads();
     }
-    const float *s_xcol = &s_x[0][tid];
-    for (int64_t row = r0 + (int64_t)blockIdx.x * kFBlock + tid; row < r1;
-         row += (int64_t)gridDim.x * kFBlock) {
-        const float4 *src = reinterpret_cast<const float4 *>(z + row * FS);
+    // walk k = r*G + g reads the features of row slot r
+    const float *xcol[K];
 #pragma unroll
-        for (int q = 0; q < FS / 4; ++q) {
-            float4 v = src[q];
-            s_x[4 * q + 0][tid] = v.x;
-            s_x[4 * q + 1][tid] = v.y;
-            s_x[4 * q + 2][tid] = v.z;
-            s_x[4 * q + 3][tid] = v.w;
+    for (int k = 0; k < K; ++k) xcol[k] = &s_x[0][(k / G) * BLOCK + tid];
+    for (int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock; base < r1;
+         base += (int64_t)gridDim.x * kRowsPerBlock) {
+        int64_t row[R];
+        bool ok[R];
+        double a[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            row[r] = base + r * BLOCK + tid;
+            ok[r] = row[r] < r1;
+            const float4 *src = reinterpret_cast<const float4 *>(z + (ok[r] ? row[r] : r0) * FS);
+#pragma unroll
+            for (int q = 0; q < FS / 4; ++q) {
+                float4 v = src[q];
+                s_x[4 * q + 0][r * BLOCK + tid] = v.x;
+                s_x[4 * q + 1][r * BLOCK + tid] = v.y;
+                s_x[4 * q + 2][r * BLOCK + tid] = v.z;
+                s_x[4 * q + 3][r * BLOCK + tid] = v.w;
+            }
+            a[r] = (first || !ok[r]) ? 0.0 : acc[row[r]];
         }
-        double a = first ? 0.0 : acc[row];
-        for (int t = t0; t < t1; t += kG) {
-            uint32_t p[kG];
-            uint64_t nd[kG];
+        for (int t = t0; t < t1; t += G) {
+            uint32_t p[K];
+            uint64_t nd[K];
             int dmax = 0;
 #pragma unroll
-            for (int g = 0; g < kG; ++g) {
-                // inactive walk slots sit on a leaf-like 0 word (a fixed point)
+            for (int g = 0; g < G; ++g) {
                 const bool act = t + g < t1;
-                p[g] = act ? (uint32_t)(root[t + g] - node_base) * 8u : 0u;
-                nd[g] = act ? node_at<LDS>(s_nodes, gbase, p[g]) : 0ull;
+                const uint32_t p0 = act ? (uint32_t)(root[t + g] - node_base) * 8u : 0u;
+                const uint64_t n0 = act ? node_at<LDS>(s_nodes, gbase, p0) : 0ull;  // inactive: leaf-like 0
                 dmax = act ? max(dmax, depth[t + g]) : dmax;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    p[r * G + g] = p0;
+                    nd[r * G + g] = n0;
+                }
             }
             if (any_nan)
-                walk_group<true, LDS>(s_nodes, gbase, s_xcol, p, nd, dmax);
+                walk_group<true, LDS, BLOCK, K>(s_nodes, gbase, xcol, p, nd, dmax);
             else
-                walk_group<false, LDS>(s_nodes, gbase, s_xcol, p, nd, dmax);
+                walk_group<false, LDS, BLOCK, K>(s_nodes, gbase, xcol, p, nd, dmax);
 #pragma unroll
-            for (int g = 0; g < kG; ++g) {
-                if (t + g < t1) {
-                    a += leaf_value(nd[g]);
-                    if (leaf_out) leaf_out[row * n_trees + t + g] = orig[node_base + (p[g] >> 3)];
+            for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (t + g < t1) {
+                        a[r] += leaf_value(nd[r * G + g]);
+                        if (leaf_out && ok[r])
+                            leaf_out[(out_perm ? (int64_t)out_perm[row[r]] : row[r]) * n_trees + t + g] =
+                                orig[node_base + (p[r * G + g] >> 3)];
+                    }
                 }
             }
         }
-        if (last)
-            proba[row] = a / (double)n_trees;
-        else
-            acc[row] = a;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!ok[r]) continue;
+            if (last)
+                proba[out_perm ? (int64_t)out_perm[row[r]] : row[r]] = a[r] / (double)n_trees;
+            else
+                acc[row[r]] = a[r];
+        }
     }
 }
 
@@ -394,6 +480,49 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
 }  // namespace
 }  // namespace fdx
 
+namespace fdx {
+namespace {
+int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
+
+// Cut the trees into chunks whose nodes fit the variant's LDS budget; whole groups of G trees
+// where more than G fit (a partial group idles walk slots); oversized trees run from global.
+void build_chunks(fdx_forest_s *F) {
+    const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
+    const int64_t cap_nodes = lds_node_bytes(F->zstride, v.block, v.rows) / 8;
+    const int G = variant_group(F);
+    const auto &off = F->node_offsets;
+    F->chunks.clear();
+    for (int32_t t = 0; t < F->n_trees;) {
+        fdx_forest_s::Chunk c;
+        c.t0 = t;
+        c.node_base = off[t];
+        if (off[t + 1] - off[t] > cap_nodes) {
+            c.t1 = t + 1;
+            c.in_lds = false;
+        } else {
+            int32_t u = t + 1;
+            while (u < F->n_trees && off[u + 1] - c.node_base <= cap_nodes) ++u;
+            if (u - t > G && (u - t) % G) u -= (u - t) % G;
+            c.t1 = u;
+            c.in_lds = true;
+        }
+        c.nodes = off[c.t1] - c.node_base;
+        F->chunks.push_back(c);
+        t = c.t1;
+    }
+}
+}  // namespace
+}  // namespace fdx
+
+extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(variant >= 0 && variant < kNumVariants, "variant must be in [0, %d)", kNumVariants);
+    FDX_REQUIRE(variant == 0 || F->zstride == 16, "variants > 0 need <= 16 features");
+    F->variant = variant;
+    build_chunks(F);
+    return FDX_OK;
+}
+
 extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, int32_t *orig_out,
                                int32_t *root_out) {
     std::vector<uint64_t> packed;
@@ -421,27 +550,8 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->n_features = d->n_features;
     F->zstride = d->n_features <= 16 ? 16 : 32;
     F->n_nodes = total;
-    const int64_t cap_nodes = (F->zstride == 16 ? kLdsNodeBytes16 : kLdsNodeBytes32) / 8;
-    for (int32_t t = 0; t < d->n_trees;) {
-        fdx_forest_s::Chunk c;
-        c.t0 = t;
-        c.node_base = d->node_offsets[t];
-        int64_t sz = d->node_offsets[t + 1] - d->node_offsets[t];
-        if (sz > cap_nodes) {
-            c.t1 = t + 1;
-            c.in_lds = false;
-        } else {
-            int32_t u = t + 1;
-            while (u < d->n_trees && d->node_offsets[u + 1] - c.node_base <= cap_nodes) ++u;
-            // keep whole groups of kG trees (a partial group idles walk slots)
-            if (u - t > kG && (u - t) % kG) u -= (u - t) % kG;
-            c.t1 = u;
-            c.in_lds = true;
-        }
-        c.nodes = d->node_offsets[c.t1] - c.node_base;
-        F->chunks.push_back(c);
-        t = c.t1;
-    }
+    F->node_offsets.assign(d->node_offsets, d->node_offsets + d->n_trees + 1);
+    build_chunks(F);
     hipStream_t st = as_stream(stream);
     auto fail = [&](hipError_t e, const char *what) {
         set_error("%s failed: %s", what, hipGetErrorString(e));
@@ -546,8 +656,8 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     return FDX_OK;
 }
 
-extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int32_t *leaf_d, void *ws,
-                                   size_t ws_bytes, void *stream) {
+static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32_t *out_perm_d,
+                           int32_t *leaf_d, void *ws, size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return FDX_OK;
@@ -564,24 +674,46 @@ extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int
     const size_t nc = F->chunks.size();
     for (int64_t s0 = 0; s0 < n; s0 += slab) {
         const int64_t s1 = std::min<int64_t>(n, s0 + slab);
-        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, kFBlock), 256 * 4);
         for (size_t c = 0; c < nc; ++c) {
             const auto &ch = F->chunks[c];
             const int first = c == 0, last = c + 1 == nc;
-#define FDX_LAUNCH_CHUNK(FS, L)                                                                        \
-    hipLaunchKernelGGL((k_forest_chunk<FS, L>), dim3(grid), dim3(kFBlock), 0, st, F->nodes_d, ch.node_base, \
-                       (int32_t)ch.nodes, F->root_d, F->depth_d, ch.t0, ch.t1, z, flag, s0, s1, acc, proba_d, \
-                       leaf_d, F->orig_d, F->n_trees, first, last)
-            if (F->zstride == 16) {
-                if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
+#define FDX_LAUNCH_CHUNK(FS, L, B, R, G)                                                                    \
+    do {                                                                                                    \
+        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), 256 * 4);    \
+        hipLaunchKernelGGL((k_forest_chunk<FS, L, B, R, G>), dim3(grid), dim3(B), 0, st, F->nodes_d,          \
+                           ch.node_base, (int32_t)ch.nodes, F->root_d, F->depth_d, ch.t0, ch.t1, z, flag, s0, s1, \
+                           acc, proba_d, out_perm_d, leaf_d, F->orig_d, F->n_trees, first, last);            \
+    } while (0)
+#define FDX_LAUNCH_VARIANT(L)                                                                               \
+    switch (F->zstride == 16 ? F->variant : -1) {                                                           \
+        case 0: FDX_LAUNCH_CHUNK(16, L, 512, 1, 4); break;                                                  \
+        case 1: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 4); break;                                                 \
+        case 2: FDX_LAUNCH_CHUNK(16, L, 512, 2, 4); break;                                                  \
+        case 3: FDX_LAUNCH_CHUNK(16, L, 512, 2, 2); break;                                                  \
+        case 4: FDX_LAUNCH_CHUNK(16, L, 256, 2, 4); break;                                                  \
+        default: FDX_LAUNCH_CHUNK(32, L, 512, 1, 4); break;                                                 \
+    }
+            if (ch.in_lds) {
+                FDX_LAUNCH_VARIANT(true);
             } else {
-                if (ch.in_lds) FDX_LAUNCH_CHUNK(32, true); else FDX_LAUNCH_CHUNK(32, false);
+                FDX_LAUNCH_VARIANT(false);
             }
+#undef FDX_LAUNCH_VARIANT
 #undef FDX_LAUNCH_CHUNK
             FDX_LAUNCHED("k_forest_chunk");
         }
     }
     return FDX_OK;
+}
+
+extern "C" int fdx_forest_traverse(fdx_forest F, int64_t n, double *proba_d, int32_t *leaf_d, void *ws,
+                                   size_t ws_bytes, void *stream) {
+    return forest_traverse(F, n, proba_d, nullptr, leaf_d, ws, ws_bytes, stream);
+}
+
+extern "C" int fdx_forest_traverse_perm(fdx_forest F, int64_t n, double *proba_d, const int32_t *out_perm_d,
+                                        int32_t *leaf_d, void *ws, size_t ws_bytes, void *stream) {
+    return forest_traverse(F, n, proba_d, out_perm_d, leaf_d, ws, ws_bytes, stream);
 }
 
 extern "C" int fdx_forest_predict(fdx_forest F, const double *X_d, int64_t n, int64_t row_stride,
@@ -670,5 +802,38 @@ extern "C" int fdx_forest_set_slab_rows(fdx_forest F, int64_t rows) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(rows >= 0, "rows < 0");
     F->slab_rows = rows;
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
+                                          const int64_t *cust_ts_d, const double *cust_amount_d,
+                                          const int32_t *cust_nb_d, const double *cust_avg_d,
+                                          const int32_t *cust_perm_d, const int32_t *term_inv_d,
+                                          const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
+    FDX_REQUIRE(flags_mode == FDX_FLAGS_NOTEBOOK || flags_mode == FDX_FLAGS_SPARK, "bad flags mode");
+    FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
+                3 + 4 * n_windows);
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && cust_perm_d && term_inv_d && term_rec_d,
+                "null pointer");
+    float *z;
+    double *acc;
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
+    const unsigned grid = stream_grid(n, 256);
+    if (F->zstride == 16)
+        hipLaunchKernelGGL(k_zfill_grouped<16>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
+                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, F->mean_d,
+                           F->scale_d, z, flag);
+    else
+        hipLaunchKernelGGL(k_zfill_grouped<32>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
+                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, F->mean_d,
+                           F->scale_d, z, flag);
+    FDX_LAUNCHED("k_zfill_grouped");
     return FDX_OK;
 }

@@ -491,6 +491,12 @@ __global__ void k_reply_assemble(const int64_t *__restrict__ reply, const int32_
     }
 }
 
+__global__ void k_invert_perm(const int32_t *__restrict__ perm, int64_t n, int32_t *__restrict__ inv) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        inv[perm[i]] = (int32_t)i;
+}
+
 template <typename T>
 static int launch_perm(bool gather, const void *src, const int32_t *perm, int64_t n, void *dst,
                        hipStream_t st) {
@@ -583,5 +589,14 @@ extern "C" int fdx_reply_assemble(const int64_t *reply_d, const int32_t *perm_d,
     hipLaunchKernelGGL(k_reply_assemble, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), reply_d,
                        perm_d, n, n_windows, X_d, ld, col0);
     FDX_LAUNCHED("k_reply_assemble");
+    return FDX_OK;
+}
+
+extern "C" int fdx_invert_perm(const int32_t *perm_d, int64_t n, int32_t *inv_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(perm_d && inv_d, "null pointer");
+    hipLaunchKernelGGL(k_invert_perm, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), perm_d, n, inv_d);
+    FDX_LAUNCHED("k_invert_perm");
     return FDX_OK;
 }

@@ -186,10 +186,26 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 //   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
 // Segments up to kTermLdsRows rows are staged in LDS (timestamps + prefix counts) with
 // coalesced loads; longer ones are searched in global memory (L2) instead.
+// Output either column-major (nb_out/risk_out [W][n]) or, when rec_out != nullptr, one packed
+// record per row: ceil(W/2) words of int32 count pairs, then W float64 risks (the layout of
+// the multi-GPU reply records, read back by fdx_forest_prepare_grouped).
+__device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, int64_t *rec_out, int64_t n,
+                                           int32_t n_win, int64_t row, int w, int32_t cnt, double risk) {
+    if (rec_out) {
+        const int words = (n_win + 1) / 2 + n_win;
+        int32_t *r32 = reinterpret_cast<int32_t *>(rec_out + row * words);
+        r32[w] = cnt;
+        rec_out[row * words + (n_win + 1) / 2 + w] = __double_as_longlong(risk);
+    } else {
+        nb_out[(int64_t)w * n + row] = cnt;
+        risk_out[(int64_t)w * n + row] = risk;
+    }
+}
+
 __global__ void __launch_bounds__(kTermBlock) k_terminal(
     const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
-    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out) {
+    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out) {
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
     __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
     const int lane = threadIdx.x & (kWave - 1);
@@ -228,8 +244,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                     const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
                     const int32_t cnt = (int32_t)(hi - lo);
                     const int32_t fr = fhi - lf[lo];
-                    nb_out[(int64_t)w * n + b + i] = cnt;
-                    risk_out[(int64_t)w * n + b + i] = cnt > 0 ? (double)fr / (double)cnt : 0.0;
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, w, cnt,
+                               cnt > 0 ? (double)fr / (double)cnt : 0.0);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -246,8 +262,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                     int32_t fr = 0;
                     for (int64_t j = lo; j < hi; ++j) fr += gf[j] != 0;
                     const int32_t cnt = (int32_t)(hi - lo);
-                    nb_out[(int64_t)w * n + b + i] = cnt;
-                    risk_out[(int64_t)w * n + b + i] = cnt > 0 ? (double)fr / (double)cnt : 0.0;
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, w, cnt,
+                               cnt > 0 ? (double)fr / (double)cnt : 0.0);
                 }
             }
         }
@@ -349,7 +365,26 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
-                       fraud_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d);
+                       fraud_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, (int64_t *)nullptr);
+    FDX_LAUNCHED("k_terminal");
+    return FDX_OK;
+}
+
+extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                           const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                           int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
+                                           int64_t *rec_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(delay_ns > 0, "delay must be > 0 ns");
+    FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && rec_d, "null pointer");
+    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
+    hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
+                       seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
+                       rec_d);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
 }

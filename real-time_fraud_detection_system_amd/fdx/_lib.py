@@ -48,6 +48,8 @@ SIGNATURES = {
     "fdx_customer_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_terminal_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_assemble_features": (ctypes.c_int, [c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_i64, P]),
+    "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
+    "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),
     "fdx_rekey": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, c_sz, P]),
     "fdx_argsort_i64_workspace_size": (c_sz, [c_i64]),
@@ -70,7 +72,10 @@ SIGNATURES = {
     "fdx_forest_prepare": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, c_sz, P]),
     "fdx_forest_traverse": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),
     "fdx_forest_prepare_features": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
+    "fdx_forest_prepare_grouped": (ctypes.c_int, [P, c_i64, c_i32, c_i32, P, P, P, P, P, P, P, P, c_sz, P]),
+    "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
     "fdx_forest_set_slab_rows": (ctypes.c_int, [P, c_i64]),
+    "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
     "fdx_forest_prepare_reply": (ctypes.c_int, [P, P, P, c_i64, c_i32, c_i32, P, c_sz, P]),
 }
 

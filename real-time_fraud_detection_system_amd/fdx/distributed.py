@@ -132,28 +132,24 @@ class ShardedPipeline:
         return X[:, : p.n_features]
 
     def run(self, ts, customer, terminal, amount, fraud, n_customers_total, proba, ws, events=None):
-        """featurize + score this rank's rows; features go straight into the forest's
-        float32 rows (customer half before the exchange, terminal half from the replies)."""
+        """featurize + score this rank's rows (customer-grouped scoring rows; the terminal
+        half comes back from the owners as packed reply records)."""
         p = self.pipe
-        W = len(p.windows_days)
         n_local = n_customers_total // self.world
-        from .pipeline import Features
-
-        we, ni = ops.time_flags(ts, p.flags_mode)
         base = self.rank * n_local if self.customer_base is None else self.customer_base
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         cperm, cseg, _ = ops.rekey(cust, n_local)
-        cnb, cavg = ops.customer_windows(ops.gather(ts, cperm), ops.gather(amount, cperm), cseg, p.windows_days)
-        f = Features(we, ni, cperm, cseg, cnb, cavg, None, None, None, None)
-        ops.forest_prepare_features(p.forest, f, amount, ws, W, with_terminal=False)
+        cts, camt = ops.gather(ts, cperm), ops.gather(amount, cperm)
+        cnb, cavg = ops.customer_windows(cts, camt, cseg, p.windows_days)
         back, send_perm = exchange_terminal_features(GpuKernels, ts, terminal, fraud, self.world,
                                                      self.n_terminals_total, p.windows_days, p.delay_days,
                                                      self.group)
-        ops.forest_prepare_reply(p.forest, back, send_perm, W, 3 + 2 * W, ws)
+        sinv = ops.invert_perm(send_perm)
+        ops.forest_prepare_grouped(p.forest, p.flags_mode, cts, camt, cnb, cavg, cperm, sinv, back, ws)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-        ops.forest_traverse(self.pipe.forest, ts.numel(), ws, proba)
+        ops.forest_traverse_perm(p.forest, ts.numel(), ws, proba, cperm)
         if events is not None:
             b.record()
             events.append((a, b))

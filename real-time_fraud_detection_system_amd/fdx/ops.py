@@ -160,6 +160,25 @@ def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30
     return nb, risk
 
 
+def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), stream=None):
+    """Grouped rows -> packed records int64 [n, ceil(W/2)+W] (counts, then float64 risks)."""
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
+    n = ts_ns.numel()
+    W = len(windows_days)
+    rec = torch.empty((n, (W + 1) // 2 + W), dtype=torch.int64, device=ts_ns.device)
+    check(_lib.load().fdx_terminal_windows_packed(_ptr(ts_ns), _ptr(fraud), _ptr(seg_off), seg_off.numel() - 1, n,
+                                                  int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W,
+                                                  _ptr(rec), _s(stream)), "fdx_terminal_windows_packed")
+    return rec
+
+
+def invert_perm(perm: torch.Tensor, stream=None) -> torch.Tensor:
+    _dev(perm, torch.int32, "perm")
+    inv = torch.empty_like(perm)
+    check(_lib.load().fdx_invert_perm(_ptr(perm), perm.numel(), _ptr(inv), _s(stream)), "fdx_invert_perm")
+    return inv
+
+
 # ----------------------------------------------------------------------------- scale
 def standard_scale(X: torch.Tensor, mean: torch.Tensor | None, scale: torch.Tensor | None, stream=None):
     """(X - mean) / scale in float64; X is a 2-D float64 GPU tensor (any strides)."""
@@ -212,6 +231,14 @@ class Forest:
             _lib._lib.fdx_forest_destroy(h)
             self._h = None
 
+    def set_variant(self, variant: int) -> None:
+        L = _lib.load()
+        check(L.fdx_forest_set_variant(self._h, int(variant)), "fdx_forest_set_variant")
+        nt, nf, nn, nc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+        check(L.fdx_forest_info(self._h, ctypes.byref(nt), ctypes.byref(nf), ctypes.byref(nn), ctypes.byref(nc)))
+        self.n_chunks = nc.value
+        self.variant = int(variant)
+
     def set_slab_rows(self, rows: int) -> None:
         check(_lib.load().fdx_forest_set_slab_rows(self._h, int(rows)), "fdx_forest_set_slab_rows")
         self.slab_rows = int(rows)
@@ -260,6 +287,21 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
                          ws: torch.Tensor, stream=None):
     check(_lib.load().fdx_forest_prepare_reply(forest._h, _ptr(reply), _ptr(perm), perm.numel(), W, col0,
                                                _ptr(ws), ws.numel(), _s(stream)), "fdx_forest_prepare_reply")
+
+
+def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
+                           ws: torch.Tensor, stream=None):
+    n, W = cts.numel(), cnb.shape[0]
+    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), _ptr(cts), _ptr(camt), _ptr(cnb),
+                                                 _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),
+                                                 ws.numel(), _s(stream)), "fdx_forest_prepare_grouped")
+
+
+def forest_traverse_perm(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, out_perm: torch.Tensor,
+                         stream=None):
+    check(_lib.load().fdx_forest_traverse_perm(forest._h, n, _ptr(out), _ptr(out_perm), None, _ptr(ws), ws.numel(),
+                                               _s(stream)), "fdx_forest_traverse_perm")
+    return out
 
 
 def forest_traverse(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, stream=None):

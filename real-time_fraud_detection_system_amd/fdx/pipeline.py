@@ -103,14 +103,21 @@ class FraudPipeline:
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
                   proba: torch.Tensor, ws: torch.Tensor, stream=None, on_traverse=None):
-        """The scoring path without the float64 feature matrix: window outputs are scaled
-        straight into the forest's float32 rows (fdx_forest_prepare_features)."""
-        f = self.featurize(ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals, False,
-                           False, stream)
-        ops.forest_prepare_features(self.forest, f, amount, ws, len(self.windows_days), True, stream)
+        """The scoring path of bench.py: no float64 feature matrix.  Rows are scored in
+        customer-grouped order (customer half already in place, terminal half one packed
+        record per row), and proba is scattered back to input order by the last launch."""
+        W = len(self.windows_days)
+        cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
+        cts, camt = ops.gather(ts_ns, cperm, stream), ops.gather(amount, cperm, stream)
+        cnb, cavg = ops.customer_windows(cts, camt, cseg, self.windows_days, stream)
+        tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
+        trec = ops.terminal_windows_packed(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
+                                           tseg, self.delay_days, self.windows_days, stream)
+        tinv = ops.invert_perm(tperm, stream)
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, cts, camt, cnb, cavg, cperm, tinv, trec, ws, stream)
         if on_traverse:
             on_traverse(0)
-        ops.forest_traverse(self.forest, amount.numel(), ws, proba, stream)
+        ops.forest_traverse_perm(self.forest, amount.numel(), ws, proba, cperm, stream)
         if on_traverse:
             on_traverse(1)
         return proba

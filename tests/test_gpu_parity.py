@@ -145,6 +145,15 @@ def test_windows_random_edge_cases(dev, max_len):
         onb, orisk = oracle.terminal_windows(ts, fr, seg, 7, windows)
         np.testing.assert_array_equal(nb, onb)
         np.testing.assert_array_equal(risk, orisk)
+        rec = ops.terminal_windows_packed(T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev),
+                                          7, windows).cpu().numpy()
+        W = len(windows)
+        cnt = rec[:, : (W + 1) // 2].copy().view(np.int32)[:, :W]
+        np.testing.assert_array_equal(cnt.T, onb)
+        np.testing.assert_array_equal(rec[:, (W + 1) // 2:].copy().view(np.float64).T, orisk)
+        perm = np.random.default_rng(W).permutation(len(ts)).astype(np.int32)
+        inv = ops.invert_perm(T(perm, torch.int32, dev)).cpu().numpy()
+        np.testing.assert_array_equal(inv[perm], np.arange(len(ts)))
 
 
 # ---------------------------------------------------------------------------- forest
