@@ -70,6 +70,28 @@ int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount_d, const i
                          int64_t n_seg, int64_t n, const int64_t *window_ns, int32_t n_windows,
                          int32_t *nb_d, double *avg_d, void *stream);
 
+/* Scoring-pipeline layout of the customer windows (coalesced form of the same arithmetic):
+ * segments ordered by decreasing length (sorder_d [n_seg]) and cut into groups of
+ * S = 64 / n_windows; group g owns slots [goff_d[g], goff_d[g+1]) and row t of its l-th
+ * segment is slot goff_d[g] + t*S + l.  fdx_customer_layout fills its_d / iamt_d (ts and
+ * amount per slot) and irow_d (time-order row of each slot, -1 = padding) from the
+ * time-ordered ts/amount through cperm_d (fdx_rekey output), writes the slot count to
+ * *n_slots_h (host; this call synchronises the stream once) and fails with
+ * FDX_E_WORKSPACE if it exceeds max_slots (it is at most n + (S-1)*max segment length).
+ * goff_d needs n_groups+1 = ceil(n_seg/S)+1 entries. */
+size_t fdx_customer_layout_workspace_size(int64_t n_seg);
+int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                        const int64_t *ts_d, const double *amount_d, int32_t n_windows,
+                        int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                        int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *workspace_d,
+                        size_t workspace_bytes, void *stream);
+/* fdx_customer_windows over that layout: nb_d/avg_d are [W][n_slots] indexed by slot. */
+int fdx_customer_windows_interleaved(const int64_t *its_d, const double *iamt_d,
+                                     const int64_t *seg_off_d, const int32_t *sorder_d,
+                                     const uint32_t *goff_d, int64_t n_seg, int64_t n_slots,
+                                     const int64_t *window_ns, int32_t n_windows, int32_t *nb_d,
+                                     double *avg_d, void *stream);
+
 /* ---- a-3: terminal delayed-risk windows -----------------------------------------------
  * Replaces get_count_risk_rolling_window(terminal_transactions, delay_period,
  * windows_size_in_days, feature) (feature_transformation.ipynb:1495-1522) applied through
@@ -126,6 +148,10 @@ int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *wor
                     size_t workspace_bytes, void *stream);
 /* *flag_d = 1 if keys_d is non-decreasing, else 0 (stream-ordered). */
 int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream);
+
+/* Device-wide exclusive prefix sum of m uint32 values, in place. */
+size_t fdx_exclusive_scan_u32_workspace_size(int64_t m);
+int fdx_exclusive_scan_u32(uint32_t *data_d, int64_t m, void *workspace_d, void *stream);
 
 /* inv_d[perm_d[i]] = i */
 int fdx_invert_perm(const int32_t *perm_d, int64_t n, int32_t *inv_d, void *stream);
@@ -248,7 +274,9 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
  * is the packed record term_rec[term_inv[r]] (fdx_terminal_windows_packed output with
  * term_inv = inverse of the terminal perm, or the multi-GPU reply records with term_inv =
  * inverse of the send perm).  Follow with fdx_forest_traverse_perm(out_perm = cust_perm)
- * so that proba lands in row order. */
+ * so that proba lands in row order.  The same call serves the interleaved customer layout
+ * (cust_* = slot arrays, cust_perm = irow): slots with cust_perm < 0 are padding (zero
+ * row, never written back). */
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
                                const int64_t *cust_ts_d, const double *cust_amount_d,
                                const int32_t *cust_nb_d, const double *cust_avg_d,

@@ -195,6 +195,13 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         float v[FS];
 #pragma unroll
         for (int f = 0; f < FS; ++f) v[f] = 0.0f;
+        const int32_t r = cust_perm[i];
+        if (r < 0) {  // padding slot of the interleaved layout
+            float4 *dst = reinterpret_cast<float4 *>(z + i * FS);
+#pragma unroll
+            for (int qd = 0; qd < FS / 4; ++qd) dst[qd] = make_float4(0.f, 0.f, 0.f, 0.f);
+            continue;
+        }
         const int64_t t = cts[i];
         int64_t day = t / kDay;
         if (t % kDay != 0 && t < 0) --day;
@@ -207,7 +214,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         v[1] = zval((double)we, mean, scale, 1);
         v[2] = zval((double)ni, mean, scale, 2);
         bool nan = v[0] != v[0];
-        const int64_t q = term_inv[cust_perm[i]];
+        const int64_t q = term_inv[r];
         const int64_t *rec = term_rec + q * words;
         const int32_t *r32 = reinterpret_cast<const int32_t *>(rec);
 #pragma unroll
@@ -344,9 +351,10 @@ __global__ void __launch_bounds__(BLOCK) k_forest_chunk(
                 for (int g = 0; g < G; ++g) {
                     if (t + g < t1) {
                         a[r] += leaf_value(nd[r * G + g]);
-                        if (leaf_out && ok[r])
-                            leaf_out[(out_perm ? (int64_t)out_perm[row[r]] : row[r]) * n_trees + t + g] =
-                                orig[node_base + (p[r * G + g] >> 3)];
+                        if (leaf_out && ok[r]) {
+                            const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+                            if (dst >= 0) leaf_out[dst * n_trees + t + g] = orig[node_base + (p[r * G + g] >> 3)];
+                        }
                     }
                 }
             }
@@ -354,10 +362,12 @@ __global__ void __launch_bounds__(BLOCK) k_forest_chunk(
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!ok[r]) continue;
-            if (last)
-                proba[out_perm ? (int64_t)out_perm[row[r]] : row[r]] = a[r] / (double)n_trees;
-            else
+            if (last) {
+                const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+                if (dst >= 0) proba[dst] = a[r] / (double)n_trees;  // < 0: padding slot
+            } else {
                 acc[row[r]] = a[r];
+            }
         }
     }
 }

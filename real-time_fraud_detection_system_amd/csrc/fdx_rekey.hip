@@ -600,3 +600,14 @@ extern "C" int fdx_invert_perm(const int32_t *perm_d, int64_t n, int32_t *inv_d,
     FDX_LAUNCHED("k_invert_perm");
     return FDX_OK;
 }
+
+extern "C" size_t fdx_exclusive_scan_u32_workspace_size(int64_t m) {
+    return sizeof(uint32_t) * (size_t)(scan_partials_count(m) + 1) + 256;
+}
+
+extern "C" int fdx_exclusive_scan_u32(uint32_t *data_d, int64_t m, void *workspace_d, void *stream) {
+    FDX_REQUIRE(m >= 0, "m < 0");
+    if (m == 0) return FDX_OK;
+    FDX_REQUIRE(data_d && workspace_d, "null pointer");
+    return exclusive_scan(data_d, m, reinterpret_cast<uint32_t *>(workspace_d), as_stream(stream));
+}

@@ -154,6 +154,112 @@ __global__ void __launch_bounds__(256) k_customer_exact(
     }
 }
 
+// ------------------------------------------------- customer windows, interleaved layout
+// The scoring pipeline's customer layout ("lane-major"): segments are ordered by length
+// (longest first) and cut into groups of S = 64 / W segments; group g owns S * L_g slots
+// (L_g = its longest segment) starting at goff[g], and row t of the group's segment l sits
+// in slot goff[g] + t*S + l.  One wave walks one group: lane k = (segment l = k / W,
+// window w = k % W) runs the exact pandas recurrence of its segment while the W lanes of a
+// segment share every head load, and every wave instruction touches S consecutive slots
+// (coalesced) instead of 64 unrelated streams.  Outputs use the same slot index; slots
+// past a segment's end are padding (row index -1).
+
+// key = LMAX - min(len, LMAX): a stable sort by it orders segments by decreasing length
+__global__ void k_seg_len_keys(const int64_t *__restrict__ seg_off, int64_t n_seg, int32_t lmax,
+                               int32_t *__restrict__ key) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t L = seg_off[s + 1] - seg_off[s];
+        key[s] = lmax - (int32_t)(L < lmax ? L : lmax);
+    }
+}
+
+// slots of group g = S * length of its first (longest) segment
+__global__ void k_group_slots(const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
+                              int64_t n_seg, int32_t S, int64_t n_groups, uint32_t *__restrict__ gslots) {
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = sorder[g * S];
+        gslots[g] = (uint32_t)(S * (seg_off[s + 1] - seg_off[s]));
+    }
+}
+
+// one block per group: slot (t, l) <- time-order row r = cperm[seg_off[s] + t]
+__global__ void __launch_bounds__(256) k_interleave(
+    const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder, const int32_t *__restrict__ cperm,
+    const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, const int64_t *__restrict__ ts,
+    const double *__restrict__ amount, int64_t *__restrict__ its, double *__restrict__ iamt,
+    int32_t *__restrict__ irow) {
+    const int64_t g = blockIdx.x;
+    const int rows_per_iter = blockDim.x / S;
+    const int l = threadIdx.x % S, tt = threadIdx.x / S;
+    if (tt >= rows_per_iter) return;
+    const int64_t si = g * S + l;
+    const int64_t s = si < n_seg ? sorder[si] : -1;
+    const int64_t b = s >= 0 ? seg_off[s] : 0;
+    const int64_t L = s >= 0 ? seg_off[s + 1] - b : 0;
+    const int64_t s0 = sorder[g * S];
+    const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
+    const int64_t base = goff[g];
+    for (int64_t t = tt; t < Lg; t += rows_per_iter) {
+        const int64_t slot = base + t * S + l;
+        if (t < L) {
+            const int32_t r = cperm[b + t];
+            its[slot] = ts[r];
+            iamt[slot] = amount[r];
+            irow[slot] = r;
+        } else {
+            its[slot] = 0;
+            iamt[slot] = 0.0;
+            irow[slot] = -1;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_customer_interleaved(
+    const int64_t *__restrict__ its, const double *__restrict__ iamt, const int64_t *__restrict__ seg_off,
+    const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int64_t n_seg, int64_t n_groups,
+    int32_t S, int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out,
+    double *__restrict__ avg_out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t g = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    if (g >= n_groups) return;
+    const int l = lane / n_win, wi = lane - l * n_win;
+    const int64_t si = g * S + l;
+    if (l >= S || si >= n_seg) return;
+    const int64_t s = sorder[si];
+    const int64_t L = seg_off[s + 1] - seg_off[s];
+    const int64_t W = win.w[wi];
+    const int64_t base = goff[g] + l;
+    int32_t *nb = nb_out + (int64_t)wi * n_slots;
+    double *avg = avg_out + (int64_t)wi * n_slots;
+    RollSum st;
+    int64_t tail = 0;
+    for (int64_t t = 0; t < L; ++t) {
+        const int64_t slot = base + t * S;
+        const int64_t tv = its[slot];
+        const double v = iamt[slot];
+        if (t == 0) {
+            st.reset(v);
+            st.add(v);
+        } else {
+            const int64_t bound = tv - W;
+            int64_t nt = tail;
+            while (nt < t && its[base + nt * S] <= bound) ++nt;
+            if (nt >= t) {  // pandas re-initialises the window
+                st.reset(v);
+                st.add(v);
+            } else {
+                for (int64_t j = tail; j < nt; ++j) st.remove(iamt[base + j * S]);
+                st.add(v);
+            }
+            tail = nt;
+        }
+        nb[slot] = st.nobs;
+        avg[slot] = st.value() / (double)st.nobs;
+    }
+}
+
 // ------------------------------------------------------------------ terminal windows
 constexpr int kTermBlock = 256;
 constexpr int kTermWaves = kTermBlock / kWave;
@@ -413,5 +519,78 @@ extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double 
                            n, n_windows, X_d, ld, 3 + 2 * n_windows);
         FDX_LAUNCHED("k_assemble_group");
     }
+    return FDX_OK;
+}
+
+static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+extern "C" size_t fdx_customer_layout_workspace_size(int64_t n_seg) {
+    if (n_seg < 0) n_seg = 0;
+    return al256((size_t)n_seg * 4) + al256((size_t)(65535 + 2) * 8) + fdx_rekey_workspace_size(n_seg, 16) +
+           fdx_exclusive_scan_u32_workspace_size(n_seg + 1) + 256;
+}
+
+extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                   const int64_t *ts_d, const double *amount_d, int32_t n_windows,
+                                   int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                                   int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                                   size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64, "bad argument");
+    FDX_REQUIRE(seg_off_d && cperm_d && ts_d && amount_d && sorder_d && goff_d && its_d && iamt_d && irow_d &&
+                    n_slots_h && ws,
+                "null pointer");
+    FDX_REQUIRE(ws_bytes >= fdx_customer_layout_workspace_size(n_seg), "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const int32_t S = kWave / n_windows;
+    const int64_t n_groups = ceil_div(n_seg, S);
+    const int32_t lmax = 65535;
+    char *w = reinterpret_cast<char *>(ws);
+    int32_t *keys = reinterpret_cast<int32_t *>(w);
+    w += al256((size_t)n_seg * 4);
+    int64_t *kseg = reinterpret_cast<int64_t *>(w);  // seg offsets of the length sort (unused)
+    w += al256((size_t)(lmax + 2) * 8);
+    hipLaunchKernelGGL(k_seg_len_keys, dim3(stream_grid(n_seg, 256)), dim3(256), 0, st, seg_off_d, n_seg, lmax, keys);
+    FDX_LAUNCHED("k_seg_len_keys");
+    const size_t rws = fdx_rekey_workspace_size(n_seg, 16);
+    int rc = fdx_rekey(keys, n_seg, 16, lmax + 1, sorder_d, nullptr, kseg, w, rws, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_group_slots, dim3(stream_grid(n_groups, 256)), dim3(256), 0, st, seg_off_d, sorder_d,
+                       n_seg, S, n_groups, goff_d);
+    FDX_LAUNCHED("k_group_slots");
+    // goff[0..n_groups] = exclusive scan of the slot counts (total in goff[n_groups])
+    FDX_HIP(hipMemsetAsync(goff_d + n_groups, 0, sizeof(uint32_t), st));
+    rc = fdx_exclusive_scan_u32(goff_d, n_groups + 1, w + rws, stream);
+    if (rc) return rc;
+    uint32_t total = 0;
+    FDX_HIP(hipMemcpyAsync(&total, goff_d + n_groups, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    FDX_HIP(hipStreamSynchronize(st));
+    *n_slots_h = total;
+    if ((int64_t)total > max_slots) {
+        set_error("interleaved layout needs %u slots > max_slots %lld", total, (long long)max_slots);
+        return FDX_E_WORKSPACE;
+    }
+    hipLaunchKernelGGL(k_interleave, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d, cperm_d,
+                       goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d);
+    FDX_LAUNCHED("k_interleave");
+    return FDX_OK;
+}
+
+extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const double *iamt_d,
+                                                const int64_t *seg_off_d, const int32_t *sorder_d,
+                                                const uint32_t *goff_d, int64_t n_seg, int64_t n_slots,
+                                                const int64_t *window_ns, int32_t n_windows, int32_t *nb_d,
+                                                double *avg_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(n_seg >= 0 && n_slots >= 0, "negative size");
+    if (n_seg == 0) return FDX_OK;
+    FDX_REQUIRE(its_d && iamt_d && seg_off_d && sorder_d && goff_d && nb_d && avg_d, "null pointer");
+    const int32_t S = kWave / n_windows;
+    const int64_t n_groups = ceil_div(n_seg, S);
+    hipLaunchKernelGGL(k_customer_interleaved, dim3((unsigned)ceil_div(n_groups, 4)), dim3(256), 0, as_stream(stream),
+                       its_d, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, n_groups, S, n_slots, wa, n_windows, nb_d,
+                       avg_d);
+    FDX_LAUNCHED("k_customer_interleaved");
     return FDX_OK;
 }

@@ -48,6 +48,11 @@ SIGNATURES = {
     "fdx_customer_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_terminal_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_assemble_features": (ctypes.c_int, [c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_i64, P]),
+    "fdx_customer_layout_workspace_size": (c_sz, [c_i64]),
+    "fdx_customer_layout": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),
+    "fdx_customer_windows_interleaved": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
+    "fdx_exclusive_scan_u32_workspace_size": (c_sz, [c_i64]),
+    "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
     "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),

@@ -160,6 +160,53 @@ def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30
     return nb, risk
 
 
+class CustomerLayout:
+    """The interleaved (lane-major) customer layout of the scoring pipeline (fdx.h)."""
+
+    def __init__(self, sorder, goff, its, iamt, irow, n_slots):
+        self.sorder, self.goff, self.its, self.iamt, self.irow, self.n_slots = sorder, goff, its, iamt, irow, n_slots
+
+
+def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, _slots_hint=None) -> CustomerLayout:
+    _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(amount, torch.float64, "amount")
+    n_seg = seg_off.numel() - 1
+    n = ts_ns.numel()
+    S = 64 // int(n_windows)
+    dev = ts_ns.device
+    L = _lib.load()
+    max_slots = int(_slots_hint or (n + S * 4096))
+    sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
+    goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
+    ws = workspace(L.fdx_customer_layout_workspace_size(n_seg), dev)
+    while True:
+        its = torch.empty(max_slots, dtype=torch.int64, device=dev)
+        iamt = torch.empty(max_slots, dtype=torch.float64, device=dev)
+        irow = torch.empty(max_slots, dtype=torch.int32, device=dev)
+        ns = ctypes.c_int64(0)
+        rc = L.fdx_customer_layout(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount), int(n_windows),
+                                   _ptr(sorder), _ptr(goff), _ptr(its), _ptr(iamt), _ptr(irow), max_slots,
+                                   ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
+        if rc == -4 and ns.value > max_slots:
+            max_slots = ns.value
+            continue
+        check(rc, "fdx_customer_layout")
+        return CustomerLayout(sorder, goff, its, iamt, irow, ns.value)
+
+
+def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 7, 30), stream=None):
+    """-> (nb int32 [W, n_slots], avg float64 [W, n_slots]) indexed by slot."""
+    W = len(windows_days)
+    dev = lay.its.device
+    nb = torch.empty((W, lay.n_slots), dtype=torch.int32, device=dev)
+    avg = torch.empty((W, lay.n_slots), dtype=torch.float64, device=dev)
+    check(_lib.load().fdx_customer_windows_interleaved(_ptr(lay.its), _ptr(lay.iamt), _ptr(seg_off), _ptr(lay.sorder),
+                                                       _ptr(lay.goff), seg_off.numel() - 1, lay.n_slots,
+                                                       _win_ns(windows_days), W, _ptr(nb), _ptr(avg), _s(stream)),
+          "fdx_customer_windows_interleaved")
+    return nb, avg
+
+
 def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), stream=None):
     """Grouped rows -> packed records int64 [n, ceil(W/2)+W] (counts, then float64 risks)."""
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
@@ -290,8 +337,9 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None):
-    n, W = cts.numel(), cnb.shape[0]
+                           ws: torch.Tensor, stream=None, n=None):
+    n = cts.numel() if n is None else int(n)
+    W = cnb.shape[0]
     check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), _ptr(cts), _ptr(camt), _ptr(cnb),
                                                  _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),
                                                  ws.numel(), _s(stream)), "fdx_forest_prepare_grouped")

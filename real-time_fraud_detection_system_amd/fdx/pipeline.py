@@ -47,6 +47,7 @@ class FraudPipeline:
         self.forest = forest
         self.n_features = 3 + 4 * len(self.windows_days)
         self._ws = None
+        self._slots_hint = None
 
     def featurize(self, ts_ns, customer, terminal, amount, fraud, n_customers: int, n_terminals: int,
                   assemble: bool = True, time_sort: bool = False, stream=None) -> Features:
@@ -102,25 +103,37 @@ class FraudPipeline:
         return f, self.score(f.X, stream=stream)
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
-                  proba: torch.Tensor, ws: torch.Tensor, stream=None, on_traverse=None):
-        """The scoring path of bench.py: no float64 feature matrix.  Rows are scored in
-        customer-grouped order (customer half already in place, terminal half one packed
-        record per row), and proba is scattered back to input order by the last launch."""
+                  proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, on_traverse=None):
+        """The scoring path of bench.py: no float64 feature matrix.  The customer half is
+        computed in the interleaved (lane-major) layout and the scoring rows follow that
+        layout (customer features already in place, the terminal half one packed record
+        per row); the last forest launch writes proba back in input row order."""
         W = len(self.windows_days)
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
-        cts, camt = ops.gather(ts_ns, cperm, stream), ops.gather(amount, cperm, stream)
-        cnb, cavg = ops.customer_windows(cts, camt, cseg, self.windows_days, stream)
+        lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
+        self._slots_hint = lay.its.numel()
+        inb, iavg = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
         trec = ops.terminal_windows_packed(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
                                            tseg, self.delay_days, self.windows_days, stream)
         tinv = ops.invert_perm(tperm, stream)
-        ops.forest_prepare_grouped(self.forest, self.flags_mode, cts, camt, cnb, cavg, cperm, tinv, trec, ws, stream)
+        ws = self._forest_ws(lay.n_slots, ws, amount.device)
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, iavg, lay.irow, tinv, trec,
+                                   ws, stream, n=lay.n_slots)
         if on_traverse:
             on_traverse(0)
-        ops.forest_traverse_perm(self.forest, amount.numel(), ws, proba, cperm, stream)
+        ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, stream)
         if on_traverse:
             on_traverse(1)
         return proba
+
+    def _forest_ws(self, n_rows, ws, device):
+        need = self.forest.workspace_size(n_rows)
+        if ws is not None and ws.numel() >= need:
+            return ws
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = ops.workspace(need, device)
+        return self._ws
 
 
 def _to_caller_order(f: Features, tperm: torch.Tensor, stream) -> Features:

@@ -267,3 +267,27 @@ def test_pipeline_large_sampled_segments(dev):
         names = oracle.CUSTOMER_COLS if key == "customer" else oracle.TERMINAL_COLS
         exp = np.stack([of[c] for c in names], axis=1)
         np.testing.assert_array_equal(X[m][:, cols], exp)
+
+
+@pytest.mark.parametrize("max_len,windows", [(300, (1, 7, 30)), (2500, (1, 7, 30)), (300, (2, 5)), (40, (3,))])
+def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
+    """The pipeline's lane-major customer layout: same bits as the oracle for every row."""
+    rng = np.random.default_rng(max_len + len(windows))
+    ts, amt, _, seg = _edge_segments(rng, 700 if max_len < 1000 else 60, max_len)
+    n = len(ts)
+    perm = rng.permutation(n).astype(np.int32)          # grouped position -> "time row"
+    ts_time = np.empty_like(ts); ts_time[perm] = ts
+    amt_time = np.empty_like(amt); amt_time[perm] = amt
+    lay = ops.customer_layout(T(seg, torch.int64, dev), T(perm, torch.int32, dev), T(ts_time, torch.int64, dev),
+                              T(amt_time, torch.float64, dev), len(windows))
+    nb, avg = ops.customer_windows_interleaved(lay, T(seg, torch.int64, dev), windows)
+    irow = lay.irow.cpu().numpy()[: lay.n_slots]
+    nb, avg = nb.cpu().numpy(), avg.cpu().numpy()
+    onb, oavg = oracle.customer_windows(ts, amt, seg, windows)
+    inv = np.empty(n, np.int64); inv[perm] = np.arange(n)   # time row -> grouped position
+    real = irow >= 0
+    assert real.sum() == n and len(np.unique(irow[real])) == n
+    g = inv[irow[real]]
+    np.testing.assert_array_equal(nb[:, real], onb[:, g])
+    np.testing.assert_array_equal(avg[:, real], oavg[:, g])
+    assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
