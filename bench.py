@@ -111,7 +111,7 @@ def main():
     ts, cust, term = T(data["ts"], torch.int64), T(data["customer"], torch.int32), T(data["terminal"], torch.int32)
     amt, fr = T(data["amount"], torch.float64), T(data["fraud"], torch.uint8)
     pipe = FraudPipeline(forest=forest)
-    ws = ops.workspace(forest.workspace_size(n_local), dev)
+    ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
     ev = []
 
@@ -212,17 +212,18 @@ def main():
         print(json.dumps({"slab_sweep_traverse_ms": res}), file=sys.stderr)
     if args.sweep_variant and rank == 0:
         res = {}
-        ref = proba.clone()
-        ops.forest_traverse(forest, n_local, ws, ref)
+        ws, n_rows = pipe._forest_ws(pipe.last_slots, ws, dev), pipe.last_slots
+        ref = torch.empty(n_rows, dtype=torch.float64, device=dev)
+        ops.forest_traverse(forest, n_rows, ws, ref)
         for v in [int(x) for x in args.sweep_variant.split(",")]:
             forest.set_variant(v)
-            out = torch.empty_like(proba)
-            ops.forest_traverse(forest, n_local, ws, out)
-            same = bool(torch.equal(out, ref))
+            pv = torch.empty_like(ref)
+            ops.forest_traverse(forest, n_rows, ws, pv)
+            same = bool(torch.equal(pv, ref))
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for _ in range(3):
-                ops.forest_traverse(forest, n_local, ws, out)
+                ops.forest_traverse(forest, n_rows, ws, pv)
             b.record()
             torch.cuda.synchronize()
             res[v] = {"ms": round(a.elapsed_time(b) / 3, 3), "chunks": forest.n_chunks, "bit_equal": same}
@@ -253,9 +254,9 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("start")
     cperm, cseg, _ = ops.rekey(cust, args.customers)
     mark("rekey_customer")
-    cts, camt = ops.gather(ts, cperm), ops.gather(amt, cperm)
-    mark("gather_customer")
-    cnb, cavg = ops.customer_windows(cts, camt, cseg)
+    lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
+    mark("customer_layout")
+    inb, iavg = ops.customer_windows_interleaved(lay, cseg)
     mark("customer_windows")
     tperm, tseg, _ = ops.rekey(term, args.terminals)
     mark("rekey_terminal")
@@ -265,13 +266,14 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("terminal_windows")
     tinv = ops.invert_perm(tperm)
     mark("invert_terminal_perm")
-    ops.forest_prepare_grouped(forest, 0, cts, camt, cnb, cavg, cperm, tinv, trec, ws)
+    wsb = pipe._forest_ws(lay.n_slots, ws, ts.device)
+    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, iavg, lay.irow, tinv, trec, wsb, n=lay.n_slots)
     mark("assemble_scale_z32")
-    ops.forest_traverse_perm(forest, n, ws, proba, cperm)
+    ops.forest_traverse_perm(forest, lay.n_slots, wsb, proba, lay.irow)
     mark("forest_traverse")
     torch.cuda.synchronize()
     return {"breakdown_ms": {marks[i][0]: round(marks[i - 1][1].elapsed_time(marks[i][1]), 4)
-                             for i in range(1, len(marks))}, "n": n}
+                             for i in range(1, len(marks))}, "n": n, "scoring_slots": lay.n_slots}
 
 
 if __name__ == "__main__":

@@ -258,7 +258,7 @@ constexpr int lds_node_bytes(int fs, int block, int rows) { return kLdsTotal - f
 // the loop is uniform across the wave.  NaN routing (missing_go_to_left) costs 3 extra
 // VALU per step: it is compiled in a second loop that runs only when the prepare step saw
 // a NaN feature (*nan_flag != 0).
-template <bool NAN_AWARE, bool LDS, int BLOCK, int K>
+template <bool NAN_AWARE, bool LDS, int XSTRIDE, int K>
 __device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
                                            uint32_t (&p)[K], uint64_t (&nd)[K], int depth) {
     for (int d = 0; d < depth; ++d) {
@@ -266,7 +266,7 @@ __device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t hi = (uint32_t)(nd[k] >> 32);
-            x[k] = xcol[k][((hi >> 24) & 63u) * (BLOCK * (K > 0 ? 1 : 1))];
+            x[k] = xcol[k][((hi >> 24) & 63u) * XSTRIDE];
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -342,9 +342,9 @@ __global__ void __launch_bounds__(BLOCK) k_forest_chunk(
                 }
             }
             if (any_nan)
-                walk_group<true, LDS, BLOCK, K>(s_nodes, gbase, xcol, p, nd, dmax);
+                walk_group<true, LDS, kRowsPerBlock, K>(s_nodes, gbase, xcol, p, nd, dmax);
             else
-                walk_group<false, LDS, BLOCK, K>(s_nodes, gbase, xcol, p, nd, dmax);
+                walk_group<false, LDS, kRowsPerBlock, K>(s_nodes, gbase, xcol, p, nd, dmax);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
 #pragma unroll

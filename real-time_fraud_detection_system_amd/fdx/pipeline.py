@@ -112,6 +112,7 @@ class FraudPipeline:
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
         lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
         self._slots_hint = lay.its.numel()
+        self.last_slots = lay.n_slots
         inb, iavg = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
         trec = ops.terminal_windows_packed(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),

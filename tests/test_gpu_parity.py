@@ -291,3 +291,24 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     np.testing.assert_array_equal(nb[:, real], onb[:, g])
     np.testing.assert_array_equal(avg[:, real], oavg[:, g])
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_forest_variants_bit_identical(dev, golden, variant):
+    """Every traversal kernel shape gives sklearn's leaves and probabilities."""
+    z = golden("forest_rf3.npz")
+    f = ops.Forest(_forest(z), 15, z["mean"], z["scale"])
+    f.set_variant(variant)
+    X = np.vstack([z["X"]] * 3)  # > one block of rows per lane slot
+    proba, leaves = f.predict(T(X, torch.float64, dev), want_leaves=True)
+    np.testing.assert_array_equal(leaves.cpu().numpy(), np.vstack([z["leaves"]] * 3))
+    np.testing.assert_array_equal(proba.cpu().numpy(), np.concatenate([z["proba"]] * 3))
+    rng = np.random.default_rng(variant)
+    arr = random_forest(rng, 24, 9)
+    Xr = rng.normal(size=(7000, 15))
+    g = ops.Forest(arr, 15)
+    g.set_variant(variant)
+    p, l = g.predict(T(Xr, torch.float64, dev), want_leaves=True)
+    op, ol = oracle.forest_predict(Xr, arr, want_leaves=True)
+    np.testing.assert_array_equal(l.cpu().numpy(), ol)
+    np.testing.assert_array_equal(p.cpu().numpy(), op)
