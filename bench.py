@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
     ap.add_argument("--slab-rows", type=int, default=0, help="forest traversal slab rows (0 = all rows)")
     ap.add_argument("--sweep-slab", default="", help="comma list of slab sizes to time (stderr)")
-    ap.add_argument("--forest-variant", type=int, default=0, help="traversal kernel shape (fdx_forest_set_variant)")
+    ap.add_argument("--forest-variant", type=int, default=1, help="traversal kernel shape (fdx_forest_set_variant)")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     return ap.parse_args()
 

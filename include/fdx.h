@@ -133,7 +133,7 @@ int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
  * keys_d[i] in [0, n_keys); key_bits = bits needed for n_keys-1 (<= 31).
  * Outputs: perm_d[j] = input row placed at grouped position j (stable: equal keys keep
  * input order), sorted_keys_d (optional, may be NULL), seg_off_d[0..n_keys] (CSR by key
- * value; empty keys get empty segments). */
+ * value; empty keys get empty segments; may be NULL when only the order is needed). */
 size_t fdx_rekey_workspace_size(int64_t n, int32_t key_bits);
 int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, int32_t *perm_d,
               int32_t *sorted_keys_d, int64_t *seg_off_d, void *workspace_d, size_t workspace_bytes,
@@ -247,8 +247,9 @@ int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *
 /* Rows per traversal slab (all chunks run over one slab before the next, so that the
  * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
 int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
-/* Traversal kernel shape: 0 = 512 threads x 1 row x 4 trees per lane (default), 1 = 1024 x 1
- * x 4, 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4 (variants > 0 need <= 16 features).
+/* Traversal kernel shape: 0 = 512 threads x 1 row x 4 trees per lane, 1 = 1024 x 1 x 4
+ * (default when <= 16 features), 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4
+ * (variants > 0 need <= 16 features).
  * Re-cuts the LDS chunks; results are identical for every variant. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
 

@@ -561,6 +561,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->zstride = d->n_features <= 16 ? 16 : 32;
     F->n_nodes = total;
     F->node_offsets.assign(d->node_offsets, d->node_offsets + d->n_trees + 1);
+    F->variant = F->zstride == 16 ? 1 : 0;  // r01 sweep: 1024 x 1 x 4 fastest on the config-3 forest
     build_chunks(F);
     hipStream_t st = as_stream(stream);
     auto fail = [&](hipError_t e, const char *what) {

@@ -243,15 +243,18 @@ __global__ void k_copy_u32(const uint32_t *__restrict__ in, uint32_t *__restrict
         out[i] = in[i];
 }
 
-// seg_off[q] = first sorted position whose key >= q, for q in [0, n_keys]
+// seg_off[q] = first sorted position whose key >= q, for q in [0, n_keys]: one binary
+// search per key value (balanced however sparse or skewed the keys are)
 __global__ void k_seg_offsets(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys,
                               int64_t *__restrict__ seg_off) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t lo = (i == 0) ? 0 : (int64_t)sk[i - 1] + 1;     // first key value owned here
-        int64_t hi = (i == n) ? n_keys : (int64_t)sk[i];        // last key value owned here
-        if (hi > n_keys) hi = n_keys;
-        for (int64_t q = lo; q <= hi; ++q) seg_off[q] = i;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n_keys;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)sk[mid] < q) lo = mid + 1; else hi = mid;
+        }
+        seg_off[q] = lo;
     }
 }
 
@@ -362,10 +365,9 @@ extern "C" int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     FDX_REQUIRE(key_bits >= 0 && key_bits <= 31, "key_bits must be in [0, 31]");
     FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
-    FDX_REQUIRE(seg_off_d, "null seg_off");
     hipStream_t st = as_stream(stream);
     if (n == 0) {
-        FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
+        if (seg_off_d) FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
         return FDX_OK;
     }
     FDX_REQUIRE(keys_d && perm_d, "null keys/perm");
@@ -385,9 +387,11 @@ extern "C" int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int
                            reinterpret_cast<uint32_t *>(sorted_keys_d), n);
         FDX_LAUNCHED("k_copy_u32");
     }
-    hipLaunchKernelGGL(k_seg_offsets, dim3(stream_grid(n + 1, 256)), dim3(256), 0, st, sorted, n, n_keys,
-                       seg_off_d);
-    FDX_LAUNCHED("k_seg_offsets");
+    if (seg_off_d) {
+        hipLaunchKernelGGL(k_seg_offsets, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, sorted, n, n_keys,
+                           seg_off_d);
+        FDX_LAUNCHED("k_seg_offsets");
+    }
     return FDX_OK;
 }
 

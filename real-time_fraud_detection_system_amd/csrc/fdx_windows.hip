@@ -216,47 +216,92 @@ __global__ void __launch_bounds__(256) k_interleave(
     }
 }
 
-__global__ void __launch_bounds__(256) k_customer_interleaved(
+// One wave per group; the wave streams its group's rows through an LDS ring (coalesced
+// chunk loads of C rows x S segments), so both the head row and the trailing rows that
+// leave the window are read from LDS.  A trailing row older than the ring (window
+// occupancy > kRing - kChunk rows) is read from global memory instead (correct, slower).
+constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
+
+// kRing rows per segment stay in LDS (30-day window occupancy at config 2: max 172 rows).
+template <int S_MAX, int kRing>
+__global__ void __launch_bounds__(64) k_customer_ring(
     const int64_t *__restrict__ its, const double *__restrict__ iamt, const int64_t *__restrict__ seg_off,
-    const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int64_t n_seg, int64_t n_groups,
-    int32_t S, int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out,
-    double *__restrict__ avg_out) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t g = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-    if (g >= n_groups) return;
+    const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S,
+    int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ avg_out) {
+    __shared__ int64_t r_ts[kRing * S_MAX];
+    __shared__ double r_amt[kRing * S_MAX];
+    const int lane = threadIdx.x;
+    const int64_t g = blockIdx.x;
     const int l = lane / n_win, wi = lane - l * n_win;
     const int64_t si = g * S + l;
-    if (l >= S || si >= n_seg) return;
-    const int64_t s = sorder[si];
-    const int64_t L = seg_off[s + 1] - seg_off[s];
-    const int64_t W = win.w[wi];
-    const int64_t base = goff[g] + l;
+    const bool active = l < S && si < n_seg;
+    const int64_t s = active ? sorder[si] : 0;
+    const int64_t L = active ? seg_off[s + 1] - seg_off[s] : 0;
+    const int64_t s0 = sorder[g * S];
+    const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
+    const int64_t W = win.w[active ? wi : 0];
+    const int64_t gbase = goff[g];
+    const int64_t base = gbase + l;
     int32_t *nb = nb_out + (int64_t)wi * n_slots;
     double *avg = avg_out + (int64_t)wi * n_slots;
     RollSum st;
     int64_t tail = 0;
-    for (int64_t t = 0; t < L; ++t) {
-        const int64_t slot = base + t * S;
-        const int64_t tv = its[slot];
-        const double v = iamt[slot];
-        if (t == 0) {
-            st.reset(v);
-            st.add(v);
-        } else {
-            const int64_t bound = tv - W;
-            int64_t nt = tail;
-            while (nt < t && its[base + nt * S] <= bound) ++nt;
-            if (nt >= t) {  // pandas re-initialises the window
+    int tail_r = 0;  // ring row of `tail`
+    int head_r = 0;  // ring row of t
+    for (int64_t t0 = 0; t0 < Lg; t0 += kChunk) {
+        // cooperative, coalesced load of rows [t0, t0 + kChunk) of all S segments
+        const int rows = (int)min<int64_t>(kChunk, Lg - t0);
+        const int ring0 = (int)(t0 % kRing);
+        for (int e = lane; e < rows * S; e += kWave) {
+            const int tt = e / S, ll = e - tt * S;
+            const int64_t src = gbase + (t0 + tt) * S + ll;
+            r_ts[(ring0 + tt) * S_MAX + ll] = its[src];
+            r_amt[(ring0 + tt) * S_MAX + ll] = iamt[src];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t oldest = t0 + kChunk - kRing;  // first row still in the ring
+        const int64_t tend = min<int64_t>(t0 + kChunk, L);
+        for (int64_t t = t0; t < tend; ++t) {
+            const int64_t tv = r_ts[head_r * S_MAX + l];
+            const double v = r_amt[head_r * S_MAX + l];
+            if (t == 0) {
                 st.reset(v);
                 st.add(v);
             } else {
-                for (int64_t j = tail; j < nt; ++j) st.remove(iamt[base + j * S]);
-                st.add(v);
+                const int64_t bound = tv - W;
+                // pandas variable-window start: first row j <= t with ts[j] > t_i - W
+                int64_t nt = tail;
+                int nr = tail_r;
+                while (nt < t) {
+                    const int64_t x = nt >= oldest ? r_ts[nr * S_MAX + l] : its[base + nt * S];
+                    if (x > bound) break;
+                    ++nt;
+                    nr = nr + 1 == kRing ? 0 : nr + 1;
+                }
+                if (nt >= t) {  // pandas re-initialises the window (start[i] >= end[i-1])
+                    st.reset(v);
+                    st.add(v);
+                } else {
+                    int jr = tail_r;
+                    for (int64_t j = tail; j < nt; ++j) {
+                        st.remove(j >= oldest ? r_amt[jr * S_MAX + l] : iamt[base + j * S]);
+                        jr = jr + 1 == kRing ? 0 : jr + 1;
+                    }
+                    st.add(v);
+                }
+                tail = nt;
+                tail_r = nr;
             }
-            tail = nt;
+            const int64_t slot = base + t * S;
+            nb[slot] = st.nobs;
+            avg[slot] = st.value() / (double)st.nobs;
+            head_r = head_r + 1 == kRing ? 0 : head_r + 1;
         }
-        nb[slot] = st.nobs;
-        avg[slot] = st.value() / (double)st.nobs;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -552,7 +597,8 @@ extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, cons
     hipLaunchKernelGGL(k_seg_len_keys, dim3(stream_grid(n_seg, 256)), dim3(256), 0, st, seg_off_d, n_seg, lmax, keys);
     FDX_LAUNCHED("k_seg_len_keys");
     const size_t rws = fdx_rekey_workspace_size(n_seg, 16);
-    int rc = fdx_rekey(keys, n_seg, 16, lmax + 1, sorder_d, nullptr, kseg, w, rws, stream);
+    (void)kseg;
+    int rc = fdx_rekey(keys, n_seg, 16, lmax + 1, sorder_d, nullptr, nullptr, w, rws, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_group_slots, dim3(stream_grid(n_groups, 256)), dim3(256), 0, st, seg_off_d, sorder_d,
                        n_seg, S, n_groups, goff_d);
@@ -588,9 +634,16 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     FDX_REQUIRE(its_d && iamt_d && seg_off_d && sorder_d && goff_d && nb_d && avg_d, "null pointer");
     const int32_t S = kWave / n_windows;
     const int64_t n_groups = ceil_div(n_seg, S);
-    hipLaunchKernelGGL(k_customer_interleaved, dim3((unsigned)ceil_div(n_groups, 4)), dim3(256), 0, as_stream(stream),
-                       its_d, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, n_groups, S, n_slots, wa, n_windows, nb_d,
-                       avg_d);
-    FDX_LAUNCHED("k_customer_interleaved");
+    // S_MAX = the LDS ring's segment stride: 21 for the reference's 3 windows
+    if (S <= 21)
+        hipLaunchKernelGGL((k_customer_ring<21, 192>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
+                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    else if (S <= 32)
+        hipLaunchKernelGGL((k_customer_ring<32, 192>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
+                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    else
+        hipLaunchKernelGGL((k_customer_ring<64, 96>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
+                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    FDX_LAUNCHED("k_customer_ring");
     return FDX_OK;
 }
