@@ -256,7 +256,7 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("rekey_customer")
     lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
     mark("customer_layout")
-    inb, iavg = ops.customer_windows_interleaved(lay, cseg)
+    inb, isum = ops.customer_windows_interleaved(lay, cseg)
     mark("customer_windows")
     tperm, tseg, _ = ops.rekey(term, args.terminals)
     mark("rekey_terminal")
@@ -267,7 +267,8 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     tinv = ops.invert_perm(tperm)
     mark("invert_terminal_perm")
     wsb = pipe._forest_ws(lay.n_slots, ws, ts.device)
-    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, iavg, lay.irow, tinv, trec, wsb, n=lay.n_slots)
+    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, isum, lay.irow, tinv, trec, wsb, n=lay.n_slots,
+                               val_is_sum=True)
     mark("assemble_scale_z32")
     ops.forest_traverse_perm(forest, lay.n_slots, wsb, proba, lay.irow)
     mark("forest_traverse")

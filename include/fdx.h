@@ -85,12 +85,15 @@ int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *
                         int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
                         int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *workspace_d,
                         size_t workspace_bytes, void *stream);
-/* fdx_customer_windows over that layout: nb_d/avg_d are [W][n_slots] indexed by slot. */
+/* fdx_customer_windows over that layout: nb_d / sum_d are [W][n_slots] indexed by slot, with
+ * sum_d the rolling SUM (pandas roll_sum, bit-exact); the average is sum / nb (IEEE float64
+ * division, done by the consumer -- fdx_forest_prepare_grouped with cust_val_is_sum = 1 --
+ * so that the division is off the sequential recurrence's critical path). */
 int fdx_customer_windows_interleaved(const int64_t *its_d, const double *iamt_d,
                                      const int64_t *seg_off_d, const int32_t *sorder_d,
                                      const uint32_t *goff_d, int64_t n_seg, int64_t n_slots,
                                      const int64_t *window_ns, int32_t n_windows, int32_t *nb_d,
-                                     double *avg_d, void *stream);
+                                     double *sum_d, void *stream);
 
 /* ---- a-3: terminal delayed-risk windows -----------------------------------------------
  * Replaces get_count_risk_rolling_window(terminal_transactions, delay_period,
@@ -248,8 +251,9 @@ int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *
  * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
 int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
 /* Traversal kernel shape: 0 = 512 threads x 1 row x 4 trees per lane, 1 = 1024 x 1 x 4
- * (default when <= 16 features), 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4
- * (variants > 0 need <= 16 features).
+ * (default when <= 16 features), 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4,
+ * 5 = 1024 x 1 x 3, 6 = 512 x 1 x 3, 7 = 768 x 1 x 3, 8 = 768 x 1 x 4, 9 = 1024 x 1 x 2
+ * (threads x rows per lane x trees per walk group; variants > 0 need <= 16 features).
  * Re-cuts the LDS chunks; results are identical for every variant. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
 
@@ -277,9 +281,10 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
  * inverse of the send perm).  Follow with fdx_forest_traverse_perm(out_perm = cust_perm)
  * so that proba lands in row order.  The same call serves the interleaved customer layout
  * (cust_* = slot arrays, cust_perm = irow): slots with cust_perm < 0 are padding (zero
- * row, never written back). */
+ * row, never written back).  cust_val_is_sum = 1: cust_avg_d holds rolling sums and the
+ * average is computed here as sum / nb. */
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
-                               const int64_t *cust_ts_d, const double *cust_amount_d,
+                               int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                const int32_t *cust_nb_d, const double *cust_avg_d,
                                const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                const int64_t *term_rec_d, void *workspace_d, size_t workspace_bytes,

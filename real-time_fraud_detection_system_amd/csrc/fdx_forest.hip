@@ -185,7 +185,7 @@ template <int FS>
 __global__ void __launch_bounds__(256) k_zfill_grouped(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
-    const int64_t *__restrict__ term_rec, int64_t n, int32_t W, int32_t flags_mode,
+    const int64_t *__restrict__ term_rec, int64_t n, int32_t W, int32_t flags_mode, int32_t val_is_sum,
     const double *__restrict__ mean, const double *__restrict__ scale, float *__restrict__ z,
     int32_t *__restrict__ nan_flag) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
@@ -220,8 +220,10 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
 #pragma unroll
         for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
             if (w < W) {
-                v[3 + 2 * w] = zval((double)cnb[(int64_t)w * n + i], mean, scale, 3 + 2 * w);
-                v[4 + 2 * w] = zval(cval[(int64_t)w * n + i], mean, scale, 4 + 2 * w);
+                const int32_t c = cnb[(int64_t)w * n + i];
+                const double cv = cval[(int64_t)w * n + i];
+                v[3 + 2 * w] = zval((double)c, mean, scale, 3 + 2 * w);
+                v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
                 v[3 + 2 * W + 2 * w] = zval((double)r32[w], mean, scale, 3 + 2 * W + 2 * w);
                 v[4 + 2 * W + 2 * w] = zval(__longlong_as_double(rec[(W + 1) / 2 + w]), mean, scale, 4 + 2 * W + 2 * w);
                 nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
@@ -245,7 +247,8 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 struct Variant {
     int block, rows, group;
 };
-constexpr Variant kVariants[] = {{512, 1, 4}, {1024, 1, 4}, {512, 2, 4}, {512, 2, 2}, {256, 2, 4}};
+constexpr Variant kVariants[] = {{512, 1, 4}, {1024, 1, 4}, {512, 2, 4}, {512, 2, 2}, {256, 2, 4},
+                                 {1024, 1, 3}, {512, 1, 3},  {768, 1, 3}, {768, 1, 4}, {1024, 1, 2}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -702,6 +705,11 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         case 2: FDX_LAUNCH_CHUNK(16, L, 512, 2, 4); break;                                                  \
         case 3: FDX_LAUNCH_CHUNK(16, L, 512, 2, 2); break;                                                  \
         case 4: FDX_LAUNCH_CHUNK(16, L, 256, 2, 4); break;                                                  \
+        case 5: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 3); break;                                                 \
+        case 6: FDX_LAUNCH_CHUNK(16, L, 512, 1, 3); break;                                                  \
+        case 7: FDX_LAUNCH_CHUNK(16, L, 768, 1, 3); break;                                                  \
+        case 8: FDX_LAUNCH_CHUNK(16, L, 768, 1, 4); break;                                                  \
+        case 9: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 2); break;                                                 \
         default: FDX_LAUNCH_CHUNK(32, L, 512, 1, 4); break;                                                 \
     }
             if (ch.in_lds) {
@@ -817,7 +825,7 @@ extern "C" int fdx_forest_set_slab_rows(fdx_forest F, int64_t rows) {
 }
 
 extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
-                                          const int64_t *cust_ts_d, const double *cust_amount_d,
+                                          int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                           const int32_t *cust_nb_d, const double *cust_avg_d,
                                           const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                           const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
@@ -839,12 +847,12 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     const unsigned grid = stream_grid(n, 256);
     if (F->zstride == 16)
         hipLaunchKernelGGL(k_zfill_grouped<16>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
-                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, F->mean_d,
-                           F->scale_d, z, flag);
+                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum,
+                           F->mean_d, F->scale_d, z, flag);
     else
         hipLaunchKernelGGL(k_zfill_grouped<32>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
-                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, F->mean_d,
-                           F->scale_d, z, flag);
+                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum,
+                           F->mean_d, F->scale_d, z, flag);
     FDX_LAUNCHED("k_zfill_grouped");
     return FDX_OK;
 }

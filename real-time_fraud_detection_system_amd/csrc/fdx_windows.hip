@@ -6,6 +6,8 @@
 //   flags     feature_transformation.ipynb:246-253, :294-301; fraud_detection.py:103-104
 //   customer  feature_transformation.ipynb:601-628 (pandas rolling('{w}d').sum()/count())
 //   terminal  feature_transformation.ipynb:1495-1522 (rolling(delay) vs rolling(delay+w))
+#include <cstdlib>
+
 #include "fdx_internal.h"
 
 namespace fdx {
@@ -296,7 +298,7 @@ __global__ void __launch_bounds__(64) k_customer_ring(
             }
             const int64_t slot = base + t * S;
             nb[slot] = st.nobs;
-            avg[slot] = st.value() / (double)st.nobs;
+            avg[slot] = st.value();  // rolling SUM: the division by nb is left to the consumer
             head_r = head_r + 1 == kRing ? 0 : head_r + 1;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -635,7 +637,17 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     const int32_t S = kWave / n_windows;
     const int64_t n_groups = ceil_div(n_seg, S);
     // S_MAX = the LDS ring's segment stride: 21 for the reference's 3 windows
-    if (S <= 21)
+    static const int ring_env = [] {
+        const char *e = getenv("FDX_CUSTOMER_RING");
+        return e ? atoi(e) : 192;
+    }();
+    if (S <= 21 && ring_env == 96)
+        hipLaunchKernelGGL((k_customer_ring<21, 96>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
+                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    else if (S <= 21 && ring_env == 48)
+        hipLaunchKernelGGL((k_customer_ring<21, 48>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
+                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    else if (S <= 21)
         hipLaunchKernelGGL((k_customer_ring<21, 192>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
                            iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
     else if (S <= 32)

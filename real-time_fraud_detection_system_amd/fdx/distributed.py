@@ -145,7 +145,7 @@ class ShardedPipeline:
                                                      self.n_terminals_total, p.windows_days, p.delay_days,
                                                      self.group)
         sinv = ops.invert_perm(send_perm)
-        ops.forest_prepare_grouped(p.forest, p.flags_mode, cts, camt, cnb, cavg, cperm, sinv, back, ws)
+        ops.forest_prepare_grouped(p.forest, p.flags_mode, cts, camt, cnb, cavg, cperm, sinv, back, ws)  # averages
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()

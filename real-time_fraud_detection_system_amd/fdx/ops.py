@@ -195,7 +195,8 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
 
 
 def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 7, 30), stream=None):
-    """-> (nb int32 [W, n_slots], avg float64 [W, n_slots]) indexed by slot."""
+    """-> (nb int32 [W, n_slots], rolling SUM float64 [W, n_slots]) indexed by slot;
+    the average is sum / nb (done by forest_prepare_grouped(val_is_sum=True))."""
     W = len(windows_days)
     dev = lay.its.device
     nb = torch.empty((W, lay.n_slots), dtype=torch.int32, device=dev)
@@ -337,10 +338,12 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None, n=None):
+                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False):
+    """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path)."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
-    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), _ptr(cts), _ptr(camt), _ptr(cnb),
+    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), int(val_is_sum), _ptr(cts),
+                                                 _ptr(camt), _ptr(cnb),
                                                  _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),
                                                  ws.numel(), _s(stream)), "fdx_forest_prepare_grouped")
 

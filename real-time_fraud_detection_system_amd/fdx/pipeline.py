@@ -113,14 +113,14 @@ class FraudPipeline:
         lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
-        inb, iavg = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
+        inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
         trec = ops.terminal_windows_packed(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
                                            tseg, self.delay_days, self.windows_days, stream)
         tinv = ops.invert_perm(tperm, stream)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
-        ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, iavg, lay.irow, tinv, trec,
-                                   ws, stream, n=lay.n_slots)
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, tinv, trec,
+                                   ws, stream, n=lay.n_slots, val_is_sum=True)
         if on_traverse:
             on_traverse(0)
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, stream)
