@@ -260,14 +260,10 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("customer_windows")
     tperm, tseg, _ = ops.rekey(term, args.terminals)
     mark("rekey_terminal")
-    tts, tfr = ops.gather(ts, tperm), ops.gather(fr, tperm)
-    mark("gather_terminal")
-    trec = ops.terminal_windows_packed(tts, tfr, tseg)
+    trec = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm)
     mark("terminal_windows")
-    tinv = ops.invert_perm(tperm)
-    mark("invert_terminal_perm")
     wsb = pipe._forest_ws(lay.n_slots, ws, ts.device)
-    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, isum, lay.irow, tinv, trec, wsb, n=lay.n_slots,
+    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, isum, lay.irow, None, trec, wsb, n=lay.n_slots,
                                val_is_sum=True)
     mark("assemble_scale_z32")
     ops.forest_traverse_perm(forest, lay.n_slots, wsb, proba, lay.irow)

@@ -122,10 +122,15 @@ int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
                           const int32_t *term_nb_d, const double *term_risk_d, double *X_d, int64_t ld,
                           void *stream);
 
-/* Same as fdx_terminal_windows, but one packed record per row (grouped order):
- * ceil(W/2) 8-byte words of int32 counts, then W float64 risks (rec_d: [n][ceil(W/2)+W]
- * int64).  The record is what fdx_forest_prepare_grouped reads. */
-int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+/* Same windows as fdx_terminal_windows, as one COUNT RECORD per row: n_windows int64 words,
+ * word w = NB_w | FRAUD_w << 32 (both uint32; RISK_w = NB_w > 0 ? (double)FRAUD_w / NB_w : 0,
+ * the same IEEE division fdx_terminal_windows does).  The consumers (fdx_forest_prepare_grouped,
+ * fdx_forest_prepare_reply, fdx_reply_assemble) do that division.
+ * row_d == NULL: ts/fraud are in grouped order and record q is rec_d[q].
+ * row_d != NULL: grouped position q is input row row_d[q] (the re-key perm): ts/fraud are
+ * read as ts[row_d[q]] and the record is written to rec_d[row_d[q]] -- records come out in
+ * input row order with no separate gather/invert pass.  rec_d: [ts rows][n_windows] int64. */
+int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
                                 const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
                                 const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
                                 void *stream);
@@ -170,10 +175,11 @@ int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, in
  * Rows are sharded by customer; the terminal windows need every row of a terminal on its
  * owner rank, owner(t) = t % world.  Per step: fdx_key_map(MOD) -> fdx_rekey(owner) ->
  * fdx_exchange_pack -> RCCL all-to-all (16 B/row) -> fdx_exchange_unpack (local terminal
- * id = t / world) -> time sort + fdx_rekey -> fdx_terminal_windows -> fdx_reply_pack
- * (records indexed by receive position) -> RCCL all-to-all back -> fdx_reply_assemble.
+ * id = t / world) -> time sort + fdx_rekey -> fdx_terminal_windows_packed with row_d = the
+ * grouped -> receive-position perm (count records indexed by receive position) -> RCCL
+ * all-to-all back -> fdx_forest_prepare_grouped / fdx_reply_assemble.
  * Record layouts: exchange rec[j] = {ts, term<<32 | fraud<<31 | source row}; reply rows
- * are ceil(W/2) words of packed int32 counts followed by W float64 risks. */
+ * are the count records of fdx_terminal_windows_packed (n_windows words). */
 #define FDX_KEY_MOD 0 /* out = key % param  (owner rank of a terminal)          */
 #define FDX_KEY_DIV 1 /* out = key / param  (owner-local terminal id)           */
 #define FDX_KEY_SUB 2 /* out = key - param  (shard-local customer id)           */
@@ -183,8 +189,6 @@ int fdx_exchange_pack(const int64_t *ts_d, const int32_t *term_d, const uint8_t 
                       const int32_t *perm_d, int64_t n, int64_t *rec_d, void *stream);
 int fdx_exchange_unpack(const int64_t *rec_d, int64_t m, int32_t world, int64_t *ts_d,
                         int32_t *term_local_d, uint8_t *fraud_d, void *stream);
-int fdx_reply_pack(const int32_t *nb_d, const double *risk_d, const int32_t *perm_d, int64_t m,
-                   int32_t n_windows, int64_t *reply_d, void *stream);
 int fdx_reply_assemble(const int64_t *reply_d, const int32_t *perm_d, int64_t n, int32_t n_windows,
                        double *X_d, int64_t ld, int32_t col0, void *stream);
 
@@ -276,9 +280,10 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
 /* The scoring rows in CUSTOMER-grouped order, each written whole (coalesced): row i is
  * transaction r = cust_perm[i]; cust_ts/cust_amount/cust_nb/cust_avg are the customer-grouped
  * copies and outputs (flags are derived from cust_ts with flags_mode), the terminal half
- * is the packed record term_rec[term_inv[r]] (fdx_terminal_windows_packed output with
- * term_inv = inverse of the terminal perm, or the multi-GPU reply records with term_inv =
- * inverse of the send perm).  Follow with fdx_forest_traverse_perm(out_perm = cust_perm)
+ * is the count record term_rec[term_inv[r]] (term_inv may be NULL = identity: the
+ * fdx_terminal_windows_packed output with row_d = the terminal perm is already in row
+ * order; the multi-GPU reply records need term_inv = inverse of the send perm).  Follow
+ * with fdx_forest_traverse_perm(out_perm = cust_perm)
  * so that proba lands in row order.  The same call serves the interleaved customer layout
  * (cust_* = slot arrays, cust_perm = irow): slots with cust_perm < 0 are padding (zero
  * row, never written back).  cust_val_is_sum = 1: cust_avg_d holds rolling sums and the

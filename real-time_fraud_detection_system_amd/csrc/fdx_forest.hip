@@ -47,6 +47,9 @@ struct fdx_forest_s {
         bool in_lds;
     };
     std::vector<Chunk> chunks;
+    int32_t *chunk_t_d = nullptr;     // [n_trees+1] first tree of each chunk (tile kernels)
+    int64_t *chunk_base_d = nullptr;  // [n_trees+1] first node of each chunk
+    bool tile_ok = false;             // every chunk of the tile variant fits its LDS budget
     int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or all rows)
     int variant = 0;        // index into kVariants
     std::vector<int64_t> node_offsets;  // host copy (chunking)
@@ -152,24 +155,21 @@ __global__ void __launch_bounds__(256) k_zfill_group(const int32_t *__restrict__
     }
 }
 
-// same, from the multi-GPU reply records (fdx_reply_pack layout), row j -> perm[j]
+// same, from the multi-GPU count records (fdx_terminal_windows_packed), row j -> perm[j]
 template <int FS>
 __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__ reply,
                                                     const int32_t *__restrict__ perm, int64_t n, int32_t W,
                                                     int32_t col0, const double *__restrict__ mean,
                                                     const double *__restrict__ scale, float *__restrict__ z,
                                                     int32_t *__restrict__ nan_flag) {
-    const int words = (W + 1) / 2 + W;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t *r = reply + j * words;
+        const int64_t *r = reply + j * W;
         float *o = z + (int64_t)perm[j] * FS + col0;
         bool nan = false;
         for (int w = 0; w < W; ++w) {
-            const uint64_t pk = (uint64_t)r[w / 2];
-            const int32_t cnt = (int32_t)((w & 1) ? (pk >> 32) : (pk & 0xFFFFFFFFu));
-            o[2 * w] = zval((double)cnt, mean, scale, col0 + 2 * w);
-            const float v = zval(__longlong_as_double(r[(W + 1) / 2 + w]), mean, scale, col0 + 2 * w + 1);
+            o[2 * w] = zval((double)term_nb(r[w]), mean, scale, col0 + 2 * w);
+            const float v = zval(term_risk(r[w]), mean, scale, col0 + 2 * w + 1);
             o[2 * w + 1] = v;
             nan |= v != v;
         }
@@ -179,8 +179,8 @@ __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__
 
 // Scoring rows in CUSTOMER-grouped order, written whole (64-byte coalesced rows): row i
 // holds the transaction r = cust_perm[i]; amount / time flags / customer windows are
-// already in this order, the terminal half is one packed record read from
-// term_rec[term_inv[r]] (term_inv: row -> terminal-grouped or send position).
+// already in this order, the terminal half is one count record read from
+// term_rec[term_inv[r]] (term_inv: row -> send position; NULL = records already by row).
 template <int FS>
 __global__ void __launch_bounds__(256) k_zfill_grouped(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
@@ -189,7 +189,6 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     const double *__restrict__ mean, const double *__restrict__ scale, float *__restrict__ z,
     int32_t *__restrict__ nan_flag) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
-    const int words = (W + 1) / 2 + W;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
@@ -214,9 +213,8 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         v[1] = zval((double)we, mean, scale, 1);
         v[2] = zval((double)ni, mean, scale, 2);
         bool nan = v[0] != v[0];
-        const int64_t q = term_inv[r];
-        const int64_t *rec = term_rec + q * words;
-        const int32_t *r32 = reinterpret_cast<const int32_t *>(rec);
+        const int64_t q = term_inv ? term_inv[r] : r;
+        const int64_t *rec = term_rec + q * W;
 #pragma unroll
         for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
             if (w < W) {
@@ -224,8 +222,9 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                 const double cv = cval[(int64_t)w * n + i];
                 v[3 + 2 * w] = zval((double)c, mean, scale, 3 + 2 * w);
                 v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
-                v[3 + 2 * W + 2 * w] = zval((double)r32[w], mean, scale, 3 + 2 * W + 2 * w);
-                v[4 + 2 * W + 2 * w] = zval(__longlong_as_double(rec[(W + 1) / 2 + w]), mean, scale, 4 + 2 * W + 2 * w);
+                const int64_t tw = rec[w];
+                v[3 + 2 * W + 2 * w] = zval((double)term_nb(tw), mean, scale, 3 + 2 * W + 2 * w);
+                v[4 + 2 * W + 2 * w] = zval(term_risk(tw), mean, scale, 4 + 2 * W + 2 * w);
                 nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
             }
         }
@@ -244,11 +243,14 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 
 // Kernel variants (block size, rows per lane R, trees per walk group G).  LDS holds the
 // row features [FS][BLOCK*R] float32 and, in the rest of the 160 KiB, the chunk's nodes.
+// tile = 1: k_forest_tile (rows resident, trees streamed) instead of k_forest_chunk.
 struct Variant {
-    int block, rows, group;
+    int block, rows, group, tile;
 };
-constexpr Variant kVariants[] = {{512, 1, 4}, {1024, 1, 4}, {512, 2, 4}, {512, 2, 2}, {256, 2, 4},
-                                 {1024, 1, 3}, {512, 1, 3},  {768, 1, 3}, {768, 1, 4}, {1024, 1, 2}};
+constexpr Variant kVariants[] = {{512, 1, 4, 0},  {1024, 1, 4, 0}, {512, 2, 4, 0}, {512, 2, 2, 0},
+                                 {256, 2, 4, 0},  {1024, 1, 3, 0}, {512, 1, 3, 0}, {768, 1, 3, 0},
+                                 {768, 1, 4, 0},  {1024, 1, 2, 0}, {768, 1, 2, 0}, {768, 2, 2, 0},
+                                 {1024, 1, 2, 1}, {512, 2, 1, 1},  {512, 3, 1, 1}, {768, 2, 1, 1}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -257,31 +259,49 @@ constexpr int lds_node_bytes(int fs, int block, int rows) { return kLdsTotal - f
 // One launch = one chunk of trees [t0, t1) over rows [r0, r1).  Each lane walks G trees
 // for each of its R rows at once (R*G independent chains).  A step is branch-free (leaves
 // are fixed points); all feature reads of a step are issued together, then all node reads,
-// so a lane keeps R*G LDS reads in flight; a walk group runs exactly max(depth) steps, so
-// the loop is uniform across the wave.  NaN routing (missing_go_to_left) costs 3 extra
-// VALU per step: it is compiled in a second loop that runs only when the prepare step saw
-// a NaN feature (*nan_flag != 0).
+// so a lane keeps R*G LDS reads in flight; a walk group runs at most max(depth) steps and
+// stops as soon as every chain of the wave is at a leaf (the loop is uniform across the
+// wave).  NaN routing (missing_go_to_left) costs 3 extra VALU per step: it is compiled in
+// a second loop that runs only when the prepare step saw a NaN feature (*nan_flag != 0).
+template <bool NAN_AWARE, bool LDS, int XSTRIDE, int K>
+__device__ __forceinline__ void walk_step(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
+                                          uint32_t (&p)[K], uint64_t (&nd)[K]) {
+    float x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t hi = (uint32_t)(nd[k] >> 32);
+        x[k] = xcol[k][((hi >> 24) & 63u) * XSTRIDE];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t hi = (uint32_t)(nd[k] >> 32);
+        bool left = x[k] <= __uint_as_float((uint32_t)nd[k]);
+        if (NAN_AWARE) left = left | ((x[k] != x[k]) & ((hi >> 30) & 1u));
+        const uint32_t step = left ? 8u : (hi & 0xFFFFFFu);
+        p[k] += step & (uint32_t)((int32_t)hi >> 31);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) nd[k] = node_at<LDS>(s_nodes, gbase, p[k]);
+}
+
+// Walks every chain to its leaf: at most `depth` steps, in blocks of kExitEvery steps with a
+// wave-uniform exit test between blocks (all chains of the wave at leaves).  In-distribution
+// rows of the bench forest end at ~5 nodes (depth 20), far-out rows run all 20 steps; testing
+// every kExitEvery steps keeps the test's cost small in the second case.
+constexpr int kExitEvery = 4;
 template <bool NAN_AWARE, bool LDS, int XSTRIDE, int K>
 __device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
                                            uint32_t (&p)[K], uint64_t (&nd)[K], int depth) {
-    for (int d = 0; d < depth; ++d) {
-        float x[K];
+    int d = 0;
+    for (; d + kExitEvery <= depth; d += kExitEvery) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t hi = (uint32_t)(nd[k] >> 32);
-            x[k] = xcol[k][((hi >> 24) & 63u) * XSTRIDE];
-        }
+        for (int e = 0; e < kExitEvery; ++e) walk_step<NAN_AWARE, LDS, XSTRIDE, K>(s_nodes, gbase, xcol, p, nd);
+        uint32_t internal = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t hi = (uint32_t)(nd[k] >> 32);
-            bool left = x[k] <= __uint_as_float((uint32_t)nd[k]);
-            if (NAN_AWARE) left = left | ((x[k] != x[k]) & ((hi >> 30) & 1u));
-            const uint32_t step = left ? 8u : (hi & 0xFFFFFFu);
-            p[k] += step & (uint32_t)((int32_t)hi >> 31);
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) nd[k] = node_at<LDS>(s_nodes, gbase, p[k]);
+        for (int k = 0; k < K; ++k) internal |= (uint32_t)(nd[k] >> 32);
+        if (!__any((int32_t)internal < 0)) return;
     }
+    for (; d < depth; ++d) walk_step<NAN_AWARE, LDS, XSTRIDE, K>(s_nodes, gbase, xcol, p, nd);
 }
 
 template <int FS, bool LDS, int BLOCK, int R, int G>
@@ -371,6 +391,101 @@ __global__ void __launch_bounds__(BLOCK) k_forest_chunk(
             } else {
                 acc[row[r]] = a[r];
             }
+        }
+    }
+}
+
+// Rows-resident traversal (tile variants): one block per CU keeps a tile of BLOCK*R rows'
+// scaled features in LDS for the WHOLE forest and streams the trees through the rest of LDS
+// chunk by chunk.  The chunks are read from L2 (the packed forest, a few MB, stays resident
+// in every XCD's 4 MiB L2 or the Infinity Cache), the running sums stay in registers, so a
+// row costs one 64-B read of z and one 8-B write of proba in HBM instead of 80 B per chunk
+// launch.  Tree order of the float64 sum is unchanged (chunks, then groups, in order).
+template <int FS, int BLOCK, int R, int G>
+__global__ void __launch_bounds__(BLOCK) k_forest_tile(
+    const uint64_t *__restrict__ nodes, const int32_t *__restrict__ chunk_t, const int64_t *__restrict__ chunk_base,
+    int32_t n_chunks, const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
+    const float *__restrict__ z, const int32_t *__restrict__ nan_flag, int64_t n, double *__restrict__ proba,
+    const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
+    int32_t n_trees) {
+    constexpr int kRowsPerBlock = BLOCK * R;
+    constexpr int kNodeCap = lds_node_bytes(FS, BLOCK, R) / 8;
+    constexpr int K = R * G;
+    __shared__ uint64_t s_nodes[kNodeCap];
+    __shared__ float s_x[FS][kRowsPerBlock];
+    const int tid = threadIdx.x;
+    const char *lbase = reinterpret_cast<const char *>(s_nodes);
+    const bool any_nan = *nan_flag != 0;
+    const float *xcol[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) xcol[k] = &s_x[0][(k / G) * BLOCK + tid];
+    for (int64_t base = (int64_t)blockIdx.x * kRowsPerBlock; base < n; base += (int64_t)gridDim.x * kRowsPerBlock) {
+        int64_t row[R];
+        bool ok[R];
+        double a[R];
+        __syncthreads();  // the previous tile is done with s_x
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            row[r] = base + r * BLOCK + tid;
+            ok[r] = row[r] < n;
+            const float4 *src = reinterpret_cast<const float4 *>(z + (ok[r] ? row[r] : 0) * FS);
+#pragma unroll
+            for (int q = 0; q < FS / 4; ++q) {
+                float4 v = src[q];
+                s_x[4 * q + 0][r * BLOCK + tid] = v.x;
+                s_x[4 * q + 1][r * BLOCK + tid] = v.y;
+                s_x[4 * q + 2][r * BLOCK + tid] = v.z;
+                s_x[4 * q + 3][r * BLOCK + tid] = v.w;
+            }
+            a[r] = 0.0;
+        }
+        for (int c = 0; c < n_chunks; ++c) {
+            const int32_t t0 = chunk_t[c], t1 = chunk_t[c + 1];
+            const int64_t nb0 = chunk_base[c];
+            const int32_t cn = (int32_t)(chunk_base[c + 1] - nb0);
+            __syncthreads();  // every wave is done with the previous chunk's nodes
+            for (int i = tid; i < cn; i += BLOCK) s_nodes[i] = nodes[nb0 + i];
+            __syncthreads();
+            for (int t = t0; t < t1; t += G) {
+                uint32_t p[K];
+                uint64_t nd[K];
+                int dmax = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const bool act = t + g < t1;
+                    const uint32_t p0 = act ? (uint32_t)(root[t + g] - nb0) * 8u : 0u;
+                    const uint64_t n0 = act ? node_at<true>(s_nodes, lbase, p0) : 0ull;
+                    dmax = act ? max(dmax, depth[t + g]) : dmax;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        p[r * G + g] = p0;
+                        nd[r * G + g] = n0;
+                    }
+                }
+                if (any_nan)
+                    walk_group<true, true, kRowsPerBlock, K>(s_nodes, lbase, xcol, p, nd, dmax);
+                else
+                    walk_group<false, true, kRowsPerBlock, K>(s_nodes, lbase, xcol, p, nd, dmax);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        if (t + g < t1) {
+                            a[r] += leaf_value(nd[r * G + g]);
+                            if (leaf_out && ok[r]) {
+                                const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+                                if (dst >= 0) leaf_out[dst * n_trees + t + g] = orig[nb0 + (p[r * G + g] >> 3)];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!ok[r]) continue;
+            const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+            if (dst >= 0) proba[dst] = a[r] / (double)n_trees;  // < 0: padding slot
         }
     }
 }
@@ -501,6 +616,7 @@ int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F
 // where more than G fit (a partial group idles walk slots); oversized trees run from global.
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
+    F->tile_ok = v.tile != 0;
     const int64_t cap_nodes = lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = F->node_offsets;
@@ -512,6 +628,7 @@ void build_chunks(fdx_forest_s *F) {
         if (off[t + 1] - off[t] > cap_nodes) {
             c.t1 = t + 1;
             c.in_lds = false;
+            F->tile_ok = false;
         } else {
             int32_t u = t + 1;
             while (u < F->n_trees && off[u + 1] - c.node_base <= cap_nodes) ++u;
@@ -524,6 +641,21 @@ void build_chunks(fdx_forest_s *F) {
         t = c.t1;
     }
 }
+// Chunk table for the tile kernels (device copy; synchronous, off the hot path).
+int upload_chunks(fdx_forest_s *F) {
+    if (!F->chunk_t_d) return FDX_OK;
+    std::vector<int32_t> ct(F->chunks.size() + 1);
+    std::vector<int64_t> cb(F->chunks.size() + 1);
+    for (size_t c = 0; c < F->chunks.size(); ++c) {
+        ct[c] = F->chunks[c].t0;
+        cb[c] = F->chunks[c].node_base;
+    }
+    ct.back() = F->n_trees;
+    cb.back() = F->n_nodes;
+    FDX_HIP(hipMemcpy(F->chunk_t_d, ct.data(), sizeof(int32_t) * ct.size(), hipMemcpyHostToDevice));
+    FDX_HIP(hipMemcpy(F->chunk_base_d, cb.data(), sizeof(int64_t) * cb.size(), hipMemcpyHostToDevice));
+    return FDX_OK;
+}
 }  // namespace
 }  // namespace fdx
 
@@ -531,9 +663,16 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(variant >= 0 && variant < kNumVariants, "variant must be in [0, %d)", kNumVariants);
     FDX_REQUIRE(variant == 0 || F->zstride == 16, "variants > 0 need <= 16 features");
+    const int prev = F->variant;
     F->variant = variant;
     build_chunks(F);
-    return FDX_OK;
+    if (kVariants[variant].tile && !F->tile_ok) {
+        F->variant = prev;
+        build_chunks(F);
+        set_error("variant %d: a tree does not fit the tile kernel's LDS node budget", variant);
+        return FDX_E_UNSUPPORTED;
+    }
+    return upload_chunks(F);
 }
 
 extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, int32_t *orig_out,
@@ -577,6 +716,9 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->root_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->depth_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&F->chunk_t_d, sizeof(int32_t) * (d->n_trees + 1))) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&F->chunk_base_d, sizeof(int64_t) * (d->n_trees + 1))) != hipSuccess)
+        return fail(e, "hipMalloc");
     if ((e = hipMemcpyAsync(F->depth_d, depth.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->nodes_d, packed.data(), sizeof(uint64_t) * total, hipMemcpyHostToDevice, st)))
@@ -599,6 +741,10 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     }
     // host vectors die at return: make the uploads complete first
     if ((e = hipStreamSynchronize(st))) return fail(e, "hipStreamSynchronize");
+    if (upload_chunks(F)) {
+        fdx_forest_destroy(F);
+        return FDX_E_HIP;
+    }
     *out = F;
     return FDX_OK;
 }
@@ -609,6 +755,8 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->orig_d);
     (void)hipFree(F->root_d);
     (void)hipFree(F->depth_d);
+    (void)hipFree(F->chunk_t_d);
+    (void)hipFree(F->chunk_base_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
     delete F;
@@ -684,6 +832,21 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
     hipStream_t st = as_stream(stream);
     // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
     // features and running sums stay in the 256 MiB Infinity Cache.
+    if (F->zstride == 16 && kVariants[F->variant].tile) {
+#define FDX_LAUNCH_TILE(B, R, G)                                                                            \
+    hipLaunchKernelGGL((k_forest_tile<16, B, R, G>), dim3((unsigned)std::min<int64_t>(ceil_div(n, (B) * (R)), 256)), \
+                       dim3(B), 0, st, F->nodes_d, F->chunk_t_d, F->chunk_base_d, (int32_t)F->chunks.size(),      \
+                       F->root_d, F->depth_d, z, flag, n, proba_d, out_perm_d, leaf_d, F->orig_d, F->n_trees)
+        switch (F->variant) {
+            case 12: FDX_LAUNCH_TILE(1024, 1, 2); break;
+            case 13: FDX_LAUNCH_TILE(512, 2, 1); break;
+            case 14: FDX_LAUNCH_TILE(512, 3, 1); break;
+            default: FDX_LAUNCH_TILE(768, 2, 1); break;
+        }
+#undef FDX_LAUNCH_TILE
+        FDX_LAUNCHED("k_forest_tile");
+        return FDX_OK;
+    }
     const int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
     const size_t nc = F->chunks.size();
     for (int64_t s0 = 0; s0 < n; s0 += slab) {
@@ -710,6 +873,8 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         case 7: FDX_LAUNCH_CHUNK(16, L, 768, 1, 3); break;                                                  \
         case 8: FDX_LAUNCH_CHUNK(16, L, 768, 1, 4); break;                                                  \
         case 9: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 2); break;                                                 \
+        case 10: FDX_LAUNCH_CHUNK(16, L, 768, 1, 2); break;                                                 \
+        case 11: FDX_LAUNCH_CHUNK(16, L, 768, 2, 2); break;                                                 \
         default: FDX_LAUNCH_CHUNK(32, L, 512, 1, 4); break;                                                 \
     }
             if (ch.in_lds) {
@@ -835,7 +1000,7 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
                 3 + 4 * n_windows);
     if (n == 0) return FDX_OK;
-    FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && cust_perm_d && term_inv_d && term_rec_d,
+    FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && cust_perm_d && term_rec_d,
                 "null pointer");
     float *z;
     double *acc;

@@ -45,6 +45,17 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
         }                                                                                 \
     } while (0)
 
+// Terminal count record word (fdx_terminal_windows_packed): NB | FRAUD << 32.
+__device__ __forceinline__ int64_t term_word(int32_t nb, int32_t fraud) {
+    return (int64_t)(((uint64_t)(uint32_t)fraud << 32) | (uint32_t)nb);
+}
+__device__ __forceinline__ int32_t term_nb(int64_t w) { return (int32_t)(uint32_t)((uint64_t)w & 0xFFFFFFFFu); }
+// RISK = FRAUD / NB with fillna(0) of 0/0 (feature_transformation.ipynb:1512-1517)
+__device__ __forceinline__ double term_risk(int64_t w) {
+    const uint32_t nb = (uint32_t)((uint64_t)w & 0xFFFFFFFFu), fr = (uint32_t)((uint64_t)w >> 32);
+    return nb > 0 ? (double)fr / (double)nb : 0.0;
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid for a grid-stride streaming kernel: enough blocks to fill 256 CUs several times,

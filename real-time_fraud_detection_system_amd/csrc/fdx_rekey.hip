@@ -462,35 +462,16 @@ __global__ void k_exchange_unpack(const int64_t *__restrict__ rec, int64_t m, in
     }
 }
 
-// reply[perm[j]] = {nb[0..W) packed 2 per word, risk bits[0..W)}
-__global__ void k_reply_pack(const int32_t *__restrict__ nb, const double *__restrict__ risk,
-                             const int32_t *__restrict__ perm, int64_t m, int32_t W,
-                             int64_t *__restrict__ reply) {
-    const int words = (W + 1) / 2 + W;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
-         j += (int64_t)gridDim.x * blockDim.x) {
-        int64_t *o = reply + (int64_t)perm[j] * words;
-        for (int w = 0; w < W; w += 2) {
-            uint64_t lo = (uint32_t)nb[(int64_t)w * m + j];
-            uint64_t hi = (w + 1 < W) ? (uint32_t)nb[(int64_t)(w + 1) * m + j] : 0u;
-            o[w / 2] = (int64_t)(lo | (hi << 32));
-        }
-        for (int w = 0; w < W; ++w) o[(W + 1) / 2 + w] = __double_as_longlong(risk[(int64_t)w * m + j]);
-    }
-}
-
-// X[perm[j]][col0 + 2w] = nb_w, X[perm[j]][col0 + 2w + 1] = risk_w from reply records
+// X[perm[j]][col0 + 2w] = nb_w, X[perm[j]][col0 + 2w + 1] = risk_w from count records
 __global__ void k_reply_assemble(const int64_t *__restrict__ reply, const int32_t *__restrict__ perm,
                                  int64_t n, int32_t W, double *__restrict__ X, int64_t ld, int32_t col0) {
-    const int words = (W + 1) / 2 + W;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t *r = reply + j * words;
+        const int64_t *r = reply + j * W;
         double *x = X + (int64_t)perm[j] * ld + col0;
         for (int w = 0; w < W; ++w) {
-            const uint64_t p = (uint64_t)r[w / 2];
-            x[2 * w] = (double)(int32_t)((w & 1) ? (p >> 32) : (p & 0xFFFFFFFFu));
-            x[2 * w + 1] = __longlong_as_double(r[(W + 1) / 2 + w]);
+            x[2 * w] = (double)term_nb(r[w]);
+            x[2 * w + 1] = term_risk(r[w]);
         }
     }
 }
@@ -570,17 +551,6 @@ extern "C" int fdx_exchange_unpack(const int64_t *rec_d, int64_t m, int32_t worl
     hipLaunchKernelGGL(k_exchange_unpack, dim3(stream_grid(m, 256)), dim3(256), 0, as_stream(stream), rec_d,
                        m, world, ts_d, term_local_d, fraud_d);
     FDX_LAUNCHED("k_exchange_unpack");
-    return FDX_OK;
-}
-
-extern "C" int fdx_reply_pack(const int32_t *nb_d, const double *risk_d, const int32_t *perm_d, int64_t m,
-                              int32_t n_windows, int64_t *reply_d, void *stream) {
-    FDX_REQUIRE(m >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
-    if (m == 0) return FDX_OK;
-    FDX_REQUIRE(nb_d && risk_d && perm_d && reply_d, "null pointer");
-    hipLaunchKernelGGL(k_reply_pack, dim3(stream_grid(m, 256)), dim3(256), 0, as_stream(stream), nb_d, risk_d,
-                       perm_d, m, n_windows, reply_d);
-    FDX_LAUNCHED("k_reply_pack");
     return FDX_OK;
 }
 

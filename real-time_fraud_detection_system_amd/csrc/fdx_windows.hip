@@ -225,11 +225,16 @@ __global__ void __launch_bounds__(256) k_interleave(
 constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
 
 // kRing rows per segment stay in LDS (30-day window occupancy at config 2: max 172 rows).
+// The per-row work is straight-line: the tail loop removes rows as it advances (pandas
+// first finds the new start, then removes rows [old start, new start) -- unless the
+// window restarts, in which case the state is re-initialised; removing first and
+// re-initialising afterwards leaves exactly the same state), and the re-initialisation is
+// a predicated select, so a wave runs one instruction stream for its 1/7/30-day lanes.
 template <int S_MAX, int kRing>
 __global__ void __launch_bounds__(64) k_customer_ring(
     const int64_t *__restrict__ its, const double *__restrict__ iamt, const int64_t *__restrict__ seg_off,
     const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S,
-    int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ avg_out) {
+    int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ sum_out) {
     __shared__ int64_t r_ts[kRing * S_MAX];
     __shared__ double r_amt[kRing * S_MAX];
     const int lane = threadIdx.x;
@@ -238,67 +243,71 @@ __global__ void __launch_bounds__(64) k_customer_ring(
     const int64_t si = g * S + l;
     const bool active = l < S && si < n_seg;
     const int64_t s = active ? sorder[si] : 0;
-    const int64_t L = active ? seg_off[s + 1] - seg_off[s] : 0;
+    const int32_t L = active ? (int32_t)(seg_off[s + 1] - seg_off[s]) : 0;
     const int64_t s0 = sorder[g * S];
-    const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
+    const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
     const int64_t W = win.w[active ? wi : 0];
     const int64_t gbase = goff[g];
-    const int64_t base = gbase + l;
-    int32_t *nb = nb_out + (int64_t)wi * n_slots;
-    double *avg = avg_out + (int64_t)wi * n_slots;
-    RollSum st;
-    int64_t tail = 0;
-    int tail_r = 0;  // ring row of `tail`
-    int head_r = 0;  // ring row of t
-    for (int64_t t0 = 0; t0 < Lg; t0 += kChunk) {
-        // cooperative, coalesced load of rows [t0, t0 + kChunk) of all S segments
-        const int rows = (int)min<int64_t>(kChunk, Lg - t0);
-        const int ring0 = (int)(t0 % kRing);
+    const int64_t *g_ts = its + gbase + l;     // row t of this lane's segment: g_ts[t * S]
+    const double *g_amt = iamt + gbase + l;
+    int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + l;
+    double *sm = sum_out + (int64_t)wi * n_slots + gbase + l;
+    const int64_t *l_ts = r_ts + l;            // ring row r of this lane: l_ts[r * S_MAX]
+    const double *l_amt = r_amt + l;
+    // pandas roll_sum state (aggregations.pyx)
+    double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
+    int32_t nobs = 0, nsame = 0;
+    int32_t tail = 0, tail_r = 0, head_r = 0;
+    for (int32_t t0 = 0; t0 < Lg; t0 += kChunk) {
+        const int rows = min(kChunk, Lg - t0);
+        const int ring0 = t0 % kRing;
         for (int e = lane; e < rows * S; e += kWave) {
             const int tt = e / S, ll = e - tt * S;
-            const int64_t src = gbase + (t0 + tt) * S + ll;
+            const int64_t src = gbase + (int64_t)(t0 + tt) * S + ll;
             r_ts[(ring0 + tt) * S_MAX + ll] = its[src];
             r_amt[(ring0 + tt) * S_MAX + ll] = iamt[src];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int64_t oldest = t0 + kChunk - kRing;  // first row still in the ring
-        const int64_t tend = min<int64_t>(t0 + kChunk, L);
-        for (int64_t t = t0; t < tend; ++t) {
-            const int64_t tv = r_ts[head_r * S_MAX + l];
-            const double v = r_amt[head_r * S_MAX + l];
-            if (t == 0) {
-                st.reset(v);
-                st.add(v);
-            } else {
-                const int64_t bound = tv - W;
-                // pandas variable-window start: first row j <= t with ts[j] > t_i - W
-                int64_t nt = tail;
-                int nr = tail_r;
-                while (nt < t) {
-                    const int64_t x = nt >= oldest ? r_ts[nr * S_MAX + l] : its[base + nt * S];
-                    if (x > bound) break;
-                    ++nt;
-                    nr = nr + 1 == kRing ? 0 : nr + 1;
+        const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
+        const int32_t tend = min(t0 + kChunk, L);
+        for (int32_t t = t0; t < tend; ++t) {
+            const int64_t tv = l_ts[head_r * S_MAX];
+            const double v = l_amt[head_r * S_MAX];
+            const int64_t bound = tv - W;
+            // advance the window start, removing each row that leaves (Kahan remove)
+            while (tail < t) {
+                const bool in_ring = tail >= oldest;
+                const int64_t x = in_ring ? l_ts[tail_r * S_MAX] : g_ts[(int64_t)tail * S];
+                if (x > bound) break;
+                const double a = in_ring ? l_amt[tail_r * S_MAX] : g_amt[(int64_t)tail * S];
+                if (a == a) {
+                    nobs -= 1;
+                    const double y = -a - c_rem;
+                    const double tt = sum + y;
+                    c_rem = (tt - sum) - y;
+                    sum = tt;
                 }
-                if (nt >= t) {  // pandas re-initialises the window (start[i] >= end[i-1])
-                    st.reset(v);
-                    st.add(v);
-                } else {
-                    int jr = tail_r;
-                    for (int64_t j = tail; j < nt; ++j) {
-                        st.remove(j >= oldest ? r_amt[jr * S_MAX + l] : iamt[base + j * S]);
-                        jr = jr + 1 == kRing ? 0 : jr + 1;
-                    }
-                    st.add(v);
-                }
-                tail = nt;
-                tail_r = nr;
+                ++tail;
+                tail_r = tail_r + 1 == kRing ? 0 : tail_r + 1;
             }
-            const int64_t slot = base + t * S;
-            nb[slot] = st.nobs;
-            avg[slot] = st.value();  // rolling SUM: the division by nb is left to the consumer
+            // start[i] >= end[i-1] (or i == 0): pandas re-initialises the window state
+            if (tail >= t) {
+                sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
+            }
+            if (v == v) {  // Kahan add
+                nobs += 1;
+                const double y = v - c_add;
+                const double tt = sum + y;
+                c_add = (tt - sum) - y;
+                sum = tt;
+                nsame = (v == prev) ? nsame + 1 : 1;
+                prev = v;
+            }
+            const double val = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
+            nb[(int64_t)t * S] = nobs;
+            sm[(int64_t)t * S] = val;  // rolling SUM: the division by nb is left to the consumer
             head_r = head_r + 1 == kRing ? 0 : head_r + 1;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -339,24 +348,40 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 //   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
 // Segments up to kTermLdsRows rows are staged in LDS (timestamps + prefix counts) with
 // coalesced loads; longer ones are searched in global memory (L2) instead.
-// Output either column-major (nb_out/risk_out [W][n]) or, when rec_out != nullptr, one packed
-// record per row: ceil(W/2) words of int32 count pairs, then W float64 risks (the layout of
-// the multi-GPU reply records, read back by fdx_forest_prepare_grouped).
+// Output either column-major (nb_out/risk_out [W][n], grouped order) or, when rec_out !=
+// nullptr, one count record per row (W words NB | FRAUD << 32, see fdx.h) at rec_out[row].
+// With `rows` (the re-key perm), grouped position q reads ts/fraud of input row rows[q] and
+// its record goes to rec_out[rows[q]]: the gather and the scatter are fused into this kernel.
 __device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, int64_t *rec_out, int64_t n,
-                                           int32_t n_win, int64_t row, int w, int32_t cnt, double risk) {
+                                           int32_t n_win, int64_t q, int64_t row, int w, int32_t cnt,
+                                           int32_t fr) {
     if (rec_out) {
-        const int words = (n_win + 1) / 2 + n_win;
-        int32_t *r32 = reinterpret_cast<int32_t *>(rec_out + row * words);
-        r32[w] = cnt;
-        rec_out[row * words + (n_win + 1) / 2 + w] = __double_as_longlong(risk);
+        rec_out[row * n_win + w] = term_word(cnt, fr);
     } else {
-        nb_out[(int64_t)w * n + row] = cnt;
-        risk_out[(int64_t)w * n + row] = risk;
+        nb_out[(int64_t)w * n + q] = cnt;
+        risk_out[(int64_t)w * n + q] = cnt > 0 ? (double)fr / (double)cnt : 0.0;
     }
 }
 
+// timestamps of a segment read through the perm (global fallback for long segments)
+struct SegTs {
+    const int64_t *ts;
+    const int32_t *rows;
+    int64_t b;
+    __device__ __forceinline__ int64_t operator[](int64_t j) const { return rows ? ts[rows[b + j]] : ts[b + j]; }
+};
+
+__device__ __forceinline__ int64_t upper_bound_seg(const SegTs &a, int64_t lo, int64_t hi, int64_t x) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ void __launch_bounds__(kTermBlock) k_terminal(
-    const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud,
+    const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
     int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out) {
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
@@ -379,8 +404,9 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                 const int64_t j = c + lane;
                 int f = 0;
                 if (j < L) {
-                    lts[j] = ts[b + j];
-                    f = fraud[b + j] != 0;
+                    const int64_t src = rows ? rows[b + j] : b + j;
+                    lts[j] = ts[src];
+                    f = fraud[src] != 0;
                 }
                 int inc = wave_incl_scan(f, lane) + carry;
                 if (j < L) lf[j + 1] = inc;
@@ -393,30 +419,26 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                 const int64_t t = lts[i];
                 const int64_t hi = upper_bound(lts, 0, i, t - delay);
                 const int32_t fhi = lf[hi];
+                const int64_t row = rows ? rows[b + i] : b + i;  // coalesced re-read
                 for (int w = 0; w < n_win; ++w) {
                     const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
-                    const int32_t cnt = (int32_t)(hi - lo);
-                    const int32_t fr = fhi - lf[lo];
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, w, cnt,
-                               cnt > 0 ? (double)fr / (double)cnt : 0.0);
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), fhi - lf[lo]);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {
-            const int64_t *gts = ts + b;
-            const uint8_t *gf = fraud + b;
+            const SegTs gts{ts, rows, b};
             for (int64_t i = lane; i < L; i += kWave) {
                 const int64_t t = gts[i];
-                const int64_t hi = upper_bound(gts, 0, i, t - delay);
+                const int64_t hi = upper_bound_seg(gts, 0, i, t - delay);
+                const int64_t row = rows ? rows[b + i] : b + i;
                 for (int w = 0; w < n_win; ++w) {
-                    const int64_t lo = upper_bound(gts, 0, hi, t - delay - win.w[w]);
+                    const int64_t lo = upper_bound_seg(gts, 0, hi, t - delay - win.w[w]);
                     int32_t fr = 0;
-                    for (int64_t j = lo; j < hi; ++j) fr += gf[j] != 0;
-                    const int32_t cnt = (int32_t)(hi - lo);
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, w, cnt,
-                               cnt > 0 ? (double)fr / (double)cnt : 0.0);
+                    for (int64_t j = lo; j < hi; ++j) fr += fraud[rows ? rows[b + j] : b + j] != 0;
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), fr);
                 }
             }
         }
@@ -518,13 +540,14 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
-                       fraud_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, (int64_t *)nullptr);
+                       fraud_d, (const int32_t *)nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d,
+                       risk_d, (int64_t *)nullptr);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
 }
 
 extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
-                                           const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                           const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
                                            int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
                                            int64_t *rec_d, void *stream) {
     WinArgs wa;
@@ -536,7 +559,7 @@ extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && rec_d, "null pointer");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
-                       seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
+                       row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
                        rec_d);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
@@ -639,7 +662,7 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     // S_MAX = the LDS ring's segment stride: 21 for the reference's 3 windows
     static const int ring_env = [] {
         const char *e = getenv("FDX_CUSTOMER_RING");
-        return e ? atoi(e) : 192;
+        return e ? atoi(e) : 96;
     }();
     if (S <= 21 && ring_env == 96)
         hipLaunchKernelGGL((k_customer_ring<21, 96>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,

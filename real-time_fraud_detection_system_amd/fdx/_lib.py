@@ -53,7 +53,7 @@ SIGNATURES = {
     "fdx_customer_windows_interleaved": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_exclusive_scan_u32_workspace_size": (c_sz, [c_i64]),
     "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),
-    "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
+    "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
     "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),
     "fdx_rekey": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, c_sz, P]),
@@ -65,7 +65,6 @@ SIGNATURES = {
     "fdx_key_map": (ctypes.c_int, [P, c_i64, c_i32, c_i32, P, P]),
     "fdx_exchange_pack": (ctypes.c_int, [P, P, P, P, c_i64, P, P]),
     "fdx_exchange_unpack": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P]),
-    "fdx_reply_pack": (ctypes.c_int, [P, P, P, c_i64, c_i32, P, P]),
     "fdx_reply_assemble": (ctypes.c_int, [P, P, c_i64, c_i32, P, c_i64, c_i32, P]),
     "fdx_standard_scale": (ctypes.c_int, [P, c_i64, c_i32, c_i64, c_i64, P, P, P, c_i64, c_i64, P]),
     "fdx_forest_create": (ctypes.c_int, [ctypes.POINTER(ForestDesc), ctypes.POINTER(P), P]),

@@ -7,8 +7,8 @@ rows of a terminal on one rank: owner(t) = t % world.  Per step
 
   owner keys -> stable re-key by owner -> pack {ts, term|fraud|row} (16 B/row)
   -> all_to_all_single (splits exchanged first, 8 B per peer)
-  -> owner: unpack, time sort + re-key by local terminal id, terminal windows,
-     reply records (ceil(W/2)+W words/row) indexed by receive position
+  -> owner: unpack, time sort + re-key by local terminal id, terminal windows as count
+     records (W words/row: NB | FRAUD << 32) written straight to receive positions
   -> all_to_all_single back (splits mirrored) -> scatter into the local feature matrix
   -> scale + forest locally.
 
@@ -59,13 +59,8 @@ class GpuKernels:
     terminal_windows = staticmethod(ops.terminal_windows)
 
     @staticmethod
-    def reply_pack(nb, risk, perm, W):
-        m = perm.numel()
-        words = (W + 1) // 2 + W
-        rep = torch.empty((m, words), dtype=torch.int64, device=nb.device)
-        check(_lib.load().fdx_reply_pack(ops._ptr(nb), ops._ptr(risk), ops._ptr(perm), m, W, ops._ptr(rep),
-                                         ops._s()), "fdx_reply_pack")
-        return rep
+    def terminal_records(ts, fraud, rows, seg, delay_days, windows_days):
+        return ops.terminal_windows_packed(ts, fraud, seg, delay_days, windows_days, rows=rows)
 
     @staticmethod
     def reply_assemble(reply, perm, W, X, col0):
@@ -76,8 +71,8 @@ class GpuKernels:
 def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
                                delay_days=7, group=None):
     """Runs the re-key exchange and the owner-side terminal windows.  Returns
-    (reply [n_local, words] in send order, send_perm [n_local] send position -> local row)."""
-    W = len(windows_days)
+    (reply [n_local, W] count records in send order, send_perm [n_local] send position ->
+    local row)."""
     owner = K.owner_keys(term, world)
     send_perm, send_seg = K.rekey(owner, world)
     send_counts = (send_seg[1:] - send_seg[:-1]).to(torch.int64)
@@ -92,8 +87,7 @@ def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, win
     tperm = K.argsort_i64(rts)                                  # time order (stable)
     gperm, gseg = K.rekey(K.gather(rterm, tperm), n_local_terms)  # then by terminal (stable)
     perm = K.gather(tperm, gperm)                               # grouped position -> receive index
-    nb, risk = K.terminal_windows(K.gather(rts, perm), K.gather(rfr, perm), gseg, delay_days, windows_days)
-    reply = K.reply_pack(nb, risk, perm, W)
+    reply = K.terminal_records(rts, rfr, perm, gseg, delay_days, windows_days)  # indexed by receive index
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
     dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
     return back, send_perm

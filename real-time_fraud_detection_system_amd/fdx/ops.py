@@ -208,16 +208,36 @@ def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 
     return nb, avg
 
 
-def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), stream=None):
-    """Grouped rows -> packed records int64 [n, ceil(W/2)+W] (counts, then float64 risks)."""
+def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), rows=None,
+                            stream=None):
+    """Terminal windows as count records int64 [ts rows, W] (word = NB | FRAUD << 32).
+    rows=None: ts/fraud are grouped (time-sorted within terminal) and record q belongs to
+    grouped row q.  rows = the re-key perm (grouped position -> input row): ts/fraud are the
+    caller's arrays, read through the perm inside the kernel, and record r belongs to input
+    row r."""
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
+    if rows is not None:
+        _dev(rows, torch.int32, "rows")
+        if rows.numel() != ts_ns.numel():
+            raise ValueError("rows must have one entry per transaction")
     n = ts_ns.numel()
     W = len(windows_days)
-    rec = torch.empty((n, (W + 1) // 2 + W), dtype=torch.int64, device=ts_ns.device)
-    check(_lib.load().fdx_terminal_windows_packed(_ptr(ts_ns), _ptr(fraud), _ptr(seg_off), seg_off.numel() - 1, n,
-                                                  int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W,
-                                                  _ptr(rec), _s(stream)), "fdx_terminal_windows_packed")
+    rec = torch.empty((n, W), dtype=torch.int64, device=ts_ns.device)
+    check(_lib.load().fdx_terminal_windows_packed(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(seg_off),
+                                                  seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
+                                                  _win_ns(windows_days), W, _ptr(rec), _s(stream)),
+          "fdx_terminal_windows_packed")
     return rec
+
+
+def unpack_term_records(rec: torch.Tensor):
+    """Count records -> (nb int32 [W, n], risk float64 [W, n]) with the kernels' division."""
+    w = rec.T
+    nb = (w & 0xFFFFFFFF).to(torch.int32)
+    fr = (w >> 32) & 0xFFFFFFFF
+    risk = torch.where(nb > 0, fr.to(torch.float64) / nb.clamp(min=1).to(torch.float64),
+                       torch.zeros((), dtype=torch.float64, device=rec.device))
+    return nb, risk
 
 
 def invert_perm(perm: torch.Tensor, stream=None) -> torch.Tensor:

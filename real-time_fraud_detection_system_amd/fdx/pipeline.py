@@ -106,8 +106,8 @@ class FraudPipeline:
                   proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, on_traverse=None):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
-        layout (customer features already in place, the terminal half one packed record
-        per row); the last forest launch writes proba back in input row order."""
+        layout (customer features already in place, the terminal half one count record per
+        row, read by input row); the last forest launch writes proba back in input row order."""
         W = len(self.windows_days)
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
         lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
@@ -115,11 +115,11 @@ class FraudPipeline:
         self.last_slots = lay.n_slots
         inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
-        trec = ops.terminal_windows_packed(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
-                                           tseg, self.delay_days, self.windows_days, stream)
-        tinv = ops.invert_perm(tperm, stream)
+        # count records in input row order (the kernel reads ts/fraud through tperm)
+        trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days, rows=tperm,
+                                           stream=stream)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
-        ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, tinv, trec,
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
                                    ws, stream, n=lay.n_slots, val_is_sum=True)
         if on_traverse:
             on_traverse(0)

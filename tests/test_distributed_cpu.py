@@ -57,24 +57,22 @@ class CpuKernels:
         return torch.from_numpy(nb.astype(np.int32)), torch.from_numpy(risk)
 
     @staticmethod
-    def reply_pack(nb, risk, perm, W):
-        words = (W + 1) // 2 + W
-        rep = np.zeros((perm.numel(), words), np.int64)
-        nbn = nb.numpy().astype(np.int64) & 0xFFFFFFFF
-        for w in range(0, W, 2):
-            hi = nbn[w + 1] if w + 1 < W else 0
-            rep[perm.numpy(), w // 2] = nbn[w] | (hi << 32)
-        rep[perm.numpy(), (W + 1) // 2:] = risk.numpy().T.view(np.int64)
-        return torch.from_numpy(rep)
+    def terminal_records(ts, fraud, rows, seg, delay_days, windows_days):
+        """count records (NB | FRAUD << 32) of grouped row q stored at rows[q]"""
+        r = rows.numpy()
+        nb, risk = oracle.terminal_windows(ts.numpy()[r], fraud.numpy()[r], seg.numpy(), delay_days, windows_days)
+        fr = np.rint(risk * nb).astype(np.int64)  # counts are small integers: exact
+        rec = np.zeros((len(r), len(windows_days)), np.int64)
+        rec[r] = (nb.astype(np.int64) | (fr << 32)).T
+        return torch.from_numpy(rec)
 
     @staticmethod
     def unpack_reply(back, W):
         b = back.numpy()
-        nb = np.zeros((len(b), W))
-        for w in range(W):
-            word = b[:, w // 2]
-            nb[:, w] = ((word >> 32) if w % 2 else word) & 0xFFFFFFFF
-        risk = np.ascontiguousarray(b[:, (W + 1) // 2:]).view(np.float64)
+        nb = (b & 0xFFFFFFFF).astype(np.float64)
+        fr = ((b >> 32) & 0xFFFFFFFF).astype(np.float64)
+        with np.errstate(all="ignore"):
+            risk = np.where(nb > 0, fr / np.maximum(nb, 1), 0.0)
         return nb, risk
 
 

@@ -146,12 +146,18 @@ def test_windows_random_edge_cases(dev, max_len):
         np.testing.assert_array_equal(nb, onb)
         np.testing.assert_array_equal(risk, orisk)
         rec = ops.terminal_windows_packed(T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev),
-                                          7, windows).cpu().numpy()
+                                          7, windows)
         W = len(windows)
-        cnt = rec[:, : (W + 1) // 2].copy().view(np.int32)[:, :W]
-        np.testing.assert_array_equal(cnt.T, onb)
-        np.testing.assert_array_equal(rec[:, (W + 1) // 2:].copy().view(np.float64).T, orisk)
+        rnb, rrisk = ops.unpack_term_records(rec)
+        np.testing.assert_array_equal(rnb.cpu().numpy(), onb)
+        np.testing.assert_array_equal(rrisk.cpu().numpy(), orisk)
+        # rows=perm: inputs read through the perm, records land at the input row
         perm = np.random.default_rng(W).permutation(len(ts)).astype(np.int32)
+        ts_in = np.empty_like(ts); ts_in[perm] = ts
+        fr_in = np.empty_like(fr); fr_in[perm] = fr
+        rec2 = ops.terminal_windows_packed(T(ts_in, torch.int64, dev), T(fr_in, torch.uint8, dev),
+                                           T(seg, torch.int64, dev), 7, windows, rows=T(perm, torch.int32, dev))
+        np.testing.assert_array_equal(rec2.cpu().numpy()[perm], rec.cpu().numpy())
         inv = ops.invert_perm(T(perm, torch.int32, dev)).cpu().numpy()
         np.testing.assert_array_equal(inv[perm], np.arange(len(ts)))
 
@@ -295,7 +301,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(10)))
+@pytest.mark.parametrize("variant", list(range(16)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")

@@ -1,0 +1,47 @@
+"""Summarise rocprofv3 --pmc CSVs per kernel (per-dispatch means over the bench-size
+dispatches, i.e. those with the kernel's largest grid), and derive HBM traffic the way
+MI355X_MICROARCH.md prescribes: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
+reads half the bytes of wide coalesced streaming reads, so traffic = 2*FETCH + WRITE
+(upper estimate for the read side; ratios between variants are unaffected).
+
+usage: python tools/pmc_summary.py gpurun_out/pmc_r7 [kernel-substring ...]
+(reads <prefix>a ... <prefix>d directories)
+"""
+import collections
+import csv
+import glob
+import sys
+
+
+def load(prefix):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in sorted(glob.glob(prefix + "*")):
+        for f in glob.glob(d + "/*/*counter_collection.csv"):
+            rows = list(csv.DictReader(open(f)))
+            big = collections.defaultdict(int)
+            for r in rows:
+                big[r["Kernel_Name"]] = max(big[r["Kernel_Name"]], int(r["Grid_Size"]))
+            for r in rows:
+                if int(r["Grid_Size"]) == big[r["Kernel_Name"]]:
+                    per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    prefix = sys.argv[1]
+    keys = sys.argv[2:] or ["k_forest_chunk", "k_customer", "k_zfill", "k_interleave", "k_terminal"]
+    per = load(prefix)
+    for name, ctr in per.items():
+        if not any(k in name for k in keys):
+            continue
+        mean = {k: sum(v) / len(v) for k, v in ctr.items()}
+        print(name[:90])
+        for k in sorted(mean):
+            print(f"   {k:24s} {mean[k]:.4g}   (n={len(ctr[k])})")
+        if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+            t = (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
+            print(f"   HBM traffic per dispatch ~ {t / 1e9:.4f} GB (2*FETCH+WRITE)")
+
+
+if __name__ == "__main__":
+    main()
