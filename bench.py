@@ -23,9 +23,16 @@ sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
 
 METRIC = "transactions/sec featurized+scored (1/2/4/8 GPU) + % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# algorithmic bytes per row of one k_forest_chunk launch: scaled float32 features
+# algorithmic bytes per row of the forest launches: every launch reads the row
+# (rank layout: 16 x u16 = 32 B; wide layout: 16 x float32 = 64 B), the running float64 sum
+# crosses launches (8 B in, 8 B out except the first / last), the last launch writes proba.
+RANK_ROW_BYTES, WIDE_ROW_BYTES = 32, 64
 # (16 x 4 B slots) in + running float64 sum in + float64 sum/proba out
-FOREST_CHUNK_BYTES_PER_ROW = 64 + 8 + 8
+
+
+def forest_bytes_per_row(variant, n_chunks):
+    row = RANK_ROW_BYTES if variant >= 16 else WIDE_ROW_BYTES
+    return row * n_chunks + 16 * (n_chunks - 1) + 8
 
 
 def parse():
@@ -42,7 +49,8 @@ def parse():
     ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
     ap.add_argument("--slab-rows", type=int, default=0, help="forest traversal slab rows (0 = all rows)")
     ap.add_argument("--sweep-slab", default="", help="comma list of slab sizes to time (stderr)")
-    ap.add_argument("--forest-variant", type=int, default=1, help="traversal kernel shape (fdx_forest_set_variant)")
+    ap.add_argument("--forest-variant", type=int, default=-1,
+                    help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     return ap.parse_args()
 
@@ -101,7 +109,9 @@ def main():
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
     forest.set_slab_rows(args.slab_rows)
-    forest.set_variant(args.forest_variant)
+    default_variant = forest.variant
+    if args.forest_variant >= 0:
+        forest.set_variant(args.forest_variant)
     T = lambda a, d: torch.from_numpy(np.ascontiguousarray(a)).to(dev, d)  # noqa: E731
     # sanity: the GPU forest reproduces sklearn on the held-out sample saved with the model
     got = forest.predict(T(check_X, torch.float64)).cpu().numpy()
@@ -169,7 +179,9 @@ def main():
     launches = forest.n_chunks * -(-n_local // slab)
     launch_ms = trav_ms / launches
     # every launch streams its slab's rows once: total algorithmic bytes / total time
-    achieved = FOREST_CHUNK_BYTES_PER_ROW * n_local * forest.n_chunks / (trav_ms * 1e-3) / 1e9
+    fvar = forest.variant if args.forest_variant < 0 else args.forest_variant
+    bpr = forest_bytes_per_row(fvar, forest.n_chunks)
+    achieved = bpr * n_local / (trav_ms * 1e-3) / 1e9
     out = {
         "metric": METRIC,
         "value": round(n_total * args.steps / dt, 1),
@@ -187,12 +199,13 @@ def main():
                                f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
                    "tx_per_gpu": n_local, "global_tx": n_total, "parallelism": f"customer-sharded x{world}",
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)"},
-        "roofline": {"kernel": "k_forest_chunk", "bound": "hbm", "achieved": round(achieved, 1),
+        "roofline": {"kernel": "k_forest_rank" if fvar >= 16 else "k_forest_chunk", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "avg_launch_ms": round(launch_ms, 4),
                      "launches_per_step": launches,
                      "traverse_ms": round(trav_ms, 3),
-                     "bytes_per_row_per_launch": FOREST_CHUNK_BYTES_PER_ROW},
+                     "forest_variant": fvar,
+                     "bytes_per_row_per_launch": round(bpr / forest.n_chunks, 2)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, args.cpu_sample_customers)
@@ -211,23 +224,25 @@ def main():
         forest.set_slab_rows(args.slab_rows)
         print(json.dumps({"slab_sweep_traverse_ms": res}), file=sys.stderr)
     if args.sweep_variant and rank == 0:
+        # each variant: one full untimed pipeline pass (the prepared row format depends on
+        # the layout), bit-equality of proba against the default, then 3 timed traversals
         res = {}
-        ws, n_rows = pipe._forest_ws(pipe.last_slots, ws, dev), pipe.last_slots
-        ref = torch.empty(n_rows, dtype=torch.float64, device=dev)
-        ops.forest_traverse(forest, n_rows, ws, ref)
+        ref = proba.clone()
         for v in [int(x) for x in args.sweep_variant.split(",")]:
             forest.set_variant(v)
-            pv = torch.empty_like(ref)
-            ops.forest_traverse(forest, n_rows, ws, pv)
+            pv = torch.empty_like(proba)
+            pipe.run_fused(ts, cust, term, amt, fr, args.customers, args.terminals, pv, ws)
             same = bool(torch.equal(pv, ref))
+            wsv, n_rows = pipe._forest_ws(pipe.last_slots, ws, dev), pipe.last_slots
+            buf = torch.empty(n_rows, dtype=torch.float64, device=dev)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for _ in range(3):
-                ops.forest_traverse(forest, n_rows, ws, pv)
+                ops.forest_traverse(forest, n_rows, wsv, buf)
             b.record()
             torch.cuda.synchronize()
             res[v] = {"ms": round(a.elapsed_time(b) / 3, 3), "chunks": forest.n_chunks, "bit_equal": same}
-        forest.set_variant(args.forest_variant)
+        forest.set_variant(args.forest_variant if args.forest_variant >= 0 else default_variant)
         print(json.dumps({"variant_sweep_traverse": res}), file=sys.stderr)
     if args.breakdown and rank == 0:
         print(json.dumps(stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba)),

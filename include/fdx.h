@@ -233,6 +233,21 @@ int fdx_forest_create(const fdx_forest_desc *desc, fdx_forest *out, void *stream
  * packed node, root_out [n_trees] packed position of each root. */
 int fdx_forest_pack(const fdx_forest_desc *desc, uint64_t *nodes_out, int32_t *orig_out,
                     int32_t *root_out);
+/* Host-only: the RANK layout fdx_forest_create builds when the forest fits it (<= 15
+ * features, <= 32767 distinct float32 thresholds per feature, every tree within the LDS
+ * node budget; else FDX_E_UNSUPPORTED and the wide 8-byte layout is used).  Per feature f,
+ * U_f = thr_out[thr_off_out[f] .. thr_off_out[f+1]) are the sorted distinct thresholds
+ * (float32 rounded toward -inf); a row value x becomes r = #{u in U_f : u < x}.
+ * nodes_out (4 B): [31:17] threshold rank k, [15:12] feature (15 = leaf / jump),
+ * [11:0] right-child offset (left child = next node; go left iff r <= k); a leaf is
+ * 0x0000F000, a jump node 0xF000 | d forwards to the node d further.  orig_out = sklearn
+ * node id per node (-1 for jumps), leaf_value_out = value1 of leaves, missing_left_out =
+ * missing_go_to_left, root_out/depth_out per tree (depth = max steps incl. jumps),
+ * thr_off_out [17].  Sizes from fdx_forest_rank_layout_size. */
+int fdx_forest_rank_layout_size(const fdx_forest_desc *desc, int64_t *n_nodes, int32_t *n_thresholds);
+int fdx_forest_pack_rank(const fdx_forest_desc *desc, uint32_t *nodes_out, int32_t *orig_out,
+                         double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out,
+                         int32_t *depth_out, float *thr_out, int32_t *thr_off_out);
 int fdx_forest_destroy(fdx_forest forest);
 int fdx_forest_info(fdx_forest forest, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
                     int32_t *n_chunks);
@@ -254,12 +269,18 @@ int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *
 /* Rows per traversal slab (all chunks run over one slab before the next, so that the
  * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
 int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
-/* Traversal kernel shape: 0 = 512 threads x 1 row x 4 trees per lane, 1 = 1024 x 1 x 4
- * (default when <= 16 features), 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4,
- * 5 = 1024 x 1 x 3, 6 = 512 x 1 x 3, 7 = 768 x 1 x 3, 8 = 768 x 1 x 4, 9 = 1024 x 1 x 2
- * (threads x rows per lane x trees per walk group; variants > 0 need <= 16 features).
- * Re-cuts the LDS chunks; results are identical for every variant. */
+/* Traversal kernel shape.  Wide layout (8-byte nodes, float32 rows): 0 = 512 threads x 1
+ * row x 4 trees per lane, 1 = 1024 x 1 x 4, 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4,
+ * 5 = 1024 x 1 x 3, 6 = 512 x 1 x 3, 7 = 768 x 1 x 3, 8 = 768 x 1 x 4, 9 = 1024 x 1 x 2,
+ * 10 = 768 x 1 x 2, 11 = 768 x 2 x 2, 12-15 = rows-resident tile kernels.  Rank layout
+ * (4-byte nodes, u16 rank rows; see fdx_forest_pack_rank): 16 = 1024 x 1 x 4 (the default
+ * when the forest fits the rank layout), 17 = 1024 x 1 x 2, 18 = 512 x 2 x 2,
+ * 19 = 512 x 2 x 4, 20 = 1024 x 1 x 3, 21 = 768 x 1 x 4, 22 = 256 x 4 x 2, 23 = 1024 x 1 x 6.
+ * Variants > 0 need <= 16 features, 16+ need the rank layout (FDX_E_UNSUPPORTED otherwise).
+ * Re-cuts the LDS chunks; results are identical for every variant.  The row format of a
+ * prepared workspace depends on the layout: prepare again after switching layouts. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
+int fdx_forest_get_variant(fdx_forest forest, int32_t *variant);
 
 /* Fused assemble + scale for the scoring pipeline: writes the forest's float32 feature
  * rows in the workspace straight from the window kernels' grouped outputs (same columns

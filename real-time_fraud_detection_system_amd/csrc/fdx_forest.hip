@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <vector>
 
@@ -53,6 +54,16 @@ struct fdx_forest_s {
     int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or all rows)
     int variant = 0;        // index into kVariants
     std::vector<int64_t> node_offsets;  // host copy (chunking)
+    // rank layout (4-byte nodes over per-feature threshold ranks, see "Rank layout" below)
+    bool rank_ok = false;
+    std::vector<int64_t> rank_offsets;  // [n_trees+1] first rank-layout node of each tree
+    int64_t rank_nodes = 0;
+    uint32_t *rnodes_d = nullptr;
+    int32_t *rorig_d = nullptr, *rroot_d = nullptr, *rdepth_d = nullptr;
+    double *rlval_d = nullptr;
+    uint8_t *rml_d = nullptr;
+    float *rthr_d = nullptr;
+    int32_t rthr_off[16] = {}, rthr_cnt[16] = {};
 };
 
 namespace fdx {
@@ -62,12 +73,111 @@ constexpr uint32_t kInternal = 0x80000000u;
 
 __device__ __forceinline__ double leaf_value(uint64_t nd) { return __longlong_as_double((long long)nd); }
 
-// z32[r][f] = (float)((x - mean[f]) / scale[f]); slots >= nf are 0.
-template <int FS>
+// ---------------------------------------------------------------------- rank layout
+// The traversal is VALU-issue bound (r01 PMC: ~0.85 VALU wave-instructions / clk / CU in
+// k_forest_chunk), so the default layout is the one with the fewest instructions per step.
+// Per feature f, U_f = sorted unique float32 thresholds (thr32_down) of the forest.  A row
+// value x is replaced by its rank r_f(x) = #{u in U_f : u < x} (lower_bound), and a node
+// with threshold U_f[k] by k:  x <= U_f[k]  <=>  r_f(x) <= k  (exact, U_f sorted unique).
+// 4-byte node:  [31:17] k  [16] 0  [15:12] feature  [11:0] right offset in nodes (left = p+1)
+// Row values in LDS are r << 17 in a [16][1024] u32 plane array at LDS offset 0, so
+//   feature address = (node & 0xF000) | lane_base          (one v_and_or_b32)
+//   go left         = x <= node  (unsigned: r << 17 <= k << 17 | low17  <=>  r <= k)
+//   next address    = addr + 4 * (left ? 1 : node & 0xFFF)   (and, cndmask, lshl_add)
+// Feature slot 15 holds 0x7FFF << 17 for every row, so a node with feature 15 always goes
+// right: a LEAF is 0x0000F000 (right offset 0 = fixed point) and a JUMP node (0xF000 | d)
+// forwards to p + d -- the packer inserts jumps after leaves wherever a right offset would
+// exceed 4095.  Leaf values (float64) and sklearn node ids live in global arrays indexed by
+// rank-layout position; NaN row values are 0xFFFF (u16) / 0xFFFFFFFF (LDS), resolved by
+// missing_go_to_left from a global byte array in the NaN-aware walk.  Ranks travel through
+// HBM as 16 x u16 = 32 B per row (half the float32 row).
+constexpr uint32_t kRankLeaf = 0x0000F000u;
+constexpr int kRankMaxOffset = 4095;
+constexpr int kRankMaxRank = 32766;  // k <= 32766 < 0x7FFF (the slot-15 sentinel)
+constexpr int kRankPlaneRows = 1024;
+constexpr int kRankXWords = 16 * kRankPlaneRows;  // 64 KiB of row planes
+
+struct RankTab {
+    const float *u;  // concatenated U_f
+    int32_t off[16], cnt[16];
+};
+
+// lower_bound(U_f, v) - U_f, branch-free (Khuong & Morin); NaN -> 0xFFFF
+__device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u, int32_t n) {
+    if (v != v) return 0xFFFFu;
+    if (n <= 0) return 0u;
+    const float *b = u;
+    while (n > 1) {
+        const int32_t h = n >> 1;
+        b = (b[h] < v) ? b + h : b;
+        n -= h;
+    }
+    return (uint32_t)(b - u) + (uint32_t)(*b < v);
+}
+
+// ranks of a whole row; the searches of all features advance together (independent loads)
+__device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const RankTab &rt, uint32_t (&out)[16]) {
+    const float *b[16];
+    int32_t n[16];
+    int32_t nmax = 0;
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+        b[f] = rt.u + rt.off[f];
+        n[f] = f < nf ? rt.cnt[f] : 0;
+        nmax = max(nmax, n[f]);
+    }
+    while (nmax > 1) {
+        nmax = 0;
+#pragma unroll
+        for (int f = 0; f < 16; ++f) {
+            if (n[f] > 1) {
+                const int32_t h = n[f] >> 1;
+                b[f] = (b[f][h] < v[f]) ? b[f] + h : b[f];
+                n[f] -= h;
+            }
+            nmax = max(nmax, n[f]);
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+        if (f >= nf) out[f] = 0u;
+        else if (v[f] != v[f]) out[f] = 0xFFFFu;
+        else if (n[f] <= 0) out[f] = 0u;
+        else out[f] = (uint32_t)(b[f] - (rt.u + rt.off[f])) + (uint32_t)(*b[f] < v[f]);
+    }
+}
+
+// Row writers of the prepare kernels: float32 rows [n][FS], or rank rows [n][16] u16.
+template <int FS, bool RANK>
+__device__ __forceinline__ void store_row(void *z, int64_t r, const float (&v)[FS], int nf, const RankTab &rt) {
+    if constexpr (RANK) {
+        static_assert(FS == 16, "rank rows have 16 slots");
+        uint32_t q[16];
+        rank_row(v, nf, rt, q);
+        uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + r * 16);
+        dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
+        dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
+    } else {
+        float4 *dst = reinterpret_cast<float4 *>(reinterpret_cast<float *>(z) + r * FS);
+#pragma unroll
+        for (int q = 0; q < FS / 4; ++q) dst[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+}
+
+template <int FS, bool RANK>
+__device__ __forceinline__ void store_col(void *z, int64_t r, int col, float v, const RankTab &rt) {
+    if constexpr (RANK)
+        reinterpret_cast<uint16_t *>(z)[r * 16 + col] = (uint16_t)rank_of(v, rt.u + rt.off[col], rt.cnt[col]);
+    else
+        reinterpret_cast<float *>(z)[r * FS + col] = v;
+}
+
+// z32[r][f] = (float)((x - mean[f]) / scale[f]) (or its rank); slots >= nf are 0.
+template <int FS, bool RANK>
 __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, int64_t n, int64_t rs,
                                                  int64_t cs, int32_t nf, const double *__restrict__ mean,
-                                                 const double *__restrict__ scale,
-                                                 float *__restrict__ z, int32_t *__restrict__ nan_flag) {
+                                                 const double *__restrict__ scale, void *__restrict__ z,
+                                                 int32_t *__restrict__ nan_flag, RankTab rt) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
@@ -85,9 +195,7 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
             }
         }
         if (nan) *nan_flag = 1;  // routes the traversal through the NaN-aware step
-        float4 *dst = reinterpret_cast<float4 *>(z + r * FS);
-#pragma unroll
-        for (int q = 0; q < FS / 4; ++q) dst[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        store_row<FS, RANK>(z, r, v, nf, rt);
     }
 }
 
@@ -116,39 +224,40 @@ __device__ __forceinline__ float zval(double x, const double *mean, const double
 
 // Fused assemble + scale: the scoring pipeline writes the forest's float32 feature rows
 // directly (no float64 feature matrix round trip).  Columns follow input_features.
-template <int FS>
+template <int FS, bool RANK>
 __global__ void __launch_bounds__(256) k_zfill_time(const double *__restrict__ amount,
                                                    const uint8_t *__restrict__ weekend,
                                                    const uint8_t *__restrict__ night, int64_t n,
                                                    const double *__restrict__ mean,
-                                                   const double *__restrict__ scale, float *__restrict__ z,
-                                                   int32_t *__restrict__ nan_flag) {
+                                                   const double *__restrict__ scale, void *__restrict__ z,
+                                                   int32_t *__restrict__ nan_flag, RankTab rt) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
-        float *o = z + r * FS;
         const float a = zval(amount[r], mean, scale, 0);
-        o[0] = a;
-        o[1] = zval((double)weekend[r], mean, scale, 1);
-        o[2] = zval((double)night[r], mean, scale, 2);
+        store_col<FS, RANK>(z, r, 0, a, rt);
+        store_col<FS, RANK>(z, r, 1, zval((double)weekend[r], mean, scale, 1), rt);
+        store_col<FS, RANK>(z, r, 2, zval((double)night[r], mean, scale, 2), rt);
+        if (RANK) store_col<FS, RANK>(z, r, 15, 0.0f, rt);  // unused slot: defined bytes
         if (a != a) *nan_flag = 1;
     }
 }
 
-template <int FS>
+template <int FS, bool RANK>
 __global__ void __launch_bounds__(256) k_zfill_group(const int32_t *__restrict__ perm,
                                                     const int32_t *__restrict__ nb,
                                                     const double *__restrict__ val, int64_t n, int32_t W,
                                                     int32_t col0, const double *__restrict__ mean,
-                                                    const double *__restrict__ scale, float *__restrict__ z,
-                                                    int32_t *__restrict__ nan_flag) {
+                                                    const double *__restrict__ scale, void *__restrict__ z,
+                                                    int32_t *__restrict__ nan_flag, RankTab rt) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        float *o = z + (int64_t)perm[i] * FS + col0;
+        const int64_t o = perm[i];
         bool nan = false;
         for (int w = 0; w < W; ++w) {
-            o[2 * w] = zval((double)nb[(int64_t)w * n + i], mean, scale, col0 + 2 * w);
+            store_col<FS, RANK>(z, o, col0 + 2 * w, zval((double)nb[(int64_t)w * n + i], mean, scale, col0 + 2 * w),
+                                rt);
             const float v = zval(val[(int64_t)w * n + i], mean, scale, col0 + 2 * w + 1);
-            o[2 * w + 1] = v;
+            store_col<FS, RANK>(z, o, col0 + 2 * w + 1, v, rt);
             nan |= v != v;
         }
         if (nan) *nan_flag = 1;
@@ -156,21 +265,21 @@ __global__ void __launch_bounds__(256) k_zfill_group(const int32_t *__restrict__
 }
 
 // same, from the multi-GPU count records (fdx_terminal_windows_packed), row j -> perm[j]
-template <int FS>
+template <int FS, bool RANK>
 __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__ reply,
                                                     const int32_t *__restrict__ perm, int64_t n, int32_t W,
                                                     int32_t col0, const double *__restrict__ mean,
-                                                    const double *__restrict__ scale, float *__restrict__ z,
-                                                    int32_t *__restrict__ nan_flag) {
+                                                    const double *__restrict__ scale, void *__restrict__ z,
+                                                    int32_t *__restrict__ nan_flag, RankTab rt) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
          j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t *r = reply + j * W;
-        float *o = z + (int64_t)perm[j] * FS + col0;
+        const int64_t o = perm[j];
         bool nan = false;
         for (int w = 0; w < W; ++w) {
-            o[2 * w] = zval((double)term_nb(r[w]), mean, scale, col0 + 2 * w);
+            store_col<FS, RANK>(z, o, col0 + 2 * w, zval((double)term_nb(r[w]), mean, scale, col0 + 2 * w), rt);
             const float v = zval(term_risk(r[w]), mean, scale, col0 + 2 * w + 1);
-            o[2 * w + 1] = v;
+            store_col<FS, RANK>(z, o, col0 + 2 * w + 1, v, rt);
             nan |= v != v;
         }
         if (nan) *nan_flag = 1;
@@ -181,24 +290,31 @@ __global__ void __launch_bounds__(256) k_zfill_reply(const int64_t *__restrict__
 // holds the transaction r = cust_perm[i]; amount / time flags / customer windows are
 // already in this order, the terminal half is one count record read from
 // term_rec[term_inv[r]] (term_inv: row -> send position; NULL = records already by row).
-template <int FS>
+template <int FS, bool RANK>
 __global__ void __launch_bounds__(256) k_zfill_grouped(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t W, int32_t flags_mode, int32_t val_is_sum,
-    const double *__restrict__ mean, const double *__restrict__ scale, float *__restrict__ z,
-    int32_t *__restrict__ nan_flag) {
+    const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
+    int32_t *__restrict__ nan_flag, RankTab rt) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
+    const int nf = 3 + 4 * W;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
 #pragma unroll
         for (int f = 0; f < FS; ++f) v[f] = 0.0f;
         const int32_t r = cust_perm[i];
-        if (r < 0) {  // padding slot of the interleaved layout
-            float4 *dst = reinterpret_cast<float4 *>(z + i * FS);
+        if (r < 0) {  // padding slot of the interleaved layout: never written back
+            if constexpr (RANK) {
+                uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
+                dst[0] = make_uint4(0, 0, 0, 0);
+                dst[1] = make_uint4(0, 0, 0, 0);
+            } else {
+                float4 *dst = reinterpret_cast<float4 *>(reinterpret_cast<float *>(z) + i * FS);
 #pragma unroll
-            for (int qd = 0; qd < FS / 4; ++qd) dst[qd] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int qd = 0; qd < FS / 4; ++qd) dst[qd] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             continue;
         }
         const int64_t t = cts[i];
@@ -229,9 +345,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             }
         }
         if (nan) *nan_flag = 1;
-        float4 *dst = reinterpret_cast<float4 *>(z + i * FS);
-#pragma unroll
-        for (int qd = 0; qd < FS / 4; ++qd) dst[qd] = make_float4(v[4 * qd], v[4 * qd + 1], v[4 * qd + 2], v[4 * qd + 3]);
+        store_row<FS, RANK>(z, i, v, nf, rt);
     }
 }
 
@@ -244,13 +358,19 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 // Kernel variants (block size, rows per lane R, trees per walk group G).  LDS holds the
 // row features [FS][BLOCK*R] float32 and, in the rest of the 160 KiB, the chunk's nodes.
 // tile = 1: k_forest_tile (rows resident, trees streamed) instead of k_forest_chunk.
+// rank = 1: k_forest_rank over the rank layout (4-byte nodes, u16 rank rows).
 struct Variant {
-    int block, rows, group, tile;
+    int block, rows, group, tile, rank;
 };
-constexpr Variant kVariants[] = {{512, 1, 4, 0},  {1024, 1, 4, 0}, {512, 2, 4, 0}, {512, 2, 2, 0},
-                                 {256, 2, 4, 0},  {1024, 1, 3, 0}, {512, 1, 3, 0}, {768, 1, 3, 0},
-                                 {768, 1, 4, 0},  {1024, 1, 2, 0}, {768, 1, 2, 0}, {768, 2, 2, 0},
-                                 {1024, 1, 2, 1}, {512, 2, 1, 1},  {512, 3, 1, 1}, {768, 2, 1, 1}};
+constexpr int kFirstRankVariant = 16;
+constexpr Variant kVariants[] = {
+    {512, 1, 4, 0, 0},  {1024, 1, 4, 0, 0}, {512, 2, 4, 0, 0},  {512, 2, 2, 0, 0},  {256, 2, 4, 0, 0},
+    {1024, 1, 3, 0, 0}, {512, 1, 3, 0, 0},  {768, 1, 3, 0, 0},  {768, 1, 4, 0, 0},  {1024, 1, 2, 0, 0},
+    {768, 1, 2, 0, 0},  {768, 2, 2, 0, 0},  {1024, 1, 2, 1, 0}, {512, 2, 1, 1, 0},  {512, 3, 1, 1, 0},
+    {768, 2, 1, 1, 0},
+    // rank layout (k_forest_rank)
+    {1024, 1, 4, 0, 1}, {1024, 1, 2, 0, 1}, {512, 2, 2, 0, 1},  {512, 2, 4, 0, 1},  {1024, 1, 3, 0, 1},
+    {768, 1, 4, 0, 1},  {256, 4, 2, 0, 1},  {1024, 1, 6, 0, 1}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -490,6 +610,137 @@ __global__ void __launch_bounds__(BLOCK) k_forest_tile(
     }
 }
 
+// Rank-layout walk step (see "Rank layout"): 5 VALU + 2 LDS reads per chain.  pa = LDS byte
+// address of the chain's node, nd = that node.
+constexpr uint32_t kRankNodeB = kRankXWords * 4;  // byte offset of the node region in LDS
+template <bool NAN_AWARE, int K>
+__device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
+                                          uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
+    uint32_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = *reinterpret_cast<const uint32_t *>(lds + ((nd[k] & 0xF000u) | lane_base[k]));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bool left = x[k] <= nd[k];
+        if (NAN_AWARE && x[k] == 0xFFFFFFFFu) left = mleft[(pa[k] - kRankNodeB) >> 2] != 0;
+        const uint32_t st = left ? 1u : (nd[k] & 0xFFFu);
+        pa[k] += st << 2;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) nd[k] = *reinterpret_cast<const uint32_t *>(lds + pa[k]);
+}
+
+template <bool NAN_AWARE, int K>
+__device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
+                                          uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft) {
+    int d = 0;
+    for (; d + kExitEvery <= depth; d += kExitEvery) {
+#pragma unroll
+        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, K>(lds, lane_base, pa, nd, mleft);
+        uint32_t moving = 0;  // leaves (and only leaves) have right offset 0
+#pragma unroll
+        for (int k = 0; k < K; ++k) moving |= nd[k] & 0xFFFu;
+        if (!__any(moving != 0)) return;
+    }
+    for (; d < depth; ++d) rank_step<NAN_AWARE, K>(lds, lane_base, pa, nd, mleft);
+}
+
+// One launch = trees [t0, t1) of one LDS chunk over rows [r0, r1), rank layout.  Each lane
+// walks G trees for each of its R rows (K = R*G chains); the float64 running sum crosses
+// launches through acc in tree order, exactly like k_forest_chunk.
+template <int BLOCK, int R, int G>
+__global__ void __launch_bounds__(BLOCK) k_forest_rank(
+    const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
+    const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
+    const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1, const double *__restrict__ lval,
+    const uint8_t *__restrict__ mleft, double *__restrict__ acc, double *__restrict__ proba,
+    const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
+    int32_t n_trees, int first, int last) {
+    static_assert(BLOCK * R <= kRankPlaneRows, "row planes hold 1024 rows");
+    constexpr int K = R * G;
+    constexpr int kRowsPerBlock = BLOCK * R;
+    constexpr int kNodeWords = (kLdsTotal - kRankXWords * 4) / 4;
+    __shared__ __align__(16) uint32_t s_mem[kRankXWords + kNodeWords];
+    const char *lds = reinterpret_cast<const char *>(s_mem);
+    const int tid = threadIdx.x;
+    const uint32_t *nb = nodes + node_base;
+    const uint8_t *ml = mleft + node_base;
+    for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = nb[i];
+    if (tid == 0) s_mem[kRankXWords + kNodeWords - 1] = kRankLeaf;  // parking leaf of idle chains
+#pragma unroll
+    for (int r = 0; r < R; ++r) s_mem[15 * kRankPlaneRows + r * BLOCK + tid] = 0x7FFFu << 17;  // slot-15 sentinel
+    __syncthreads();
+    const bool any_nan = *nan_flag != 0;  // uniform
+    uint32_t lane_base[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) lane_base[k] = (uint32_t)(((k / G) * BLOCK + tid) * 4);
+    for (int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock; base < r1;
+         base += (int64_t)gridDim.x * kRowsPerBlock) {
+        int64_t row[R];
+        bool ok[R];
+        double a[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            row[r] = base + r * BLOCK + tid;
+            ok[r] = row[r] < r1;
+            const uint4 *src = reinterpret_cast<const uint4 *>(zr + (ok[r] ? row[r] : r0) * 16);
+            const uint4 q0 = src[0], q1 = src[1];
+            const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+            for (int f = 0; f < 15; ++f) {
+                const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
+                s_mem[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 17;
+            }
+            a[r] = (first || !ok[r]) ? 0.0 : acc[row[r]];
+        }
+        for (int t = t0; t < t1; t += G) {
+            uint32_t pa[K], nd[K];
+            int dmax = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const bool act = t + g < t1;
+                const uint32_t p0 = act ? kRankNodeB + (uint32_t)(root[t + g] - node_base) * 4u
+                                        : kRankNodeB + (uint32_t)(kNodeWords - 1) * 4u;
+                const uint32_t n0 = *reinterpret_cast<const uint32_t *>(lds + p0);
+                dmax = act ? max(dmax, depth[t + g]) : dmax;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    pa[r * G + g] = p0;
+                    nd[r * G + g] = n0;
+                }
+            }
+            if (any_nan)
+                rank_walk<true, K>(lds, lane_base, pa, nd, dmax, ml);
+            else
+                rank_walk<false, K>(lds, lane_base, pa, nd, dmax, ml);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (t + g < t1) {
+                        const int64_t p = node_base + ((pa[r * G + g] - kRankNodeB) >> 2);
+                        a[r] += lval[p];
+                        if (leaf_out && ok[r]) {
+                            const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+                            if (dst >= 0) leaf_out[dst * n_trees + t + g] = orig[p];
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!ok[r]) continue;
+            if (last) {
+                const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+                if (dst >= 0) proba[dst] = a[r] / (double)n_trees;  // < 0: padding slot
+            } else {
+                acc[row[r]] = a[r];
+            }
+        }
+    }
+}
+
 int64_t forest_slab_rows() {
     static int64_t v = [] {
         const char *e = getenv("FDX_FOREST_SLAB_ROWS");
@@ -605,6 +856,137 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
     }
     return FDX_OK;
 }
+
+// Rank layout (see the device-side comment "Rank layout") built from the wide packing.
+struct RankLayout {
+    std::vector<uint32_t> nodes;
+    std::vector<int32_t> orig, root, depth;
+    std::vector<double> lval;
+    std::vector<uint8_t> ml;
+    std::vector<int64_t> offsets;
+    std::vector<float> thr;
+    int32_t thr_off[17] = {};
+};
+
+// Returns FDX_OK, or FDX_E_UNSUPPORTED (with the reason in fdx_last_error) when the forest
+// does not fit the layout (> 15 features, > 32767 distinct thresholds of one feature, a
+// tree larger than the LDS node budget).  `max_tree_nodes` = LDS node budget per chunk.
+int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
+                      const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
+                      RankLayout &L) {
+    if (d->n_features > 15) {
+        set_error("rank layout: %d features > 15", d->n_features);
+        return FDX_E_UNSUPPORTED;
+    }
+    // U_f: sorted unique float32 thresholds per feature
+    std::vector<std::vector<float>> U(16);
+    for (uint64_t nd : packed)
+        if (nd >> 63) {
+            const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
+            float t;
+            memcpy(&t, &lo, 4);
+            U[(hi >> 24) & 63].push_back(t);
+        }
+    L.thr.clear();
+    for (int f = 0; f < 16; ++f) {
+        auto &u = U[f];
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end(), [](float a, float b) { return a == b; }), u.end());
+        if ((int64_t)u.size() > kRankMaxRank + 1) {
+            set_error("rank layout: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank + 1);
+            return FDX_E_UNSUPPORTED;
+        }
+        L.thr_off[f] = (int32_t)L.thr.size();
+        L.thr.insert(L.thr.end(), u.begin(), u.end());
+    }
+    L.thr_off[16] = (int32_t)L.thr.size();
+    L.nodes.clear(); L.orig.clear(); L.lval.clear(); L.ml.clear(); L.root.clear(); L.depth.clear();
+    L.offsets.assign(1, 0);
+    struct Pend { int64_t owner; };
+    std::vector<Pend> pend;
+    int margin = 0;
+    bool ok = true;
+    auto push = [&](uint32_t node, int32_t o, double v, uint8_t m) {
+        L.nodes.push_back(node); L.orig.push_back(o); L.lval.push_back(v); L.ml.push_back(m);
+    };
+    auto set_off = [&](int64_t pos, int64_t off) {
+        if (off < 1 || off > kRankMaxOffset) ok = false;
+        L.nodes[(size_t)pos] = (L.nodes[(size_t)pos] & ~0xFFFu) | (uint32_t)(off & 0xFFF);
+    };
+    // pre-order emission; after every leaf, pending right pointers that are about to run out
+    // of range are forwarded through a jump node placed right there (the slot after a leaf
+    // is only ever reached through a right pointer, so nothing else moves semantically)
+    std::function<void(int64_t)> emit = [&](int64_t w) {
+        const uint64_t nd = packed[(size_t)w];
+        const int64_t pos = (int64_t)L.nodes.size();
+        if (!(nd >> 63)) {
+            double v;
+            memcpy(&v, &nd, 8);
+            push(kRankLeaf, worig[(size_t)w], v, 0);
+            for (auto &p : pend)
+                if ((int64_t)L.nodes.size() - p.owner + margin > kRankMaxOffset) {
+                    const int64_t j = (int64_t)L.nodes.size();
+                    push(kRankLeaf, -1, 0.0, 0);
+                    set_off(p.owner, j - p.owner);
+                    p.owner = j;
+                }
+            return;
+        }
+        const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
+        const int f = (int)((hi >> 24) & 63);
+        float t;
+        memcpy(&t, &lo, 4);
+        const auto &u = U[f];
+        const int64_t k = std::lower_bound(u.begin(), u.end(), t) - u.begin();
+        push(((uint32_t)k << 17) | ((uint32_t)f << 12), worig[(size_t)w], 0.0, (uint8_t)((hi >> 30) & 1));
+        pend.push_back({pos});
+        const size_t pi = pend.size() - 1;
+        emit(w + 1);
+        set_off(pend[pi].owner, (int64_t)L.nodes.size() - pend[pi].owner);
+        pend.pop_back();
+        emit(w + (int64_t)((hi & 0xFFFFFFu) >> 3));
+    };
+    for (int32_t tr = 0; tr < d->n_trees; ++tr) {
+        const int64_t tb = (int64_t)L.nodes.size();
+        margin = 2 * wdepth[(size_t)tr] + 16;
+        if (margin > kRankMaxOffset / 2) {
+            set_error("rank layout: tree %d is too deep (%d)", tr, wdepth[(size_t)tr]);
+            return FDX_E_UNSUPPORTED;
+        }
+        emit(d->node_offsets[tr]);
+        if (!ok) {
+            set_error("rank layout: tree %d: right offset out of range", tr);
+            return FDX_E_UNSUPPORTED;
+        }
+        const int64_t te = (int64_t)L.nodes.size();
+        if (te - tb > max_tree_nodes) {
+            set_error("rank layout: tree %d has %lld nodes > LDS budget %lld", tr, (long long)(te - tb),
+                      (long long)max_tree_nodes);
+            return FDX_E_UNSUPPORTED;
+        }
+        // steps to reach a leaf (jumps count): children always follow their parent
+        std::vector<int32_t> st((size_t)(te - tb), 0);
+        int32_t dm = 0;
+        for (int64_t p = tb; p < te; ++p) {
+            const uint32_t nd = L.nodes[(size_t)p];
+            const int64_t off = nd & 0xFFF, s = st[(size_t)(p - tb)];
+            if (off == 0) {
+                dm = std::max<int32_t>(dm, (int32_t)s);
+                continue;
+            }
+            if (((nd >> 12) & 15) != 15) st[(size_t)(p + 1 - tb)] = (int32_t)s + 1;
+            st[(size_t)(p + off - tb)] = (int32_t)s + 1;
+        }
+        L.root.push_back((int32_t)tb);
+        L.depth.push_back(dm);
+        L.offsets.push_back(te);
+    }
+    if (L.nodes.size() >= (size_t(1) << 31)) {
+        set_error("rank layout: too many nodes");
+        return FDX_E_UNSUPPORTED;
+    }
+    return FDX_OK;
+}
 }  // namespace
 }  // namespace fdx
 
@@ -612,14 +994,19 @@ namespace fdx {
 namespace {
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
+constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
+
+bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
+
 // Cut the trees into chunks whose nodes fit the variant's LDS budget; whole groups of G trees
-// where more than G fit (a partial group idles walk slots); oversized trees run from global.
+// where more than G fit (a partial group idles walk slots); oversized trees run from global
+// (wide layout only: a rank-layout forest has every tree within the budget by construction).
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
     F->tile_ok = v.tile != 0;
-    const int64_t cap_nodes = lds_node_bytes(F->zstride, v.block, v.rows) / 8;
+    const int64_t cap_nodes = v.rank ? kRankNodeCap : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
-    const auto &off = F->node_offsets;
+    const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
     F->chunks.clear();
     for (int32_t t = 0; t < F->n_trees;) {
         fdx_forest_s::Chunk c;
@@ -663,6 +1050,10 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(variant >= 0 && variant < kNumVariants, "variant must be in [0, %d)", kNumVariants);
     FDX_REQUIRE(variant == 0 || F->zstride == 16, "variants > 0 need <= 16 features");
+    if (kVariants[variant].rank && !F->rank_ok) {
+        set_error("variant %d needs the rank layout, which this forest does not fit", variant);
+        return FDX_E_UNSUPPORTED;
+    }
     const int prev = F->variant;
     F->variant = variant;
     build_chunks(F);
@@ -675,6 +1066,12 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     return upload_chunks(F);
 }
 
+extern "C" int fdx_forest_get_variant(fdx_forest F, int32_t *variant) {
+    FDX_REQUIRE(F && variant, "null pointer");
+    *variant = F->variant;
+    return FDX_OK;
+}
+
 extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, int32_t *orig_out,
                                int32_t *root_out) {
     std::vector<uint64_t> packed;
@@ -685,6 +1082,47 @@ extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, in
     memcpy(nodes_out, packed.data(), packed.size() * 8);
     memcpy(orig_out, orig.data(), orig.size() * 4);
     memcpy(root_out, root.data(), root.size() * 4);
+    return FDX_OK;
+}
+
+static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL) {
+    std::vector<uint64_t> packed;
+    std::vector<int32_t> orig, root, depth;
+    int rc = pack_forest(d, packed, orig, root, depth);
+    if (rc) return rc;
+    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL);
+}
+
+extern "C" int fdx_forest_rank_layout_size(const fdx_forest_desc *d, int64_t *n_nodes, int32_t *n_thresholds) {
+    FDX_REQUIRE(n_nodes && n_thresholds, "null output");
+    RankLayout RL;
+    int rc = rank_layout_host(d, RL);
+    if (rc) return rc;
+    *n_nodes = (int64_t)RL.nodes.size();
+    *n_thresholds = (int32_t)RL.thr.size();
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_pack_rank(const fdx_forest_desc *d, uint32_t *nodes_out, int32_t *orig_out,
+                                    double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out,
+                                    int32_t *depth_out, float *thr_out, int32_t *thr_off_out) {
+    FDX_REQUIRE(nodes_out && orig_out && leaf_value_out && missing_left_out && root_out && depth_out && thr_off_out,
+                "null output");
+    RankLayout RL;
+    int rc = rank_layout_host(d, RL);
+    if (rc) return rc;
+    const size_t n = RL.nodes.size();
+    memcpy(nodes_out, RL.nodes.data(), 4 * n);
+    memcpy(orig_out, RL.orig.data(), 4 * n);
+    memcpy(leaf_value_out, RL.lval.data(), 8 * n);
+    memcpy(missing_left_out, RL.ml.data(), n);
+    memcpy(root_out, RL.root.data(), 4 * RL.root.size());
+    memcpy(depth_out, RL.depth.data(), 4 * RL.depth.size());
+    if (!RL.thr.empty()) {
+        FDX_REQUIRE(thr_out, "null output");
+        memcpy(thr_out, RL.thr.data(), 4 * RL.thr.size());
+    }
+    memcpy(thr_off_out, RL.thr_off, sizeof(RL.thr_off));
     return FDX_OK;
 }
 
@@ -703,7 +1141,19 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->zstride = d->n_features <= 16 ? 16 : 32;
     F->n_nodes = total;
     F->node_offsets.assign(d->node_offsets, d->node_offsets + d->n_trees + 1);
-    F->variant = F->zstride == 16 ? 1 : 0;  // r01 sweep: 1024 x 1 x 4 fastest on the config-3 forest
+    RankLayout RL;
+    F->rank_ok = build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL) == FDX_OK;
+    set_error("");
+    // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
+    F->variant = F->rank_ok ? kFirstRankVariant : (F->zstride == 16 ? 1 : 0);
+    if (F->rank_ok) {
+        F->rank_offsets = RL.offsets;
+        F->rank_nodes = (int64_t)RL.nodes.size();
+        for (int f = 0; f < 16; ++f) {
+            F->rthr_off[f] = RL.thr_off[f];
+            F->rthr_cnt[f] = RL.thr_off[f + 1] - RL.thr_off[f];
+        }
+    }
     build_chunks(F);
     hipStream_t st = as_stream(stream);
     auto fail = [&](hipError_t e, const char *what) {
@@ -727,6 +1177,23 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
+    if (F->rank_ok) {
+        const size_t rn = RL.nodes.size(), nt = (size_t)d->n_trees, nthr = std::max<size_t>(RL.thr.size(), 1);
+        if ((e = hipMalloc(&F->rnodes_d, 4 * rn)) || (e = hipMalloc(&F->rorig_d, 4 * rn)) ||
+            (e = hipMalloc(&F->rlval_d, 8 * rn)) || (e = hipMalloc(&F->rml_d, rn)) ||
+            (e = hipMalloc(&F->rroot_d, 4 * nt)) || (e = hipMalloc(&F->rdepth_d, 4 * nt)) ||
+            (e = hipMalloc(&F->rthr_d, 4 * nthr)))
+            return fail(e, "hipMalloc");
+        if ((e = hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rlval_d, RL.lval.data(), 8 * rn, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rml_d, RL.ml.data(), rn, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rroot_d, RL.root.data(), 4 * nt, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rdepth_d, RL.depth.data(), 4 * nt, hipMemcpyHostToDevice, st)) ||
+            (!RL.thr.empty() &&
+             (e = hipMemcpyAsync(F->rthr_d, RL.thr.data(), 4 * RL.thr.size(), hipMemcpyHostToDevice, st))))
+            return fail(e, "hipMemcpyAsync");
+    }
     if (d->scaler_mean) {
         if ((e = hipMalloc(&F->mean_d, sizeof(double) * d->n_features))) return fail(e, "hipMalloc");
         if ((e = hipMemcpyAsync(F->mean_d, d->scaler_mean, sizeof(double) * d->n_features,
@@ -757,6 +1224,13 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->depth_d);
     (void)hipFree(F->chunk_t_d);
     (void)hipFree(F->chunk_base_d);
+    (void)hipFree(F->rnodes_d);
+    (void)hipFree(F->rorig_d);
+    (void)hipFree(F->rlval_d);
+    (void)hipFree(F->rml_d);
+    (void)hipFree(F->rroot_d);
+    (void)hipFree(F->rdepth_d);
+    (void)hipFree(F->rthr_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
     delete F;
@@ -778,6 +1252,29 @@ extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows) {
     return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows) +
            256;  // + NaN flag word
 }
+
+static RankTab rank_tab(const fdx_forest_s *F) {
+    RankTab rt;
+    rt.u = F->rthr_d;
+    for (int f = 0; f < 16; ++f) {
+        rt.off[f] = F->rthr_off[f];
+        rt.cnt[f] = F->rthr_cnt[f];
+    }
+    return rt;
+}
+
+// Launch a prepare kernel in the row format of the forest's current variant: rank rows
+// (rank layout), float32 rows of 16 or 32 slots (wide layout).
+#define FDX_PREP(KERNEL, GRID, ST, ...)                                                                    \
+    do {                                                                                                  \
+        const RankTab rt_ = rank_tab(F);                                                                  \
+        if (rank_mode(F))                                                                                 \
+            hipLaunchKernelGGL((KERNEL<16, true>), GRID, dim3(256), 0, ST, __VA_ARGS__, rt_);             \
+        else if (F->zstride == 16)                                                                        \
+            hipLaunchKernelGGL((KERNEL<16, false>), GRID, dim3(256), 0, ST, __VA_ARGS__, rt_);            \
+        else                                                                                              \
+            hipLaunchKernelGGL((KERNEL<32, false>), GRID, dim3(256), 0, ST, __VA_ARGS__, rt_);            \
+    } while (0)
 
 static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, double **acc,
                      int32_t **nan_flag = nullptr) {
@@ -808,12 +1305,8 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
-    if (F->zstride == 16)
-        hipLaunchKernelGGL(k_prepare<16>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
-                           F->n_features, F->mean_d, F->scale_d, z, flag);
-    else
-        hipLaunchKernelGGL(k_prepare<32>, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride,
-                           F->n_features, F->mean_d, F->scale_d, z, flag);
+    FDX_PREP(k_prepare, dim3(grid), st, X_d, n, row_stride, col_stride, F->n_features, F->mean_d, F->scale_d,
+             (void *)z, flag);
     FDX_LAUNCHED("k_prepare");
     return FDX_OK;
 }
@@ -832,6 +1325,38 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
     hipStream_t st = as_stream(stream);
     // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
     // features and running sums stay in the 256 MiB Infinity Cache.
+    if (rank_mode(F)) {
+        const int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
+        const size_t nc = F->chunks.size();
+        const uint16_t *zr = reinterpret_cast<const uint16_t *>(z);
+        for (int64_t s0 = 0; s0 < n; s0 += slab) {
+            const int64_t s1 = std::min<int64_t>(n, s0 + slab);
+            for (size_t c = 0; c < nc; ++c) {
+                const auto &ch = F->chunks[c];
+                const int first = c == 0, last = c + 1 == nc;
+#define FDX_LAUNCH_RANK(B, R, G)                                                                              \
+    do {                                                                                                      \
+        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), 256 * 4);      \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
+                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
+                           F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last);     \
+    } while (0)
+                switch (F->variant) {
+                    case 17: FDX_LAUNCH_RANK(1024, 1, 2); break;
+                    case 18: FDX_LAUNCH_RANK(512, 2, 2); break;
+                    case 19: FDX_LAUNCH_RANK(512, 2, 4); break;
+                    case 20: FDX_LAUNCH_RANK(1024, 1, 3); break;
+                    case 21: FDX_LAUNCH_RANK(768, 1, 4); break;
+                    case 22: FDX_LAUNCH_RANK(256, 4, 2); break;
+                    case 23: FDX_LAUNCH_RANK(1024, 1, 6); break;
+                    default: FDX_LAUNCH_RANK(1024, 1, 4); break;
+                }
+#undef FDX_LAUNCH_RANK
+                FDX_LAUNCHED("k_forest_rank");
+            }
+        }
+        return FDX_OK;
+    }
     if (F->zstride == 16 && kVariants[F->variant].tile) {
 #define FDX_LAUNCH_TILE(B, R, G)                                                                            \
     hipLaunchKernelGGL((k_forest_tile<16, B, R, G>), dim3((unsigned)std::min<int64_t>(ceil_div(n, (B) * (R)), 256)), \
@@ -942,18 +1467,12 @@ extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_wi
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
-#define FDX_ZFILL(FS)                                                                                       \
-    do {                                                                                                    \
-        hipLaunchKernelGGL(k_zfill_time<FS>, dim3(grid), dim3(256), 0, st, amount_d, weekend_d, night_d, n,   \
-                           F->mean_d, F->scale_d, z, flag);                                                 \
-        hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, cust_perm_d, cust_nb_d,          \
-                           cust_avg_d, n, n_windows, 3, F->mean_d, F->scale_d, z, flag);                    \
-        if (term_perm_d && term_nb_d && term_risk_d)                                                       \
-            hipLaunchKernelGGL(k_zfill_group<FS>, dim3(grid), dim3(256), 0, st, term_perm_d, term_nb_d,      \
-                               term_risk_d, n, n_windows, 3 + 2 * n_windows, F->mean_d, F->scale_d, z, flag); \
-    } while (0)
-    if (F->zstride == 16) FDX_ZFILL(16); else FDX_ZFILL(32);
-#undef FDX_ZFILL
+    FDX_PREP(k_zfill_time, dim3(grid), st, amount_d, weekend_d, night_d, n, F->mean_d, F->scale_d, (void *)z, flag);
+    FDX_PREP(k_zfill_group, dim3(grid), st, cust_perm_d, cust_nb_d, cust_avg_d, n, n_windows, 3, F->mean_d,
+             F->scale_d, (void *)z, flag);
+    if (term_perm_d && term_nb_d && term_risk_d)
+        FDX_PREP(k_zfill_group, dim3(grid), st, term_perm_d, term_nb_d, term_risk_d, n, n_windows, 3 + 2 * n_windows,
+                 F->mean_d, F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill");
     return FDX_OK;
 }
@@ -972,12 +1491,8 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
     int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     const unsigned grid = stream_grid(n, 256);
-    if (F->zstride == 16)
-        hipLaunchKernelGGL(k_zfill_reply<16>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
-                           n_windows, col0, F->mean_d, F->scale_d, z, flag);
-    else
-        hipLaunchKernelGGL(k_zfill_reply<32>, dim3(grid), dim3(256), 0, as_stream(stream), reply_d, perm_d, n,
-                           n_windows, col0, F->mean_d, F->scale_d, z, flag);
+    FDX_PREP(k_zfill_reply, dim3(grid), as_stream(stream), reply_d, perm_d, n, n_windows, col0, F->mean_d,
+             F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill_reply");
     return FDX_OK;
 }
@@ -1010,14 +1525,8 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
-    if (F->zstride == 16)
-        hipLaunchKernelGGL(k_zfill_grouped<16>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
-                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum,
-                           F->mean_d, F->scale_d, z, flag);
-    else
-        hipLaunchKernelGGL(k_zfill_grouped<32>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
-                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum,
-                           F->mean_d, F->scale_d, z, flag);
+    FDX_PREP(k_zfill_grouped, dim3(grid), st, cust_ts_d, cust_amount_d, cust_nb_d, cust_avg_d, cust_perm_d,
+             term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum, F->mean_d, F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill_grouped");
     return FDX_OK;
 }

@@ -69,6 +69,8 @@ SIGNATURES = {
     "fdx_standard_scale": (ctypes.c_int, [P, c_i64, c_i32, c_i64, c_i64, P, P, P, c_i64, c_i64, P]),
     "fdx_forest_create": (ctypes.c_int, [ctypes.POINTER(ForestDesc), ctypes.POINTER(P), P]),
     "fdx_forest_pack": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P]),
+    "fdx_forest_rank_layout_size": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P]),
+    "fdx_forest_pack_rank": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P, P, P, P, P, P]),
     "fdx_forest_destroy": (ctypes.c_int, [P]),
     "fdx_forest_info": (ctypes.c_int, [P, P, P, P, P]),
     "fdx_forest_workspace_size": (c_sz, [P, c_i64]),
@@ -80,6 +82,7 @@ SIGNATURES = {
     "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
     "fdx_forest_set_slab_rows": (ctypes.c_int, [P, c_i64]),
     "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
+    "fdx_forest_get_variant": (ctypes.c_int, [P, P]),
     "fdx_forest_prepare_reply": (ctypes.c_int, [P, P, P, c_i64, c_i32, c_i32, P, c_sz, P]),
 }
 

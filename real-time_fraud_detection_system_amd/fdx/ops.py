@@ -292,6 +292,9 @@ class Forest:
         nt, nf, nn, nc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
         check(L.fdx_forest_info(h, ctypes.byref(nt), ctypes.byref(nf), ctypes.byref(nn), ctypes.byref(nc)))
         self.n_nodes, self.n_chunks = nn.value, nc.value
+        v = ctypes.c_int32()
+        check(L.fdx_forest_get_variant(h, ctypes.byref(v)), "fdx_forest_get_variant")
+        self.variant = v.value  # the library default (rank layout when the forest fits it)
 
     def __del__(self):
         h = getattr(self, "_h", None)

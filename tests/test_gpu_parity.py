@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import oracle
+from forest_gen import random_forest
 from fdx import ops
 from fdx.pipeline import FraudPipeline
 
@@ -180,31 +181,6 @@ def test_forest_matches_sklearn_golden(dev, golden, name):
     np.testing.assert_array_equal(f.predict(Xc).cpu().numpy(), z["proba"])
 
 
-def random_forest(rng, n_trees, depth, n_feat=15, p_leaf=0.15):
-    """Random sklearn-layout trees (pre-order, -1 leaves) for chunking / global-path tests."""
-    L, R, F, TH, ML, V, off = [], [], [], [], [], [], [0]
-    for _ in range(n_trees):
-        left, right, feat, thr, ml, val = [], [], [], [], [], []
-
-        def build(d):
-            i = len(left)
-            left.append(-1); right.append(-1); feat.append(-2); thr.append(-2.0); ml.append(0)
-            val.append(float(rng.integers(0, 1000)) / 999.0)
-            if d < depth and (d < 2 or rng.random() > p_leaf):
-                feat[i] = int(rng.integers(0, n_feat)); thr[i] = float(rng.normal()) * 1.3
-                ml[i] = int(rng.random() < 0.5)
-                left[i] = build(d + 1)
-                right[i] = build(d + 1)
-            return i
-
-        build(0)
-        L += left; R += right; F += feat; TH += thr; ML += ml; V += val
-        off.append(off[-1] + len(left))
-    return dict(left=np.array(L, np.int64), right=np.array(R, np.int64), feature=np.array(F, np.int64),
-                threshold=np.array(TH), missing_left=np.array(ML, np.uint8), value1=np.array(V),
-                node_offsets=np.array(off, np.int64))
-
-
 @pytest.mark.parametrize("n_trees,depth", [(60, 10), (2, 15)])
 def test_forest_chunks_and_global_path(dev, n_trees, depth):
     rng = np.random.default_rng(depth)
@@ -212,12 +188,15 @@ def test_forest_chunks_and_global_path(dev, n_trees, depth):
     X = rng.normal(size=(20_000, 15))
     X[rng.random(X.shape) < 0.01] = np.nan
     mean, scale = rng.normal(size=15) * 0.1, rng.uniform(0.5, 2.0, size=15)
-    f = ops.Forest(arr, 15, mean, scale)
-    assert f.n_chunks >= 2
-    proba, leaves = f.predict(T(X, torch.float64, dev), want_leaves=True)
     op, ol = oracle.forest_predict(X, arr, mean, scale, want_leaves=True)
-    np.testing.assert_array_equal(leaves.cpu().numpy(), ol)
-    np.testing.assert_array_equal(proba.cpu().numpy(), op)
+    for variant in (None, 1):  # default (rank layout) and the wide layout, whose trees spill
+        f = ops.Forest(arr, 15, mean, scale)
+        if variant is not None:
+            f.set_variant(variant)
+            assert f.n_chunks >= 2
+        proba, leaves = f.predict(T(X, torch.float64, dev), want_leaves=True)
+        np.testing.assert_array_equal(leaves.cpu().numpy(), ol)
+        np.testing.assert_array_equal(proba.cpu().numpy(), op)
 
 
 def test_standard_scale(dev, golden):
@@ -301,7 +280,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(16)))
+@pytest.mark.parametrize("variant", list(range(24)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")

@@ -1,0 +1,147 @@
+"""The rank layout of the forest traversal (host only, no GPU): fdx_forest_pack_rank's
+4-byte nodes walked by a numpy model of k_forest_rank's step must give sklearn's leaves
+and probabilities bit for bit (golden vectors from sklearn, and the C oracle of
+sklearn's Tree._apply_dense for random forests -- incl. trees large enough to need
+jump nodes, and NaN rows routed by missing_go_to_left)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from forest_gen import random_forest
+
+LEAF = 0x0000F000
+
+
+def _desc(a, n_features):
+    from fdx import _lib
+
+    keep = {k: np.ascontiguousarray(a[k], dt) for k, dt in
+            (("node_offsets", np.int64), ("left", np.int64), ("right", np.int64), ("feature", np.int64),
+             ("threshold", np.float64), ("missing_left", np.uint8), ("value1", np.float64))}
+    nt = len(keep["node_offsets"]) - 1
+    d = _lib.ForestDesc(nt, n_features, keep["node_offsets"].ctypes.data, keep["left"].ctypes.data,
+                        keep["right"].ctypes.data, keep["feature"].ctypes.data, keep["threshold"].ctypes.data,
+                        keep["missing_left"].ctypes.data, keep["value1"].ctypes.data, None, None)
+    return d, keep
+
+
+def pack_rank(a, n_features=15):
+    from fdx import _lib
+
+    L = _lib.load()
+    d, keep = _desc(a, n_features)
+    nn, nthr = ctypes.c_int64(), ctypes.c_int32()
+    rc = L.fdx_forest_rank_layout_size(ctypes.byref(d), ctypes.byref(nn), ctypes.byref(nthr))
+    if rc != 0:
+        return None
+    n, nt = nn.value, d.n_trees
+    out = dict(nodes=np.zeros(n, np.uint32), orig=np.zeros(n, np.int32), lval=np.zeros(n), ml=np.zeros(n, np.uint8),
+               root=np.zeros(nt, np.int32), depth=np.zeros(nt, np.int32), thr=np.zeros(max(nthr.value, 1), np.float32),
+               thr_off=np.zeros(17, np.int32))
+    rc = L.fdx_forest_pack_rank(ctypes.byref(d), *[out[k].ctypes.data for k in
+                                                   ("nodes", "orig", "lval", "ml", "root", "depth", "thr", "thr_off")])
+    assert rc == 0, L.fdx_last_error()
+    return out
+
+
+def walk_rank(R, z32):
+    """numpy model of k_forest_rank: ranks r = #{u < x}, x << 17 vs the node word, fixed
+    number of steps (depth), leaves are fixed points, float64 sum in tree order."""
+    n = z32.shape[0]
+    xv = np.zeros((n, 16), np.uint64)
+    for f in range(min(z32.shape[1], 15)):
+        u = R["thr"][R["thr_off"][f]:R["thr_off"][f + 1]]
+        r = np.searchsorted(u, z32[:, f], side="left").astype(np.uint64)
+        xv[:, f] = np.where(np.isnan(z32[:, f]), np.uint64(0xFFFFFFFF), r << np.uint64(17))
+    xv[:, 15] = 0x7FFF << 17
+    nodes = R["nodes"].astype(np.uint64)
+    acc = np.zeros(n)
+    nt = len(R["root"])
+    leaves = np.zeros((n, nt), np.int32)
+    rows = np.arange(n)
+    for t in range(nt):
+        p = np.full(n, R["root"][t], np.int64)
+        for _ in range(int(R["depth"][t])):
+            nd = nodes[p]
+            x = xv[rows, ((nd >> np.uint64(12)) & np.uint64(15)).astype(np.int64)]
+            left = np.where(x == 0xFFFFFFFF, R["ml"][p] != 0, x <= nd)
+            p = p + np.where(left, 1, (nd & np.uint64(0xFFF)).astype(np.int64))
+        assert ((nodes[p] & np.uint64(0xFFF)) == 0).all(), "walk did not end on leaves within depth"
+        acc = acc + R["lval"][p]
+        leaves[:, t] = R["orig"][p]
+    return acc / nt, leaves
+
+
+def _z32(X, mean, scale):
+    return ((X - mean) / scale).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"])
+def test_rank_layout_reproduces_sklearn(golden, name):
+    z = golden(name)
+    R = pack_rank(z)
+    assert R is not None
+    assert (R["nodes"][R["orig"] >= 0] & 0xFFF).min() >= 0
+    proba, leaves = walk_rank(R, _z32(z["X"], z["mean"], z["scale"]))
+    np.testing.assert_array_equal(leaves, z["leaves"])
+    np.testing.assert_array_equal(proba, z["proba"])
+
+
+def test_rank_layout_jump_nodes():
+    """Complete-ish depth-13 trees: root left subtrees of ~8k nodes exceed the 12-bit right
+    offset, so the packer must forward those pointers through jump nodes."""
+    rng = np.random.default_rng(13)
+    a = random_forest(rng, 3, 13, p_leaf=0.02)
+    R = pack_rank(a)
+    assert R is not None
+    jumps = int((R["orig"] == -1).sum())
+    assert jumps > 0
+    assert len(R["nodes"]) == int(a["node_offsets"][-1]) + jumps
+    X = rng.normal(size=(3000, 15))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    proba, leaves = walk_rank(R, X.astype(np.float32))
+    op, ol = oracle.forest_predict(X, a, want_leaves=True)
+    np.testing.assert_array_equal(leaves, ol)
+    np.testing.assert_array_equal(proba, op)
+
+
+def test_rank_layout_bench_model():
+    """The config-3 model (RF 100 trees, depth 20) fits the rank layout and reproduces the
+    sklearn predict_proba saved with it."""
+    import os
+
+    from conftest import ROOT
+
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    R = pack_rank(z)
+    assert R is not None
+    proba, _ = walk_rank(R, _z32(z["check_X"], z["mean"], z["scale"]))
+    np.testing.assert_array_equal(proba, z["check_proba"])
+
+
+def test_rank_threshold_edge_cases():
+    """x32 <= thr64 <=> rank(x32) <= k for thresholds between floats, at floats, +-0, +-inf."""
+    thr = np.array([0.1, -0.1, 1e-40, -1e-40, 3.4e38, 1.0, 0.5 + 2**-30, -2.5 - 2**-40, 0.0, -0.0], np.float64)
+    n = len(thr)
+    a = dict(node_offsets=np.arange(0, 3 * n + 1, 3, dtype=np.int64),
+             left=np.tile(np.array([1, -1, -1], np.int64), n), right=np.tile(np.array([2, -1, -1], np.int64), n),
+             feature=np.zeros(3 * n, np.int64), threshold=np.repeat(thr, 3), missing_left=np.zeros(3 * n, np.uint8),
+             value1=np.tile(np.array([0.0, 1.0, 0.0]), n))
+    R = pack_rank(a)
+    f32 = thr.astype(np.float32)
+    cand = np.concatenate([np.nextafter(f32, np.float32(np.inf)), f32, np.nextafter(f32, np.float32(-np.inf)),
+                           np.array([np.inf, -np.inf, 0.0, -0.0], np.float32)])
+    z32 = np.zeros((len(cand), 15), np.float32)
+    z32[:, 0] = cand
+    _, leaves = walk_rank(R, z32)
+    expect = np.stack([(cand.astype(np.float64) <= t) for t in thr], axis=1)
+    np.testing.assert_array_equal(leaves == 1, expect)
+
+
+def test_rank_layout_ineligible_forest_falls_back():
+    """> 15 features: no rank layout (the wide layout serves it)."""
+    rng = np.random.default_rng(2)
+    a = random_forest(rng, 2, 5, n_feat=20)
+    assert pack_rank(a, n_features=20) is None
