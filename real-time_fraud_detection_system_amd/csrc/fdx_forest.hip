@@ -64,6 +64,9 @@ struct fdx_forest_s {
     uint8_t *rml_d = nullptr;
     float *rthr_d = nullptr;
     int32_t rthr_off[16] = {}, rthr_cnt[16] = {};
+    float *rseg_d = nullptr, *rsmp_d = nullptr;  // two-level rank search tables
+    int32_t ruoff[16] = {}, rsoff[16] = {}, rscnt[16] = {}, rseg = 16, rnsmp = 0;
+    int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
 };
 
 namespace fdx {
@@ -100,7 +103,14 @@ constexpr int kRankXWords = 16 * kRankPlaneRows;  // 64 KiB of row planes
 struct RankTab {
     const float *u;  // concatenated U_f
     int32_t off[16], cnt[16];
+    // two-level search tables (rank_row): U_f padded with +inf to whole segments of `seg`
+    // floats at 16-float-aligned offsets (useg + uoff[f]), and the first float of every
+    // segment (smp + soff[f], scnt[f] segments) -- staged into LDS by the prepare kernels
+    const float *useg, *smp;
+    int32_t uoff[16], soff[16], scnt[16];
+    int32_t seg, n_smp;
 };
+constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
 
 // lower_bound(U_f, v) - U_f, branch-free (Khuong & Morin); NaN -> 0xFFFF
 __device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u, int32_t n) {
@@ -115,15 +125,19 @@ __device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u
     return (uint32_t)(b - u) + (uint32_t)(*b < v);
 }
 
-// ranks of a whole row; the searches of all features advance together (independent loads)
-__device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const RankTab &rt, uint32_t (&out)[16]) {
-    const float *b[16];
-    int32_t n[16];
+// ranks of a whole row: per feature, a branch-free lower_bound over the segment samples
+// in LDS (all features advance together), then the count of values < v inside the one
+// segment it lands in, read from global memory as seg/4 independent float4 loads.
+// r = #{u in U_f : u < v}:  c = #{samples < v};  c == 0 -> 0, else seg*(c-1) + #{u < v in
+// segment c-1} (every value of later segments is >= the next sample >= v; padding is +inf).
+__device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const RankTab &rt, const float *s_smp,
+                                         uint32_t (&out)[16]) {
+    int32_t lo[16], n[16];
     int32_t nmax = 0;
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
-        b[f] = rt.u + rt.off[f];
-        n[f] = f < nf ? rt.cnt[f] : 0;
+        lo[f] = rt.soff[f];
+        n[f] = f < nf ? rt.scnt[f] : 0;
         nmax = max(nmax, n[f]);
     }
     while (nmax > 1) {
@@ -132,7 +146,7 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
         for (int f = 0; f < 16; ++f) {
             if (n[f] > 1) {
                 const int32_t h = n[f] >> 1;
-                b[f] = (b[f][h] < v[f]) ? b[f] + h : b[f];
+                lo[f] = (s_smp[lo[f] + h] < v[f]) ? lo[f] + h : lo[f];
                 n[f] -= h;
             }
             nmax = max(nmax, n[f]);
@@ -140,20 +154,38 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
     }
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
-        if (f >= nf) out[f] = 0u;
-        else if (v[f] != v[f]) out[f] = 0xFFFFu;
-        else if (n[f] <= 0) out[f] = 0u;
-        else out[f] = (uint32_t)(b[f] - (rt.u + rt.off[f])) + (uint32_t)(*b[f] < v[f]);
+        uint32_t r = 0u;
+        if (f < nf && n[f] > 0) {
+            const int32_t c = lo[f] - rt.soff[f] + (s_smp[lo[f]] < v[f] ? 1 : 0);
+            if (c > 0) {
+                const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
+                uint32_t k = 0;
+                for (int q = 0; q < rt.seg / 4; ++q) {
+                    const float4 w = sg[q];
+                    k += (uint32_t)(w.x < v[f]) + (uint32_t)(w.y < v[f]) + (uint32_t)(w.z < v[f]) +
+                         (uint32_t)(w.w < v[f]);
+                }
+                r = (uint32_t)(c - 1) * (uint32_t)rt.seg + k;
+            }
+        }
+        out[f] = (f < nf && v[f] != v[f]) ? 0xFFFFu : r;
     }
+}
+
+// every thread of the block: stage the sample table into LDS (prepare kernels, RANK mode)
+__device__ __forceinline__ void stage_samples(float *s_smp, const RankTab &rt) {
+    for (int i = threadIdx.x; i < rt.n_smp; i += blockDim.x) s_smp[i] = rt.smp[i];
+    __syncthreads();
 }
 
 // Row writers of the prepare kernels: float32 rows [n][FS], or rank rows [n][16] u16.
 template <int FS, bool RANK>
-__device__ __forceinline__ void store_row(void *z, int64_t r, const float (&v)[FS], int nf, const RankTab &rt) {
+__device__ __forceinline__ void store_row(void *z, int64_t r, const float (&v)[FS], int nf, const RankTab &rt,
+                                          const float *s_smp) {
     if constexpr (RANK) {
         static_assert(FS == 16, "rank rows have 16 slots");
         uint32_t q[16];
-        rank_row(v, nf, rt, q);
+        rank_row(v, nf, rt, s_smp, q);
         uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + r * 16);
         dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
         dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
@@ -178,6 +210,8 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
                                                  int64_t cs, int32_t nf, const double *__restrict__ mean,
                                                  const double *__restrict__ scale, void *__restrict__ z,
                                                  int32_t *__restrict__ nan_flag, RankTab rt) {
+    __shared__ float s_smp[RANK ? kMaxRankSamples : 1];
+    if (RANK) stage_samples(s_smp, rt);
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
@@ -195,7 +229,7 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
             }
         }
         if (nan) *nan_flag = 1;  // routes the traversal through the NaN-aware step
-        store_row<FS, RANK>(z, r, v, nf, rt);
+        store_row<FS, RANK>(z, r, v, nf, rt, s_smp);
     }
 }
 
@@ -299,6 +333,8 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     int32_t *__restrict__ nan_flag, RankTab rt) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     const int nf = 3 + 4 * W;
+    __shared__ float s_smp[RANK ? kMaxRankSamples : 1];
+    if (RANK) stage_samples(s_smp, rt);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
@@ -345,7 +381,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             }
         }
         if (nan) *nan_flag = 1;
-        store_row<FS, RANK>(z, i, v, nf, rt);
+        store_row<FS, RANK>(z, i, v, nf, rt, s_smp);
     }
 }
 
@@ -613,21 +649,33 @@ __global__ void __launch_bounds__(BLOCK) k_forest_tile(
 // Rank-layout walk step (see "Rank layout"): 5 VALU + 2 LDS reads per chain.  pa = LDS byte
 // address of the chain's node, nd = that node.
 constexpr uint32_t kRankNodeB = kRankXWords * 4;  // byte offset of the node region in LDS
+
+__device__ __forceinline__ uint32_t lds32(const char *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
+}
+// Opaque to the optimiser: keeps `(left ? 1 : off) << 2` as select + v_lshl_add_u32 instead
+// of being distributed into `left ? 4 : (nd << 2) & 0x3FFC` (one extra VALU per step).
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 template <bool NAN_AWARE, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = *reinterpret_cast<const uint32_t *>(lds + ((nd[k] & 0xF000u) | lane_base[k]));
+    for (int k = 0; k < K; ++k) x[k] = lds32(lds, (nd[k] & 0xF000u) | lane_base[k]);
+    bool left[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        bool left = x[k] <= nd[k];
-        if (NAN_AWARE && x[k] == 0xFFFFFFFFu) left = mleft[(pa[k] - kRankNodeB) >> 2] != 0;
-        const uint32_t st = left ? 1u : (nd[k] & 0xFFFu);
-        pa[k] += st << 2;
+        left[k] = x[k] <= nd[k];
+        if (NAN_AWARE && x[k] == 0xFFFFFFFFu) left[k] = mleft[(pa[k] - kRankNodeB) >> 2] != 0;
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) nd[k] = *reinterpret_cast<const uint32_t *>(lds + pa[k]);
+    for (int k = 0; k < K; ++k) pa[k] += opaque(left[k] ? 1u : (nd[k] & 0xFFFu)) << 2;
+#pragma unroll
+    for (int k = 0; k < K; ++k) nd[k] = lds32(lds, pa[k]);
 }
 
 template <bool NAN_AWARE, int K>
@@ -645,9 +693,73 @@ __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane
     for (; d < depth; ++d) rank_step<NAN_AWARE, K>(lds, lane_base, pa, nd, mleft);
 }
 
-// One launch = trees [t0, t1) of one LDS chunk over rows [r0, r1), rank layout.  Each lane
-// walks G trees for each of its R rows (K = R*G chains); the float64 running sum crosses
-// launches through acc in tree order, exactly like k_forest_chunk.
+// Walk trees [t, t+GG) for the R rows of this lane (chain k = r*GG + g); pa = final leaves.
+template <int R, int GG>
+__device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
+                                           const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
+                                           int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
+                                           uint32_t (&pa)[R * GG]) {
+    constexpr int K = R * GG;
+    uint32_t lane_base[K], nd[K];
+    int dmax = 0;
+#pragma unroll
+    for (int g = 0; g < GG; ++g) {
+        const uint32_t p0 = kRankNodeB + (uint32_t)(root[t + g] - node_base) * 4u;
+        const uint32_t n0 = lds32(lds, p0);
+        dmax = max(dmax, depth[t + g]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            pa[r * GG + g] = p0;
+            nd[r * GG + g] = n0;
+            lane_base[r * GG + g] = lrow[r];
+        }
+    }
+    if (any_nan)
+        rank_walk<true, K>(lds, lane_base, pa, nd, dmax, ml);
+    else
+        rank_walk<false, K>(lds, lane_base, pa, nd, dmax, ml);
+}
+
+template <int K>
+__device__ __forceinline__ void rank_leaf_values(const uint32_t (&pa)[K], int64_t node_base,
+                                                 const double *__restrict__ lval, double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = lval[node_base + ((pa[k] - kRankNodeB) >> 2)];
+}
+
+// a[r] += v[r*GG + g] in tree order
+template <int R, int GG>
+__device__ __forceinline__ void rank_accumulate(double (&a)[R], const double (&v)[R * GG]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int g = 0; g < GG; ++g) a[r] += v[r * GG + g];
+}
+
+template <int R, int GG>
+__device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int64_t node_base, int t,
+                                              const int64_t (&row)[R], const bool (&ok)[R],
+                                              const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out,
+                                              const int32_t *__restrict__ orig, int32_t n_trees) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;
+        const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
+        if (dst < 0) continue;
+#pragma unroll
+        for (int g = 0; g < GG; ++g)
+            leaf_out[dst * n_trees + t + g] = orig[node_base + ((pa[r * GG + g] - kRankNodeB) >> 2)];
+    }
+}
+
+// One launch = trees [t0, t1) of one LDS chunk over rows [r0, r1), rank layout; one block
+// per CU (the LDS holds one block), grid-striding over row tiles of BLOCK*R rows.  Each lane
+// walks G trees for each of its R rows at once (K = R*G chains); a chunk's last t1-t0 mod G
+// trees run as a narrower tail group.  Latency hiding: the next tile's rank rows and running
+// sums are loaded into registers while the current tile walks (a thread's LDS row slots are
+// only ever read by that thread, so no barrier is needed to refill them), and the leaf
+// values of a walk group are loaded while the next group walks (accumulation stays in tree
+// order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
 template <int BLOCK, int R, int G>
 __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
@@ -661,21 +773,38 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kRankXWords * 4) / 4;
     __shared__ __align__(16) uint32_t s_mem[kRankXWords + kNodeWords];
+    uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
     const int tid = threadIdx.x;
-    const uint32_t *nb = nodes + node_base;
-    const uint8_t *ml = mleft + node_base;
-    for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = nb[i];
-    if (tid == 0) s_mem[kRankXWords + kNodeWords - 1] = kRankLeaf;  // parking leaf of idle chains
+    {
+        const uint32_t *nb = nodes + node_base;
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = nb[i];
+    }
 #pragma unroll
-    for (int r = 0; r < R; ++r) s_mem[15 * kRankPlaneRows + r * BLOCK + tid] = 0x7FFFu << 17;  // slot-15 sentinel
+    for (int r = 0; r < R; ++r) s_x[15 * kRankPlaneRows + r * BLOCK + tid] = 0x7FFFu << 17;  // slot-15 sentinel
     __syncthreads();
+    const uint8_t *ml = mleft + node_base;
     const bool any_nan = *nan_flag != 0;  // uniform
-    uint32_t lane_base[K];
+    uint32_t lrow[R];
 #pragma unroll
-    for (int k = 0; k < K; ++k) lane_base[k] = (uint32_t)(((k / G) * BLOCK + tid) * 4);
-    for (int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock; base < r1;
-         base += (int64_t)gridDim.x * kRowsPerBlock) {
+    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * 4);
+    const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
+    int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
+    uint4 q0[R], q1[R];
+    double pacc[R];
+    auto fetch = [&](int64_t b) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t rw = b + r * BLOCK + tid;
+            const bool okr = rw < r1;
+            const uint4 *src = reinterpret_cast<const uint4 *>(zr + (okr ? rw : r0) * 16);
+            q0[r] = src[0];
+            q1[r] = src[1];
+            pacc[r] = (first || !okr) ? 0.0 : acc[rw];
+        }
+    };
+    if (base < r1) fetch(base);
+    for (; base < r1; base += stride) {
         int64_t row[R];
         bool ok[R];
         double a[R];
@@ -683,51 +812,49 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
         for (int r = 0; r < R; ++r) {
             row[r] = base + r * BLOCK + tid;
             ok[r] = row[r] < r1;
-            const uint4 *src = reinterpret_cast<const uint4 *>(zr + (ok[r] ? row[r] : r0) * 16);
-            const uint4 q0 = src[0], q1 = src[1];
-            const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
 #pragma unroll
             for (int f = 0; f < 15; ++f) {
                 const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                s_mem[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 17;
+                s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 17;
             }
-            a[r] = (first || !ok[r]) ? 0.0 : acc[row[r]];
+            a[r] = pacc[r];
         }
-        for (int t = t0; t < t1; t += G) {
-            uint32_t pa[K], nd[K];
-            int dmax = 0;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const bool act = t + g < t1;
-                const uint32_t p0 = act ? kRankNodeB + (uint32_t)(root[t + g] - node_base) * 4u
-                                        : kRankNodeB + (uint32_t)(kNodeWords - 1) * 4u;
-                const uint32_t n0 = *reinterpret_cast<const uint32_t *>(lds + p0);
-                dmax = act ? max(dmax, depth[t + g]) : dmax;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    pa[r * G + g] = p0;
-                    nd[r * G + g] = n0;
-                }
-            }
-            if (any_nan)
-                rank_walk<true, K>(lds, lane_base, pa, nd, dmax, ml);
-            else
-                rank_walk<false, K>(lds, lane_base, pa, nd, dmax, ml);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    if (t + g < t1) {
-                        const int64_t p = node_base + ((pa[r * G + g] - kRankNodeB) >> 2);
-                        a[r] += lval[p];
-                        if (leaf_out && ok[r]) {
-                            const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
-                            if (dst >= 0) leaf_out[dst * n_trees + t + g] = orig[p];
-                        }
-                    }
-                }
-            }
+        if (base + stride < r1) fetch(base + stride);
+        double pv[K];
+        bool pending = false;
+        int t = t0;
+        for (; t + G <= t1; t += G) {
+            uint32_t pa[K];
+            rank_trees<R, G>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
+            if (pending) rank_accumulate<R, G>(a, pv);
+            rank_leaf_values<K>(pa, node_base, lval, pv);
+            pending = true;
+            if (leaf_out) rank_leaf_ids<R, G>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees);
         }
+        const int nt = t1 - t;
+#define FDX_RANK_TAIL(NT)                                                                                  \
+    if constexpr (G > NT) {                                                                                \
+        if (nt == NT) {                                                                                    \
+            uint32_t pt[R * NT];                                                                           \
+            double vt[R * NT];                                                                             \
+            rank_trees<R, NT>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);                      \
+            if (pending) rank_accumulate<R, G>(a, pv);                                                     \
+            pending = false;                                                                               \
+            rank_leaf_values<R * NT>(pt, node_base, lval, vt);                                             \
+            rank_accumulate<R, NT>(a, vt);                                                                 \
+            if (leaf_out) rank_leaf_ids<R, NT>(pt, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees); \
+        }                                                                                                  \
+    }
+        FDX_RANK_TAIL(1)
+        FDX_RANK_TAIL(2)
+        FDX_RANK_TAIL(3)
+        FDX_RANK_TAIL(4)
+        FDX_RANK_TAIL(5)
+        FDX_RANK_TAIL(6)
+        FDX_RANK_TAIL(7)
+#undef FDX_RANK_TAIL
+        if (pending) rank_accumulate<R, G>(a, pv);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!ok[r]) continue;
@@ -1019,7 +1146,7 @@ void build_chunks(fdx_forest_s *F) {
         } else {
             int32_t u = t + 1;
             while (u < F->n_trees && off[u + 1] - c.node_base <= cap_nodes) ++u;
-            if (u - t > G && (u - t) % G) u -= (u - t) % G;
+            if (!v.rank && u - t > G && (u - t) % G) u -= (u - t) % G;  // rank kernel: narrower tail group
             c.t1 = u;
             c.in_lds = true;
         }
@@ -1162,6 +1289,12 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         return FDX_E_HIP;
     };
     hipError_t e;
+    {
+        int dev = 0, ncu = 0;
+        if ((e = hipGetDevice(&dev)) || (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)))
+            return fail(e, "hipDeviceGetAttribute");
+        if (ncu > 0) F->n_cu = ncu;
+    }
     if ((e = hipMalloc(&F->nodes_d, sizeof(uint64_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->root_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
@@ -1177,13 +1310,39 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
+    std::vector<float> useg, smp;
+    if (F->rank_ok) {  // two-level search tables (RankTab): smallest segment with <= kMaxRankSamples samples
+        int seg = 16;
+        for (;; seg *= 2) {
+            int64_t m = 0;
+            for (int f = 0; f < 16; ++f) m += ceil_div(F->rthr_cnt[f], seg);
+            if (m <= kMaxRankSamples) break;
+        }
+        F->rseg = seg;
+        for (int f = 0; f < 16; ++f) {
+            const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, seg);
+            F->ruoff[f] = (int32_t)useg.size();
+            F->rsoff[f] = (int32_t)smp.size();
+            F->rscnt[f] = ns;
+            for (int32_t j = 0; j < ns * seg; ++j)
+                useg.push_back(j < c ? RL.thr[(size_t)(RL.thr_off[f] + j)] : INFINITY);
+            for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
+        }
+        F->rnsmp = (int32_t)smp.size();
+        if (useg.empty()) useg.push_back(INFINITY);
+        if (smp.empty()) smp.push_back(INFINITY);
+    }
     if (F->rank_ok) {
         const size_t rn = RL.nodes.size(), nt = (size_t)d->n_trees, nthr = std::max<size_t>(RL.thr.size(), 1);
         if ((e = hipMalloc(&F->rnodes_d, 4 * rn)) || (e = hipMalloc(&F->rorig_d, 4 * rn)) ||
             (e = hipMalloc(&F->rlval_d, 8 * rn)) || (e = hipMalloc(&F->rml_d, rn)) ||
             (e = hipMalloc(&F->rroot_d, 4 * nt)) || (e = hipMalloc(&F->rdepth_d, 4 * nt)) ||
-            (e = hipMalloc(&F->rthr_d, 4 * nthr)))
+            (e = hipMalloc(&F->rthr_d, 4 * nthr)) || (e = hipMalloc(&F->rseg_d, 4 * useg.size())) ||
+            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())))
             return fail(e, "hipMalloc");
+        if ((e = hipMemcpyAsync(F->rseg_d, useg.data(), 4 * useg.size(), hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st)))
+            return fail(e, "hipMemcpyAsync");
         if ((e = hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(F->rlval_d, RL.lval.data(), 8 * rn, hipMemcpyHostToDevice, st)) ||
@@ -1231,6 +1390,8 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->rroot_d);
     (void)hipFree(F->rdepth_d);
     (void)hipFree(F->rthr_d);
+    (void)hipFree(F->rseg_d);
+    (void)hipFree(F->rsmp_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
     delete F;
@@ -1256,10 +1417,17 @@ extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows) {
 static RankTab rank_tab(const fdx_forest_s *F) {
     RankTab rt;
     rt.u = F->rthr_d;
+    rt.useg = F->rseg_d;
+    rt.smp = F->rsmp_d;
     for (int f = 0; f < 16; ++f) {
         rt.off[f] = F->rthr_off[f];
         rt.cnt[f] = F->rthr_cnt[f];
+        rt.uoff[f] = F->ruoff[f];
+        rt.soff[f] = F->rsoff[f];
+        rt.scnt[f] = F->rscnt[f];
     }
+    rt.seg = F->rseg;
+    rt.n_smp = F->rnsmp;
     return rt;
 }
 
@@ -1336,7 +1504,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_RANK(B, R, G)                                                                              \
     do {                                                                                                      \
-        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), 256 * 4);      \
+        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), F->n_cu);      \
         hipLaunchKernelGGL((k_forest_rank<B, R, G>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
                            (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
                            F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last);     \
