@@ -238,9 +238,9 @@ int fdx_forest_pack(const fdx_forest_desc *desc, uint64_t *nodes_out, int32_t *o
  * node budget; else FDX_E_UNSUPPORTED and the wide 8-byte layout is used).  Per feature f,
  * U_f = thr_out[thr_off_out[f] .. thr_off_out[f+1]) are the sorted distinct thresholds
  * (float32 rounded toward -inf); a row value x becomes r = #{u in U_f : u < x}.
- * nodes_out (4 B): [31:17] threshold rank k, [15:12] feature (15 = leaf / jump),
+ * nodes_out (4 B): [30:16] threshold rank k, [15:12] feature (15 = leaf / jump),
  * [11:0] right-child offset (left child = next node; go left iff r <= k); a leaf is
- * 0x0000F000, a jump node 0xF000 | d forwards to the node d further.  orig_out = sklearn
+ * 0x7FFFF000, a jump node 0x0000F000 | d forwards to the node d further.  orig_out = sklearn
  * node id per node (-1 for jumps), leaf_value_out = value1 of leaves, missing_left_out =
  * missing_go_to_left, root_out/depth_out per tree (depth = max steps incl. jumps),
  * thr_off_out [17].  Sizes from fdx_forest_rank_layout_size. */

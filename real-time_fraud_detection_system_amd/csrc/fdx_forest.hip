@@ -82,21 +82,26 @@ __device__ __forceinline__ double leaf_value(uint64_t nd) { return __longlong_as
 // Per feature f, U_f = sorted unique float32 thresholds (thr32_down) of the forest.  A row
 // value x is replaced by its rank r_f(x) = #{u in U_f : u < x} (lower_bound), and a node
 // with threshold U_f[k] by k:  x <= U_f[k]  <=>  r_f(x) <= k  (exact, U_f sorted unique).
-// 4-byte node:  [31:17] k  [16] 0  [15:12] feature  [11:0] right offset in nodes (left = p+1)
-// Row values in LDS are r << 17 in a [16][1024] u32 plane array at LDS offset 0, so
-//   feature address = (node & 0xF000) | lane_base          (one v_and_or_b32)
-//   go left         = x <= node  (unsigned: r << 17 <= k << 17 | low17  <=>  r <= k)
-//   next address    = addr + 4 * (left ? 1 : node & 0xFFF)   (and, cndmask, lshl_add)
-// Feature slot 15 holds 0x7FFF << 17 for every row, so a node with feature 15 always goes
-// right: a LEAF is 0x0000F000 (right offset 0 = fixed point) and a JUMP node (0xF000 | d)
-// forwards to p + d -- the packer inserts jumps after leaves wherever a right offset would
-// exceed 4095.  Leaf values (float64) and sklearn node ids live in global arrays indexed by
-// rank-layout position; NaN row values are 0xFFFF (u16) / 0xFFFFFFFF (LDS), resolved by
+// 4-byte node:  [31] 0  [30:16] k  [15:12] feature  [11:0] right offset (left child = p+1)
+// Row values in LDS are x = r << 16 in a [16][1024] u32 plane array at LDS offset 0, so
+//   feature address = (node & 0xF000) | lane_base                 (v_and_or_b32)
+//   d = x - node (as int32; both < 2^31):  d <= 0 iff r <= k (go left); when r > k,
+//       d >= 65536 - (node & 0xFFFF) > 4095 >= right offset   (features 0..14)
+//   step = med3(d, 1, node & 0xFFF)   -> 1 (left) or the right offset
+//   next address = addr + 4 * step                             (sub, and, med3, lshl_add)
+// Feature slot 15 holds the sentinel 0x4000 << 16 for every row: a LEAF (0x7FFFF000) has
+// d < 0 and right offset 0, so med3 = 0 (fixed point); a JUMP node (0x0000F000 | j) has
+// d > 4095, so med3 = j: it forwards to p + j (the packer inserts jumps after leaves wherever
+// a right offset would exceed 4095).  No lane-mask instruction, so no VCC hazard stalls.
+// Leaf values (float64) and sklearn node ids live in global arrays indexed by rank-layout
+// position; NaN row values are 0xFFFF (u16) / 0xFFFFFFFF (LDS), resolved by
 // missing_go_to_left from a global byte array in the NaN-aware walk.  Ranks travel through
 // HBM as 16 x u16 = 32 B per row (half the float32 row).
-constexpr uint32_t kRankLeaf = 0x0000F000u;
+constexpr uint32_t kRankLeaf = 0x7FFFF000u;
+constexpr uint32_t kRankJump = 0x0000F000u;
+constexpr uint32_t kRankSentinel = 0x4000u << 16;
 constexpr int kRankMaxOffset = 4095;
-constexpr int kRankMaxRank = 32766;  // k <= 32766 < 0x7FFF (the slot-15 sentinel)
+constexpr int kRankMaxRank = 32766;  // rank values stay <= 0x7FFF so x < 2^31
 constexpr int kRankPlaneRows = 1024;
 constexpr int kRankXWords = 16 * kRankPlaneRows;  // 64 KiB of row planes
 
@@ -396,17 +401,22 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 // tile = 1: k_forest_tile (rows resident, trees streamed) instead of k_forest_chunk.
 // rank = 1: k_forest_rank over the rank layout (4-byte nodes, u16 rank rows).
 struct Variant {
-    int block, rows, group, tile, rank;
+    int block, rows, group, tile, rank, p16 = 0, pipe = 0;
 };
-constexpr int kFirstRankVariant = 16;
+constexpr int kDefaultRankVariant = 34;  // measured fastest on MI355X (r01: G=6 walks per lane, pipelined)
 constexpr Variant kVariants[] = {
     {512, 1, 4, 0, 0},  {1024, 1, 4, 0, 0}, {512, 2, 4, 0, 0},  {512, 2, 2, 0, 0},  {256, 2, 4, 0, 0},
     {1024, 1, 3, 0, 0}, {512, 1, 3, 0, 0},  {768, 1, 3, 0, 0},  {768, 1, 4, 0, 0},  {1024, 1, 2, 0, 0},
     {768, 1, 2, 0, 0},  {768, 2, 2, 0, 0},  {1024, 1, 2, 1, 0}, {512, 2, 1, 1, 0},  {512, 3, 1, 1, 0},
     {768, 2, 1, 1, 0},
-    // rank layout (k_forest_rank)
+    // rank layout (k_forest_rank): variants 16..
     {1024, 1, 4, 0, 1}, {1024, 1, 2, 0, 1}, {512, 2, 2, 0, 1},  {512, 2, 4, 0, 1},  {1024, 1, 3, 0, 1},
-    {768, 1, 4, 0, 1},  {256, 4, 2, 0, 1},  {1024, 1, 6, 0, 1}};
+    {768, 1, 4, 0, 1},  {256, 4, 2, 0, 1},  {1024, 1, 6, 0, 1}, {1024, 1, 8, 0, 1}, {1024, 1, 5, 0, 1},
+    // rank layout, u16 row planes (2048 rows per tile in the same 64 KiB): variants 26..
+    {1024, 2, 3, 0, 1, 1}, {1024, 2, 4, 0, 1, 1}, {1024, 2, 5, 0, 1, 1}, {512, 4, 3, 0, 1, 1}, {1024, 2, 2, 0, 1, 1},
+    // + software-pipelined walk (each chain's next LDS read issued as soon as it can be): 31..
+    {1024, 2, 3, 0, 1, 1, 1}, {1024, 2, 4, 0, 1, 1, 1}, {1024, 2, 5, 0, 1, 1, 1}, {1024, 1, 6, 0, 1, 0, 1},
+    {1024, 1, 4, 0, 1, 1, 1}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -653,48 +663,97 @@ constexpr uint32_t kRankNodeB = kRankXWords * 4;  // byte offset of the node reg
 __device__ __forceinline__ uint32_t lds32(const char *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
-// Opaque to the optimiser: keeps `(left ? 1 : off) << 2` as select + v_lshl_add_u32 instead
-// of being distributed into `left ? 4 : (nd << 2) & 0x3FFC` (one extra VALU per step).
-__device__ __forceinline__ uint32_t opaque(uint32_t v) {
-    asm("" : "+v"(v));
-    return v;
+__device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint16_t *>(lds + byte_addr);
 }
-
-template <bool NAN_AWARE, int K>
+// P16: row planes hold the raw u16 ranks (NaN = 0xFFFF) and the LDS copy of every node is
+// S = node ^ 0xFFFF0000, i.e. its high half is -(k+1) mod 2^16.  Then
+//   d = (r << 16) + S = ((r - k - 1) << 16) + (node & 0xFFFF)     (one v_lshl_add_u32)
+// is < 0 iff r <= k, and >= node & 0xFFFF >= right offset otherwise, so med3(d, 1, off)
+// steps exactly as in the 32-bit form (leaf: k = 0x7FFF vs sentinel 0x4000 -> d < 0, off 0;
+// jump: k = 0 -> d > 0); |d| < 2^31 because r, k <= 0x7FFF.
+template <bool NAN_AWARE, bool P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = lds32(lds, (nd[k] & 0xF000u) | lane_base[k]);
-    bool left[K];
+    for (int k = 0; k < K; ++k)
+        x[k] = P16 ? lds16(lds, (nd[k] & 0xF000u) | lane_base[k]) : lds32(lds, (nd[k] & 0xF000u) | lane_base[k]);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        left[k] = x[k] <= nd[k];
-        if (NAN_AWARE && x[k] == 0xFFFFFFFFu) left[k] = mleft[(pa[k] - kRankNodeB) >> 2] != 0;
+        uint32_t st;
+        if (NAN_AWARE && x[k] == (P16 ? 0xFFFFu : 0xFFFFFFFFu)) {
+            st = mleft[(pa[k] - kRankNodeB) >> 2] != 0 ? 1u : (nd[k] & 0xFFFu);
+        } else {
+            const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
+            asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
+        }
+        pa[k] += st << 2;
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) pa[k] += opaque(left[k] ? 1u : (nd[k] & 0xFFFu)) << 2;
 #pragma unroll
     for (int k = 0; k < K; ++k) nd[k] = lds32(lds, pa[k]);
 }
 
-template <bool NAN_AWARE, int K>
+template <bool NAN_AWARE, bool P16, int K>
 __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft) {
     int d = 0;
     for (; d + kExitEvery <= depth; d += kExitEvery) {
 #pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, K>(lds, lane_base, pa, nd, mleft);
+        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
         uint32_t moving = 0;  // leaves (and only leaves) have right offset 0
 #pragma unroll
         for (int k = 0; k < K; ++k) moving |= nd[k] & 0xFFFu;
         if (!__any(moving != 0)) return;
     }
-    for (; d < depth; ++d) rank_step<NAN_AWARE, K>(lds, lane_base, pa, nd, mleft);
+    for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
 }
 
 // Walk trees [t, t+GG) for the R rows of this lane (chain k = r*GG + g); pa = final leaves.
-template <int R, int GG>
+// Software-pipelined form of rank_walk (no NaN rows): the source order -- per chain, its
+// step arithmetic then at once its node read; then per chain, its feature read -- is pinned
+// with sched_barrier, so every chain has its next LDS read in flight while the others
+// compute (the default schedule clusters all K reads of a phase behind all K updates, and
+// a wave's outstanding reads drain to zero twice per step).
+template <bool P16>
+__device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
+    return P16 ? lds16(lds, addr) : lds32(lds, addr);
+}
+template <bool P16, int K>
+__device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
+                                               uint32_t (&nd)[K], int depth) {
+    uint32_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = rank_x<P16>(lds, (nd[k] & 0xF000u) | lane_base[k]);
+    auto step = [&]() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
+            uint32_t st;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
+            asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %0"
+                : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
+            nd[k] = lds32(lds, pa[k]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            x[k] = rank_x<P16>(lds, (nd[k] & 0xF000u) | lane_base[k]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    int d = 0;
+    for (; d + kExitEvery <= depth; d += kExitEvery) {
+#pragma unroll
+        for (int e = 0; e < kExitEvery; ++e) step();
+        uint32_t moving = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) moving |= nd[k] & 0xFFFu;
+        if (!__any(moving != 0)) return;
+    }
+    for (; d < depth; ++d) step();
+}
+
+template <int R, int GG, bool P16, bool PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
                                            int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
@@ -715,9 +774,11 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
         }
     }
     if (any_nan)
-        rank_walk<true, K>(lds, lane_base, pa, nd, dmax, ml);
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
+    else if (PIPE)
+        rank_walk_pipe<P16, K>(lds, lane_base, pa, nd, dmax);
     else
-        rank_walk<false, K>(lds, lane_base, pa, nd, dmax, ml);
+        rank_walk<false, P16, K>(lds, lane_base, pa, nd, dmax, ml);
 }
 
 template <int K>
@@ -760,7 +821,7 @@ __device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int6
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-template <int BLOCK, int R, int G>
+template <int BLOCK, int R, int G, bool P16, bool PIPE>
 __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
@@ -768,7 +829,8 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const uint8_t *__restrict__ mleft, double *__restrict__ acc, double *__restrict__ proba,
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
     int32_t n_trees, int first, int last) {
-    static_assert(BLOCK * R <= kRankPlaneRows, "row planes hold 1024 rows");
+    constexpr int kPlaneRows = P16 ? 2 * kRankPlaneRows : kRankPlaneRows;  // both: 4 KiB per plane
+    static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kRankXWords * 4) / 4;
@@ -778,16 +840,22 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const int tid = threadIdx.x;
     {
         const uint32_t *nb = nodes + node_base;
-        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = nb[i];
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
     }
+    uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
-    for (int r = 0; r < R; ++r) s_x[15 * kRankPlaneRows + r * BLOCK + tid] = 0x7FFFu << 17;  // slot-15 sentinel
+    for (int r = 0; r < R; ++r) {  // slot 15: the leaf / jump sentinel
+        if (P16)
+            s_x16[15 * kPlaneRows + r * BLOCK + tid] = (uint16_t)(kRankSentinel >> 16);
+        else
+            s_x[15 * kRankPlaneRows + r * BLOCK + tid] = kRankSentinel;
+    }
     __syncthreads();
     const uint8_t *ml = mleft + node_base;
     const bool any_nan = *nan_flag != 0;  // uniform
     uint32_t lrow[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * 4);
+    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * (P16 ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R];
@@ -816,7 +884,10 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
 #pragma unroll
             for (int f = 0; f < 15; ++f) {
                 const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 17;
+                if (P16)
+                    s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
+                else
+                    s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
             }
             a[r] = pacc[r];
         }
@@ -826,7 +897,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
         int t = t0;
         for (; t + G <= t1; t += G) {
             uint32_t pa[K];
-            rank_trees<R, G>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
+            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
             if (pending) rank_accumulate<R, G>(a, pv);
             rank_leaf_values<K>(pa, node_base, lval, pv);
             pending = true;
@@ -838,7 +909,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
         if (nt == NT) {                                                                                    \
             uint32_t pt[R * NT];                                                                           \
             double vt[R * NT];                                                                             \
-            rank_trees<R, NT>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);                      \
+            rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);           \
             if (pending) rank_accumulate<R, G>(a, pv);                                                     \
             pending = false;                                                                               \
             rank_leaf_values<R * NT>(pt, node_base, lval, vt);                                             \
@@ -1053,7 +1124,7 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
             for (auto &p : pend)
                 if ((int64_t)L.nodes.size() - p.owner + margin > kRankMaxOffset) {
                     const int64_t j = (int64_t)L.nodes.size();
-                    push(kRankLeaf, -1, 0.0, 0);
+                    push(kRankJump, -1, 0.0, 0);
                     set_off(p.owner, j - p.owner);
                     p.owner = j;
                 }
@@ -1065,7 +1136,7 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         memcpy(&t, &lo, 4);
         const auto &u = U[f];
         const int64_t k = std::lower_bound(u.begin(), u.end(), t) - u.begin();
-        push(((uint32_t)k << 17) | ((uint32_t)f << 12), worig[(size_t)w], 0.0, (uint8_t)((hi >> 30) & 1));
+        push(((uint32_t)k << 16) | ((uint32_t)f << 12), worig[(size_t)w], 0.0, (uint8_t)((hi >> 30) & 1));
         pend.push_back({pos});
         const size_t pi = pend.size() - 1;
         emit(w + 1);
@@ -1272,7 +1343,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->rank_ok = build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL) == FDX_OK;
     set_error("");
     // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
-    F->variant = F->rank_ok ? kFirstRankVariant : (F->zstride == 16 ? 1 : 0);
+    F->variant = F->rank_ok ? kDefaultRankVariant : (F->zstride == 16 ? 1 : 0);
     if (F->rank_ok) {
         F->rank_offsets = RL.offsets;
         F->rank_nodes = (int64_t)RL.nodes.size();
@@ -1502,22 +1573,34 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             for (size_t c = 0; c < nc; ++c) {
                 const auto &ch = F->chunks[c];
                 const int first = c == 0, last = c + 1 == nc;
-#define FDX_LAUNCH_RANK(B, R, G)                                                                              \
+#define FDX_LAUNCH_RANK(B, R, G, P, ...)                                                                      \
     do {                                                                                                      \
         const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), F->n_cu);      \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0 != 0>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
                            (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
                            F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last);     \
     } while (0)
                 switch (F->variant) {
-                    case 17: FDX_LAUNCH_RANK(1024, 1, 2); break;
-                    case 18: FDX_LAUNCH_RANK(512, 2, 2); break;
-                    case 19: FDX_LAUNCH_RANK(512, 2, 4); break;
-                    case 20: FDX_LAUNCH_RANK(1024, 1, 3); break;
-                    case 21: FDX_LAUNCH_RANK(768, 1, 4); break;
-                    case 22: FDX_LAUNCH_RANK(256, 4, 2); break;
-                    case 23: FDX_LAUNCH_RANK(1024, 1, 6); break;
-                    default: FDX_LAUNCH_RANK(1024, 1, 4); break;
+                    case 17: FDX_LAUNCH_RANK(1024, 1, 2, false); break;
+                    case 18: FDX_LAUNCH_RANK(512, 2, 2, false); break;
+                    case 19: FDX_LAUNCH_RANK(512, 2, 4, false); break;
+                    case 20: FDX_LAUNCH_RANK(1024, 1, 3, false); break;
+                    case 21: FDX_LAUNCH_RANK(768, 1, 4, false); break;
+                    case 22: FDX_LAUNCH_RANK(256, 4, 2, false); break;
+                    case 23: FDX_LAUNCH_RANK(1024, 1, 6, false); break;
+                    case 24: FDX_LAUNCH_RANK(1024, 1, 8, false); break;
+                    case 25: FDX_LAUNCH_RANK(1024, 1, 5, false); break;
+                    case 26: FDX_LAUNCH_RANK(1024, 2, 3, true); break;
+                    case 27: FDX_LAUNCH_RANK(1024, 2, 4, true); break;
+                    case 28: FDX_LAUNCH_RANK(1024, 2, 5, true); break;
+                    case 29: FDX_LAUNCH_RANK(512, 4, 3, true); break;
+                    case 30: FDX_LAUNCH_RANK(1024, 2, 2, true); break;
+                    case 31: FDX_LAUNCH_RANK(1024, 2, 3, true, 1); break;
+                    case 32: FDX_LAUNCH_RANK(1024, 2, 4, true, 1); break;
+                    case 33: FDX_LAUNCH_RANK(1024, 2, 5, true, 1); break;
+                    case 34: FDX_LAUNCH_RANK(1024, 1, 6, false, 1); break;
+                    case 35: FDX_LAUNCH_RANK(1024, 1, 4, true, 1); break;
+                    default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK
                 FDX_LAUNCHED("k_forest_rank");

@@ -221,98 +221,156 @@ __global__ void __launch_bounds__(256) k_interleave(
 // One wave per group; the wave streams its group's rows through an LDS ring (coalesced
 // chunk loads of C rows x S segments), so both the head row and the trailing rows that
 // leave the window are read from LDS.  A trailing row older than the ring (window
-// occupancy > kRing - kChunk rows) is read from global memory instead (correct, slower).
+// occupancy > kRing - kChunk rows) is copied from global memory instead (correct, slower).
 constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
 
-// kRing rows per segment stay in LDS (30-day window occupancy at config 2: max 172 rows).
+// kRing rows per segment stay in LDS.  Launched once per ring size over length classes of
+// groups (a block outside [lg_min, lg_max) exits at once): long segments belong to busy
+// customers whose 30-day windows hold the most rows.
 // The per-row work is straight-line: the tail loop removes rows as it advances (pandas
 // first finds the new start, then removes rows [old start, new start) -- unless the
 // window restarts, in which case the state is re-initialised; removing first and
 // re-initialising afterwards leaves exactly the same state), and the re-initialisation is
 // a predicated select, so a wave runs one instruction stream for its 1/7/30-day lanes.
+// Memory schedule (the walk is a latency chain, so nothing in it may wait on HBM):
+//  * the next chunk is loaded into registers while the current one is walked;
+//  * a chunk's outputs are kept in registers and stored after its walk, alternating two
+//    register sets, so no walk step overwrites a register an in-flight store still reads
+//    (on gfx9 that forces a vmcnt wait);
+//  * a ring miss copies the row into the lane's LDS miss slot, so the common path never
+//    merges a pending global load into a VGPR.
 template <int S_MAX, int kRing>
 __global__ void __launch_bounds__(64) k_customer_ring(
     const int64_t *__restrict__ its, const double *__restrict__ iamt, const int64_t *__restrict__ seg_off,
     const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S,
-    int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ sum_out) {
-    __shared__ int64_t r_ts[kRing * S_MAX];
-    __shared__ double r_amt[kRing * S_MAX];
+    int64_t n_slots, WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ sum_out,
+    int32_t lg_min, int32_t lg_max) {
+    static_assert(kRing % kChunk == 0, "ring holds whole chunks");
+    constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;  // chunk elements per lane
+    // ring rows [0, kRing) + one miss slot per lane
+    constexpr int kRingEl = kRing * S_MAX + kWave;
+    __shared__ int64_t r_ts[kRingEl];
+    __shared__ double r_amt[kRingEl];
     const int lane = threadIdx.x;
     const int64_t g = blockIdx.x;
+    const int64_t s0 = sorder[g * S];
+    const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
+    if (Lg < lg_min || Lg >= lg_max) return;  // another launch's length class
     const int l = lane / n_win, wi = lane - l * n_win;
     const int64_t si = g * S + l;
     const bool active = l < S && si < n_seg;
     const int64_t s = active ? sorder[si] : 0;
     const int32_t L = active ? (int32_t)(seg_off[s + 1] - seg_off[s]) : 0;
-    const int64_t s0 = sorder[g * S];
-    const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
-    const int64_t W = win.w[active ? wi : 0];
+    int64_t W = win.w[0];  // select from the kernel arguments (no indexed load)
+#pragma unroll
+    for (int i = 1; i < FDX_MAX_WINDOWS; ++i) W = (active && wi == i) ? win.w[i] : W;
     const int64_t gbase = goff[g];
     const int64_t *g_ts = its + gbase + l;     // row t of this lane's segment: g_ts[t * S]
     const double *g_amt = iamt + gbase + l;
     int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + l;
     double *sm = sum_out + (int64_t)wi * n_slots + gbase + l;
-    const int64_t *l_ts = r_ts + l;            // ring row r of this lane: l_ts[r * S_MAX]
-    const double *l_amt = r_amt + l;
+    // chunk prefetch registers: element e = lane + j * 64 of a chunk is (row e / S, seg e % S)
+    int64_t pts[kPer];
+    double pam[kPer];
+    auto fetch = [&](int32_t t0) {
+        const int n_el = min(kChunk, Lg - t0) * S;
+        const int64_t src0 = gbase + (int64_t)t0 * S;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = lane + j * kWave;
+            if (e < n_el) {
+                pts[j] = its[src0 + e];
+                pam[j] = iamt[src0 + e];
+            }
+        }
+    };
+    auto commit = [&](int32_t t0) {
+        const int n_el = min(kChunk, Lg - t0) * S;
+        const int ring0 = t0 % kRing;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = lane + j * kWave;
+            if (e < n_el) {
+                const int tt = e / S, ll = e - tt * S;
+                r_ts[(ring0 + tt) * S_MAX + ll] = pts[j];
+                r_amt[(ring0 + tt) * S_MAX + ll] = pam[j];
+            }
+        }
+    };
     // pandas roll_sum state (aggregations.pyx)
     double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
     int32_t nobs = 0, nsame = 0;
     int32_t tail = 0, tail_r = 0, head_r = 0;
-    for (int32_t t0 = 0; t0 < Lg; t0 += kChunk) {
-        const int rows = min(kChunk, Lg - t0);
-        const int ring0 = t0 % kRing;
-        for (int e = lane; e < rows * S; e += kWave) {
-            const int tt = e / S, ll = e - tt * S;
-            const int64_t src = gbase + (int64_t)(t0 + tt) * S + ll;
-            r_ts[(ring0 + tt) * S_MAX + ll] = its[src];
-            r_amt[(ring0 + tt) * S_MAX + ll] = iamt[src];
-        }
+    auto chunk = [&](int32_t t0, int32_t (&onb)[kChunk], double (&oval)[kChunk]) {
+        commit(t0);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (t0 + kChunk < Lg) fetch(t0 + kChunk);  // in flight while this chunk is walked
         const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
-        const int32_t tend = min(t0 + kChunk, L);
-        for (int32_t t = t0; t < tend; ++t) {
-            const int64_t tv = l_ts[head_r * S_MAX];
-            const double v = l_amt[head_r * S_MAX];
-            const int64_t bound = tv - W;
-            // advance the window start, removing each row that leaves (Kahan remove)
-            while (tail < t) {
-                const bool in_ring = tail >= oldest;
-                const int64_t x = in_ring ? l_ts[tail_r * S_MAX] : g_ts[(int64_t)tail * S];
-                if (x > bound) break;
-                const double a = in_ring ? l_amt[tail_r * S_MAX] : g_amt[(int64_t)tail * S];
-                if (a == a) {
-                    nobs -= 1;
-                    const double y = -a - c_rem;
-                    const double tt = sum + y;
-                    c_rem = (tt - sum) - y;
-                    sum = tt;
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const int32_t t = t0 + j;
+            if (t < L) {
+                const int64_t tv = r_ts[head_r * S_MAX + l];
+                const double v = r_amt[head_r * S_MAX + l];
+                const int64_t bound = tv - W;
+                // advance the window start, removing each row that leaves (Kahan remove)
+                while (tail < t) {
+                    int e = tail_r * S_MAX + l;
+                    if (tail < oldest) {  // older than the ring: via this lane's miss slot
+                        e = kRing * S_MAX + lane;
+                        r_ts[e] = g_ts[(int64_t)tail * S];
+                        r_amt[e] = g_amt[(int64_t)tail * S];
+                    }
+                    const int64_t x = r_ts[e];
+                    if (x > bound) break;
+                    const double a = r_amt[e];
+                    if (a == a) {
+                        nobs -= 1;
+                        const double y = -a - c_rem;
+                        const double tt = sum + y;
+                        c_rem = (tt - sum) - y;
+                        sum = tt;
+                    }
+                    ++tail;
+                    tail_r = tail_r + 1 == kRing ? 0 : tail_r + 1;
                 }
-                ++tail;
-                tail_r = tail_r + 1 == kRing ? 0 : tail_r + 1;
+                // start[i] >= end[i-1] (or i == 0): pandas re-initialises the window state
+                if (tail >= t) {
+                    sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
+                }
+                if (v == v) {  // Kahan add
+                    nobs += 1;
+                    const double y = v - c_add;
+                    const double tt = sum + y;
+                    c_add = (tt - sum) - y;
+                    sum = tt;
+                    nsame = (v == prev) ? nsame + 1 : 1;
+                    prev = v;
+                }
+                onb[j] = nobs;
+                oval[j] = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
+                head_r = head_r + 1 == kRing ? 0 : head_r + 1;
             }
-            // start[i] >= end[i-1] (or i == 0): pandas re-initialises the window state
-            if (tail >= t) {
-                sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
-            }
-            if (v == v) {  // Kahan add
-                nobs += 1;
-                const double y = v - c_add;
-                const double tt = sum + y;
-                c_add = (tt - sum) - y;
-                sum = tt;
-                nsame = (v == prev) ? nsame + 1 : 1;
-                prev = v;
-            }
-            const double val = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
-            nb[(int64_t)t * S] = nobs;
-            sm[(int64_t)t * S] = val;  // rolling SUM: the division by nb is left to the consumer
-            head_r = head_r + 1 == kRing ? 0 : head_r + 1;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            if (t0 + j < L) {
+                nb[(int64_t)(t0 + j) * S] = onb[j];
+                sm[(int64_t)(t0 + j) * S] = oval[j];  // rolling SUM: the division by nb is the consumer's
+            }
+        }
+    };
+    int32_t nb_a[kChunk], nb_b[kChunk];
+    double val_a[kChunk], val_b[kChunk];
+    if (Lg > 0) fetch(0);
+    for (int32_t t0 = 0; t0 < Lg; t0 += 2 * kChunk) {
+        chunk(t0, nb_a, val_a);
+        if (t0 + kChunk < Lg) chunk(t0 + kChunk, nb_b, val_b);
     }
 }
 
@@ -659,26 +717,28 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     FDX_REQUIRE(its_d && iamt_d && seg_off_d && sorder_d && goff_d && nb_d && avg_d, "null pointer");
     const int32_t S = kWave / n_windows;
     const int64_t n_groups = ceil_div(n_seg, S);
-    // S_MAX = the LDS ring's segment stride: 21 for the reference's 3 windows
-    static const int ring_env = [] {
-        const char *e = getenv("FDX_CUSTOMER_RING");
-        return e ? atoi(e) : 96;
+    // Length classes (segment rows Lg of a group's longest segment): groups with Lg >= split
+    // get a 192-row ring (2 waves per CU, no ring misses at config 2), the rest a 96-row ring
+    // (4 per CU).  Measured (r01, config 2): occupancy wins -- all groups on the 96-row ring
+    // 1.74 ms, split at 320 rows 2.48 ms, all on 192 rows 2.33 ms -- so the default sends
+    // every group to the 96-row ring (FDX_CUSTOMER_RING_SPLIT overrides).
+    static const int split_env = [] {
+        const char *e = getenv("FDX_CUSTOMER_RING_SPLIT");
+        return e ? atoi(e) : INT32_MAX;
     }();
-    if (S <= 21 && ring_env == 96)
-        hipLaunchKernelGGL((k_customer_ring<21, 96>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
-                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
-    else if (S <= 21 && ring_env == 48)
-        hipLaunchKernelGGL((k_customer_ring<21, 48>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
-                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
-    else if (S <= 21)
-        hipLaunchKernelGGL((k_customer_ring<21, 192>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
-                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
-    else if (S <= 32)
-        hipLaunchKernelGGL((k_customer_ring<32, 192>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
-                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
-    else
-        hipLaunchKernelGGL((k_customer_ring<64, 96>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), its_d,
-                           iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d);
+    hipStream_t st = as_stream(stream);
+#define FDX_RING(SM, RG, LO, HI)                                                                          \
+    hipLaunchKernelGGL((k_customer_ring<SM, RG>), dim3((unsigned)n_groups), dim3(64), 0, st, its_d, iamt_d, seg_off_d, \
+                       sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d, (int32_t)(LO), (int32_t)(HI))
+    if (S <= 21) {
+        if (split_env < INT32_MAX) FDX_RING(21, 192, split_env, INT32_MAX);
+        FDX_RING(21, 96, 0, split_env);
+    } else if (S <= 32) {
+        FDX_RING(32, 192, 0, INT32_MAX);
+    } else {
+        FDX_RING(64, 96, 0, INT32_MAX);
+    }
+#undef FDX_RING
     FDX_LAUNCHED("k_customer_ring");
     return FDX_OK;
 }

@@ -46,17 +46,23 @@ def pack_rank(a, n_features=15):
     return out
 
 
-def walk_rank(R, z32):
-    """numpy model of k_forest_rank: ranks r = #{u < x}, x << 17 vs the node word, fixed
-    number of steps (depth), leaves are fixed points, float64 sum in tree order."""
+def walk_rank(R, z32, p16=False):
+    """numpy model of k_forest_rank: ranks r = #{u < x}, x = r << 16, step =
+    med3(x - node, 1, node & 0xFFF) as int32 (NaN rows: missing_go_to_left), a fixed number
+    of steps (depth), leaves are fixed points, float64 sum in tree order.
+    p16: the u16-plane form -- raw ranks r, LDS node S = node ^ 0xFFFF0000 and
+    d = int32((r << 16) + S) (the kernel's v_lshl_add_u32), same med3 step."""
     n = z32.shape[0]
-    xv = np.zeros((n, 16), np.uint64)
+    xv = np.zeros((n, 16), np.int64)
+    nanm = np.zeros((n, 16), bool)
     for f in range(min(z32.shape[1], 15)):
         u = R["thr"][R["thr_off"][f]:R["thr_off"][f + 1]]
-        r = np.searchsorted(u, z32[:, f], side="left").astype(np.uint64)
-        xv[:, f] = np.where(np.isnan(z32[:, f]), np.uint64(0xFFFFFFFF), r << np.uint64(17))
-    xv[:, 15] = 0x7FFF << 17
-    nodes = R["nodes"].astype(np.uint64)
+        r = np.searchsorted(u, z32[:, f], side="left").astype(np.int64)
+        xv[:, f] = r << 16
+        nanm[:, f] = np.isnan(z32[:, f])
+    xv[:, 15] = 0x4000 << 16
+    nodes = R["nodes"].astype(np.int64)
+    assert (nodes < 2**31).all() and (xv < 2**31).all()
     acc = np.zeros(n)
     nt = len(R["root"])
     leaves = np.zeros((n, nt), np.int32)
@@ -65,10 +71,18 @@ def walk_rank(R, z32):
         p = np.full(n, R["root"][t], np.int64)
         for _ in range(int(R["depth"][t])):
             nd = nodes[p]
-            x = xv[rows, ((nd >> np.uint64(12)) & np.uint64(15)).astype(np.int64)]
-            left = np.where(x == 0xFFFFFFFF, R["ml"][p] != 0, x <= nd)
-            p = p + np.where(left, 1, (nd & np.uint64(0xFFF)).astype(np.int64))
-        assert ((nodes[p] & np.uint64(0xFFF)) == 0).all(), "walk did not end on leaves within depth"
+            f = (nd >> 12) & 15
+            if p16:
+                S = nd ^ 0xFFFF0000
+                d = (((xv[rows, f] >> 16) << 16) + S) & 0xFFFFFFFF
+                d = np.where(d >= 2**31, d - 2**32, d)
+            else:
+                d = xv[rows, f] - nd
+            off = nd & 0xFFF
+            st = np.median(np.stack([d, np.ones_like(d), off]), axis=0).astype(np.int64)
+            st = np.where(nanm[rows, f], np.where(R["ml"][p] != 0, 1, off), st)
+            p = p + st
+        assert ((nodes[p] & 0xFFF) == 0).all(), "walk did not end on leaves within depth"
         acc = acc + R["lval"][p]
         leaves[:, t] = R["orig"][p]
     return acc / nt, leaves
@@ -84,9 +98,10 @@ def test_rank_layout_reproduces_sklearn(golden, name):
     R = pack_rank(z)
     assert R is not None
     assert (R["nodes"][R["orig"] >= 0] & 0xFFF).min() >= 0
-    proba, leaves = walk_rank(R, _z32(z["X"], z["mean"], z["scale"]))
-    np.testing.assert_array_equal(leaves, z["leaves"])
-    np.testing.assert_array_equal(proba, z["proba"])
+    for p16 in (False, True):
+        proba, leaves = walk_rank(R, _z32(z["X"], z["mean"], z["scale"]), p16)
+        np.testing.assert_array_equal(leaves, z["leaves"])
+        np.testing.assert_array_equal(proba, z["proba"])
 
 
 def test_rank_layout_jump_nodes():
@@ -101,10 +116,11 @@ def test_rank_layout_jump_nodes():
     assert len(R["nodes"]) == int(a["node_offsets"][-1]) + jumps
     X = rng.normal(size=(3000, 15))
     X[rng.random(X.shape) < 0.05] = np.nan
-    proba, leaves = walk_rank(R, X.astype(np.float32))
     op, ol = oracle.forest_predict(X, a, want_leaves=True)
-    np.testing.assert_array_equal(leaves, ol)
-    np.testing.assert_array_equal(proba, op)
+    for p16 in (False, True):
+        proba, leaves = walk_rank(R, X.astype(np.float32), p16)
+        np.testing.assert_array_equal(leaves, ol)
+        np.testing.assert_array_equal(proba, op)
 
 
 def test_rank_layout_bench_model():
@@ -117,8 +133,9 @@ def test_rank_layout_bench_model():
     z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
     R = pack_rank(z)
     assert R is not None
-    proba, _ = walk_rank(R, _z32(z["check_X"], z["mean"], z["scale"]))
-    np.testing.assert_array_equal(proba, z["check_proba"])
+    for p16 in (False, True):
+        proba, _ = walk_rank(R, _z32(z["check_X"], z["mean"], z["scale"]), p16)
+        np.testing.assert_array_equal(proba, z["check_proba"])
 
 
 def test_rank_threshold_edge_cases():
