@@ -65,6 +65,7 @@ struct fdx_forest_s {
     float *rthr_d = nullptr;
     int32_t rthr_off[16] = {}, rthr_cnt[16] = {};
     float *rseg_d = nullptr, *rsmp_d = nullptr;  // two-level rank search tables
+    uint16_t *ritab_d = nullptr;                  // [16][kIntTab] ranks of small integer values
     int32_t ruoff[16] = {}, rsoff[16] = {}, rscnt[16] = {}, rseg = 16, rnsmp = 0;
     int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
 };
@@ -114,8 +115,12 @@ struct RankTab {
     const float *useg, *smp;
     int32_t uoff[16], soff[16], scnt[16];
     int32_t seg, n_smp;
+    // itab[f * kIntTab + c] = rank of the scaled integer c (c < kIntTab) in feature f: the
+    // flags and window counts are small integers, so the prepare looks their ranks up
+    const uint16_t *itab;
 };
 constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
+constexpr int kIntTab = 256;           // integer rank table entries per feature (8 KiB in LDS)
 
 // lower_bound(U_f, v) - U_f, branch-free (Khuong & Morin); NaN -> 0xFFFF
 __device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u, int32_t n) {
@@ -135,14 +140,15 @@ __device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u
 // segment it lands in, read from global memory as seg/4 independent float4 loads.
 // r = #{u in U_f : u < v}:  c = #{samples < v};  c == 0 -> 0, else seg*(c-1) + #{u < v in
 // segment c-1} (every value of later segments is >= the next sample >= v; padding is +inf).
+// Only the features in `need` are searched; out[f] of the others is left as the caller set it.
 __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const RankTab &rt, const float *s_smp,
-                                         uint32_t (&out)[16]) {
+                                         uint32_t (&out)[16], uint32_t need = 0xFFFFu) {
     int32_t lo[16], n[16];
     int32_t nmax = 0;
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
         lo[f] = rt.soff[f];
-        n[f] = f < nf ? rt.scnt[f] : 0;
+        n[f] = (f < nf && ((need >> f) & 1u)) ? rt.scnt[f] : 0;
         nmax = max(nmax, n[f]);
     }
     while (nmax > 1) {
@@ -159,6 +165,7 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
     }
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
+        if (!((need >> f) & 1u)) continue;
         uint32_t r = 0u;
         if (f < nf && n[f] > 0) {
             const int32_t c = lo[f] - rt.soff[f] + (s_smp[lo[f]] < v[f] ? 1 : 0);
@@ -339,7 +346,11 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     const int nf = 3 + 4 * W;
     __shared__ float s_smp[RANK ? kMaxRankSamples : 1];
-    if (RANK) stage_samples(s_smp, rt);
+    __shared__ uint16_t s_itab[RANK ? 16 * kIntTab : 1];
+    if (RANK) {
+        for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
+        stage_samples(s_smp, rt);  // (its __syncthreads covers s_itab too)
+    }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         float v[FS];
@@ -366,6 +377,46 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         if (wd < 0) wd += 7;
         const bool we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
         const bool ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+        if constexpr (RANK) {
+            // flags and window counts: integer rank table; amount, averages and risks: search
+            uint32_t q[16];
+            uint32_t need = 1u | (0xFFFFu << nf);
+            auto count = [&](int f, int32_t c) {
+                if (c >= 0 && c < kIntTab) {
+                    q[f] = s_itab[f * kIntTab + c];
+                } else {
+                    v[f] = zval((double)c, mean, scale, f);
+                    need |= 1u << f;
+                }
+            };
+            q[1] = s_itab[1 * kIntTab + (we ? 1 : 0)];
+            q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
+            q[15] = 0u;
+            v[0] = zval(camt[i], mean, scale, 0);
+            bool nan = v[0] != v[0];
+            const int64_t q_ = term_inv ? term_inv[r] : r;
+            const int64_t *rec = term_rec + q_ * W;
+#pragma unroll
+            for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                if (w < W) {
+                    const int32_t c = cnb[(int64_t)w * n + i];
+                    const double cv = cval[(int64_t)w * n + i];
+                    count(3 + 2 * w, c);
+                    v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
+                    const int64_t tw = rec[w];
+                    count(3 + 2 * W + 2 * w, term_nb(tw));
+                    v[4 + 2 * W + 2 * w] = zval(term_risk(tw), mean, scale, 4 + 2 * W + 2 * w);
+                    need |= (1u << (4 + 2 * w)) | (1u << (4 + 2 * W + 2 * w));
+                    nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
+                }
+            }
+            if (nan) *nan_flag = 1;
+            rank_row(v, nf, rt, s_smp, q, need & 0xFFFFu);
+            uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
+            dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
+            dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
+            continue;
+        }
         v[0] = zval(camt[i], mean, scale, 0);
         v[1] = zval((double)we, mean, scale, 1);
         v[2] = zval((double)ni, mean, scale, 2);
@@ -1382,6 +1433,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
     std::vector<float> useg, smp;
+    std::vector<uint16_t> itab;
     if (F->rank_ok) {  // two-level search tables (RankTab): smallest segment with <= kMaxRankSamples samples
         int seg = 16;
         for (;; seg *= 2) {
@@ -1402,6 +1454,19 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         F->rnsmp = (int32_t)smp.size();
         if (useg.empty()) useg.push_back(INFINITY);
         if (smp.empty()) smp.push_back(INFINITY);
+        // integer rank table: the same float64 scaling and float32 cast as zval(), then the
+        // lower_bound the device search computes (bit-identical arithmetic on the host)
+        itab.assign((size_t)16 * kIntTab, 0);
+        for (int f = 0; f < 16 && f < d->n_features; ++f) {
+            const float *u0 = RL.thr.data() + RL.thr_off[f], *u1 = RL.thr.data() + RL.thr_off[f + 1];
+            for (int c = 0; c < kIntTab; ++c) {
+                double x = (double)c;
+                if (d->scaler_mean) x = x - d->scaler_mean[f];
+                if (d->scaler_scale) x = x / d->scaler_scale[f];
+                const float zf = (float)x;
+                itab[(size_t)f * kIntTab + c] = (uint16_t)(std::lower_bound(u0, u1, zf) - u0);
+            }
+        }
     }
     if (F->rank_ok) {
         const size_t rn = RL.nodes.size(), nt = (size_t)d->n_trees, nthr = std::max<size_t>(RL.thr.size(), 1);
@@ -1409,10 +1474,11 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
             (e = hipMalloc(&F->rlval_d, 8 * rn)) || (e = hipMalloc(&F->rml_d, rn)) ||
             (e = hipMalloc(&F->rroot_d, 4 * nt)) || (e = hipMalloc(&F->rdepth_d, 4 * nt)) ||
             (e = hipMalloc(&F->rthr_d, 4 * nthr)) || (e = hipMalloc(&F->rseg_d, 4 * useg.size())) ||
-            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())))
+            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())) || (e = hipMalloc(&F->ritab_d, 2 * itab.size())))
             return fail(e, "hipMalloc");
         if ((e = hipMemcpyAsync(F->rseg_d, useg.data(), 4 * useg.size(), hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st)))
+            (e = hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st)))
             return fail(e, "hipMemcpyAsync");
         if ((e = hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
@@ -1462,6 +1528,7 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->rdepth_d);
     (void)hipFree(F->rthr_d);
     (void)hipFree(F->rseg_d);
+    (void)hipFree(F->ritab_d);
     (void)hipFree(F->rsmp_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
@@ -1499,6 +1566,7 @@ static RankTab rank_tab(const fdx_forest_s *F) {
     }
     rt.seg = F->rseg;
     rt.n_smp = F->rnsmp;
+    rt.itab = F->ritab_d;
     return rt;
 }
 

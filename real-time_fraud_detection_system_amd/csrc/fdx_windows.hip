@@ -731,8 +731,17 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     hipLaunchKernelGGL((k_customer_ring<SM, RG>), dim3((unsigned)n_groups), dim3(64), 0, st, its_d, iamt_d, seg_off_d, \
                        sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d, (int32_t)(LO), (int32_t)(HI))
     if (S <= 21) {
+        static const int small_env = [] {  // FDX_CUSTOMER_RING: rows of the small ring (64 / 96 / 128)
+            const char *e = getenv("FDX_CUSTOMER_RING");
+            return e ? atoi(e) : 96;
+        }();
         if (split_env < INT32_MAX) FDX_RING(21, 192, split_env, INT32_MAX);
-        FDX_RING(21, 96, 0, split_env);
+        if (small_env == 64)
+            FDX_RING(21, 64, 0, split_env);
+        else if (small_env == 128)
+            FDX_RING(21, 128, 0, split_env);
+        else
+            FDX_RING(21, 96, 0, split_env);
     } else if (S <= 32) {
         FDX_RING(32, 192, 0, INT32_MAX);
     } else {
