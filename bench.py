@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--forest-variant", type=int, default=-1,
                     help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
 
 
@@ -101,6 +103,10 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    elif args.sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
     # weak scaling: every rank adds its own customers and terminals to one shared map
     data = synth.generate(args.customers, args.terminals * world, args.days, seed=1234 + rank,
@@ -125,7 +131,7 @@ def main():
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
     ev = []
 
-    if world > 1:
+    if world > 1 or args.sharded:
         from fdx.distributed import ShardedPipeline
 
         sp = ShardedPipeline(pipe, world, rank, args.terminals * world)
@@ -249,7 +255,7 @@ def main():
               file=sys.stderr)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or args.sharded:
         dist.destroy_process_group()
 
 

@@ -135,6 +135,16 @@ int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, 
                                 const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
                                 void *stream);
 
+/* Same records when the segments are NOT in time order (the multi-GPU owner side: a
+ * terminal's rows arrive as one time-sorted run per source rank, so a stable re-key by
+ * terminal gives segments of concatenated runs).  Each segment is time-sorted inside the
+ * kernel (LDS bitonic sort; direct O(L^2) counts past 1024 rows) -- no global time sort.
+ * The features are tie-order independent, so the records equal the sorted-input ones. */
+int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
+                                         const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                         const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
+                                         void *stream);
+
 /* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
  * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /
  * groupby('TERMINAL_ID') (feature_transformation.ipynb:1092-1093, :2435-2436).
@@ -175,7 +185,7 @@ int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, in
  * Rows are sharded by customer; the terminal windows need every row of a terminal on its
  * owner rank, owner(t) = t % world.  Per step: fdx_key_map(MOD) -> fdx_rekey(owner) ->
  * fdx_exchange_pack -> RCCL all-to-all (16 B/row) -> fdx_exchange_unpack (local terminal
- * id = t / world) -> time sort + fdx_rekey -> fdx_terminal_windows_packed with row_d = the
+ * id = t / world) -> fdx_rekey -> fdx_terminal_windows_packed_unsorted with row_d = the
  * grouped -> receive-position perm (count records indexed by receive position) -> RCCL
  * all-to-all back -> fdx_forest_prepare_grouped / fdx_reply_assemble.
  * Record layouts: exchange rec[j] = {ts, term<<32 | fraud<<31 | source row}; reply rows

@@ -66,6 +66,7 @@ struct fdx_forest_s {
     int32_t rthr_off[16] = {}, rthr_cnt[16] = {};
     float *rseg_d = nullptr, *rsmp_d = nullptr;  // two-level rank search tables
     uint16_t *ritab_d = nullptr;                  // [16][kIntTab] ranks of small integer values
+    uint16_t *rrat_d = nullptr;                   // [16][kRatN][kRatN] ranks of small ratios fr / nb
     int32_t ruoff[16] = {}, rsoff[16] = {}, rscnt[16] = {}, rseg = 16, rnsmp = 0;
     int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
 };
@@ -118,9 +119,13 @@ struct RankTab {
     // itab[f * kIntTab + c] = rank of the scaled integer c (c < kIntTab) in feature f: the
     // flags and window counts are small integers, so the prepare looks their ranks up
     const uint16_t *itab;
+    // rat[(f * kRatN + nb) * kRatN + fr] = rank of the scaled ratio fr / nb (0 when nb == 0,
+    // the reference's fillna(0)) for nb < kRatN: the terminal risks are such ratios
+    const uint16_t *rat;
 };
 constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
 constexpr int kIntTab = 256;           // integer rank table entries per feature (8 KiB in LDS)
+constexpr int kRatN = 128;             // ratio rank table: nb, fr < kRatN (32 KiB per feature, global)
 
 // lower_bound(U_f, v) - U_f, branch-free (Khuong & Morin); NaN -> 0xFFFF
 __device__ __forceinline__ uint32_t rank_of(float v, const float *__restrict__ u, int32_t n) {
@@ -181,6 +186,52 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
             }
         }
         out[f] = (f < nf && v[f] != v[f]) ? 0xFFFFu : r;
+    }
+}
+
+// rank_row over a compile-time feature list (the continuous features of the reference's
+// 15-column layout): the search loop runs a fixed, uniform number of rounds over only them.
+template <int NS>
+__device__ __forceinline__ void rank_fixed(const float (&v)[16], const int (&fs)[NS], const RankTab &rt,
+                                           const float *s_smp, uint32_t (&out)[16]) {
+    int32_t lo[NS], n[NS];
+    int32_t nmax = 0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        lo[i] = rt.soff[fs[i]];
+        n[i] = rt.scnt[fs[i]];
+        nmax = max(nmax, n[i]);
+    }
+    while (nmax > 1) {  // uniform: the trip count depends on the table sizes only
+        nmax = 0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (n[i] > 1) {
+                const int32_t h = n[i] >> 1;
+                lo[i] = (s_smp[lo[i] + h] < v[fs[i]]) ? lo[i] + h : lo[i];
+                n[i] -= h;
+            }
+            nmax = max(nmax, n[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int f = fs[i];
+        uint32_t r = 0u;
+        if (n[i] > 0) {
+            const int32_t c = lo[i] - rt.soff[f] + (s_smp[lo[i]] < v[f] ? 1 : 0);
+            if (c > 0) {
+                const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
+                uint32_t k = 0;
+                for (int q = 0; q < rt.seg / 4; ++q) {
+                    const float4 w = sg[q];
+                    k += (uint32_t)(w.x < v[f]) + (uint32_t)(w.y < v[f]) + (uint32_t)(w.z < v[f]) +
+                         (uint32_t)(w.w < v[f]);
+                }
+                r = (uint32_t)(c - 1) * (uint32_t)rt.seg + k;
+            }
+        }
+        out[f] = v[f] != v[f] ? 0xFFFFu : r;
     }
 }
 
@@ -404,14 +455,30 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                     count(3 + 2 * w, c);
                     v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
                     const int64_t tw = rec[w];
-                    count(3 + 2 * W + 2 * w, term_nb(tw));
-                    v[4 + 2 * W + 2 * w] = zval(term_risk(tw), mean, scale, 4 + 2 * W + 2 * w);
-                    need |= (1u << (4 + 2 * w)) | (1u << (4 + 2 * W + 2 * w));
-                    nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
+                    const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
+                    count(3 + 2 * W + 2 * w, tnb);
+                    const int fr_ = 4 + 2 * W + 2 * w;
+                    if (tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb) {
+                        q[fr_] = rt.rat[((int64_t)fr_ * kRatN + tnb) * kRatN + tfr];
+                    } else {
+                        v[fr_] = zval(term_risk(tw), mean, scale, fr_);
+                        need |= 1u << fr_;
+                        nan |= v[fr_] != v[fr_];
+                    }
+                    need |= 1u << (4 + 2 * w);
+                    nan |= v[4 + 2 * w] != v[4 + 2 * w];
                 }
             }
             if (nan) *nan_flag = 1;
-            rank_row(v, nf, rt, s_smp, q, need & 0xFFFFu);
+            if (W == 3) {  // the reference's layout: amount + 3 averages searched in fixed rounds
+                constexpr int kFix[4] = {0, 4, 6, 8};
+                rank_fixed<4>(v, kFix, rt, s_smp, q);
+                need &= ~((1u << 0) | (1u << 4) | (1u << 6) | (1u << 8));
+                need &= (1u << nf) - 1u;
+                if (__any(need != 0)) rank_row(v, nf, rt, s_smp, q, need);  // table overflows (rare)
+            } else {
+                rank_row(v, nf, rt, s_smp, q, need & 0xFFFFu);
+            }
             uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
             dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
             dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
@@ -1433,7 +1500,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
     std::vector<float> useg, smp;
-    std::vector<uint16_t> itab;
+    std::vector<uint16_t> itab, rat;
     if (F->rank_ok) {  // two-level search tables (RankTab): smallest segment with <= kMaxRankSamples samples
         int seg = 16;
         for (;; seg *= 2) {
@@ -1457,6 +1524,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         // integer rank table: the same float64 scaling and float32 cast as zval(), then the
         // lower_bound the device search computes (bit-identical arithmetic on the host)
         itab.assign((size_t)16 * kIntTab, 0);
+        rat.assign((size_t)16 * kRatN * kRatN, 0);
         for (int f = 0; f < 16 && f < d->n_features; ++f) {
             const float *u0 = RL.thr.data() + RL.thr_off[f], *u1 = RL.thr.data() + RL.thr_off[f + 1];
             for (int c = 0; c < kIntTab; ++c) {
@@ -1466,6 +1534,14 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
                 const float zf = (float)x;
                 itab[(size_t)f * kIntTab + c] = (uint16_t)(std::lower_bound(u0, u1, zf) - u0);
             }
+            for (int nb = 0; nb < kRatN; ++nb)  // term_risk(): nb > 0 ? fr / nb : 0.0
+                for (int fr = 0; fr < kRatN; ++fr) {
+                    double x = nb > 0 ? (double)fr / (double)nb : 0.0;
+                    if (d->scaler_mean) x = x - d->scaler_mean[f];
+                    if (d->scaler_scale) x = x / d->scaler_scale[f];
+                    const float zf = (float)x;
+                    rat[((size_t)f * kRatN + nb) * kRatN + fr] = (uint16_t)(std::lower_bound(u0, u1, zf) - u0);
+                }
         }
     }
     if (F->rank_ok) {
@@ -1474,11 +1550,13 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
             (e = hipMalloc(&F->rlval_d, 8 * rn)) || (e = hipMalloc(&F->rml_d, rn)) ||
             (e = hipMalloc(&F->rroot_d, 4 * nt)) || (e = hipMalloc(&F->rdepth_d, 4 * nt)) ||
             (e = hipMalloc(&F->rthr_d, 4 * nthr)) || (e = hipMalloc(&F->rseg_d, 4 * useg.size())) ||
-            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())) || (e = hipMalloc(&F->ritab_d, 2 * itab.size())))
+            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())) || (e = hipMalloc(&F->ritab_d, 2 * itab.size())) ||
+            (e = hipMalloc(&F->rrat_d, 2 * rat.size())))
             return fail(e, "hipMalloc");
         if ((e = hipMemcpyAsync(F->rseg_d, useg.data(), 4 * useg.size(), hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st)))
+            (e = hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(F->rrat_d, rat.data(), 2 * rat.size(), hipMemcpyHostToDevice, st)))
             return fail(e, "hipMemcpyAsync");
         if ((e = hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
@@ -1529,6 +1607,7 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->rthr_d);
     (void)hipFree(F->rseg_d);
     (void)hipFree(F->ritab_d);
+    (void)hipFree(F->rrat_d);
     (void)hipFree(F->rsmp_d);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
@@ -1567,6 +1646,7 @@ static RankTab rank_tab(const fdx_forest_s *F) {
     rt.seg = F->rseg;
     rt.n_smp = F->rnsmp;
     rt.itab = F->ritab_d;
+    rt.rat = F->rrat_d;
     return rt;
 }
 

@@ -374,6 +374,193 @@ __global__ void __launch_bounds__(64) k_customer_ring(
     }
 }
 
+// ---------------------------------------------------- customer windows, two-pass form
+// Pass 1 (k_customer_starts, fully parallel): pandas' variable-window start of every row,
+//   start_w(t) = first row j of the segment with ts_j > ts_t - W_w   (closed='right'),
+// written into the nb output array (same [W][n_slots] int32 shape; pass 2 overwrites each
+// entry with the count after reading it).  One wave per 16 interleaved rows; each lane (one
+// segment x window) binary-searches its first row's start, then advances it row by row.
+// Pass 2 (k_customer_walk): the exact Kahan add/remove recurrence, one lane per (segment,
+// window) -- the only sequential part -- now free of timestamp compares: per row it removes
+// rows [start(t-1), start(t)) (or re-initialises when start(t) == t) and adds row t.  Only
+// the amounts ride in the LDS ring (8 B per row), so more waves fit per CU.
+__global__ void __launch_bounds__(256) k_customer_starts(
+    const int64_t *__restrict__ its, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
+    const uint32_t *__restrict__ goff, int64_t n_groups, int64_t n_seg, int32_t S, int64_t n_slots, WinArgs win,
+    int32_t n_win, int32_t *__restrict__ starts) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t rho0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) * kChunk;
+    const int64_t n_rows = n_slots / S;
+    if (rho0 >= n_rows) return;
+    const int l = lane / n_win, wi = lane - l * n_win;
+    if (l >= S) return;
+    int64_t W = win.w[0];
+#pragma unroll
+    for (int i = 1; i < FDX_MAX_WINDOWS; ++i) W = wi == i ? win.w[i] : W;
+    // group of row rho0: the last g with goff[g] <= rho0 * S
+    int64_t lo = 0, hi = n_groups;
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)goff[mid] <= rho0 * S) lo = mid; else hi = mid;
+    }
+    int64_t g = lo;
+    int64_t gbase = goff[g], grows = ((int64_t)goff[g + 1] - gbase) / S;
+    auto seg_len = [&](int64_t gg) -> int32_t {
+        const int64_t si = gg * S + l;
+        if (si >= n_seg) return 0;
+        const int64_t sg = sorder[si];
+        return (int32_t)(seg_off[sg + 1] - seg_off[sg]);
+    };
+    int32_t L = seg_len(g);
+    int32_t t = (int32_t)(rho0 - gbase / S);
+    int32_t st = -1;  // start of the previous row of this lane (-1: not known yet)
+    for (int j = 0; j < kChunk && rho0 + j < n_rows; ++j) {
+        if (t == grows) {  // next group
+            ++g;
+            gbase = goff[g];
+            grows = ((int64_t)goff[g + 1] - gbase) / S;
+            L = seg_len(g);
+            t = 0;
+            st = -1;
+        }
+        if (t < L) {
+            const int64_t *ts = its + gbase + l;  // row k of this lane's segment: ts[k * S]
+            const int64_t bound = ts[(int64_t)t * S] - W;
+            if (st < 0) {
+                int32_t a = 0, b = t;  // first k in [0, t] with ts[k] > bound (k = t qualifies)
+                while (a < b) {
+                    const int32_t m = (a + b) >> 1;
+                    if (ts[(int64_t)m * S] > bound) b = m; else a = m + 1;
+                }
+                st = a;
+            } else {
+                while (ts[(int64_t)st * S] <= bound) ++st;
+            }
+            starts[(int64_t)wi * n_slots + gbase + (int64_t)t * S + l] = st;
+        }
+        ++t;
+    }
+}
+
+template <int S_MAX, int kRing>
+__global__ void __launch_bounds__(64) k_customer_walk(
+    const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
+    const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
+    int32_t *__restrict__ nb_out, double *__restrict__ sum_out) {
+    static_assert((kRing & (kRing - 1)) == 0 && kRing % kChunk == 0, "power-of-two ring of whole chunks");
+    constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;  // chunk elements per lane
+    constexpr int kRingEl = kRing * S_MAX + kWave;             // + one miss slot per lane
+    __shared__ double r_amt[kRingEl];
+    const int lane = threadIdx.x;
+    const int64_t g = blockIdx.x;
+    const int64_t s0 = sorder[g * S];
+    const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
+    const int l = lane / n_win, wi = lane - l * n_win;
+    const int64_t si = g * S + l;
+    const bool active = l < S && si < n_seg;
+    const int64_t s = active ? sorder[si] : 0;
+    const int32_t L = active ? (int32_t)(seg_off[s + 1] - seg_off[s]) : 0;
+    const int64_t gbase = goff[g];
+    const double *g_amt = iamt + gbase + l;  // row t of this lane's segment: g_amt[t * S]
+    int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + l;
+    double *sm = sum_out + (int64_t)wi * n_slots + gbase + l;
+    double pam[kPer];
+    int32_t pst[kChunk];
+    auto fetch = [&](int32_t t0) {
+        const int n_el = min(kChunk, Lg - t0) * S;
+        const int64_t src0 = gbase + (int64_t)t0 * S;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = lane + j * kWave;
+            if (e < n_el) pam[j] = iamt[src0 + e];
+        }
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j)
+            if (t0 + j < L) pst[j] = nb[(int64_t)(t0 + j) * S];
+    };
+    auto commit = [&](int32_t t0) {
+        const int n_el = min(kChunk, Lg - t0) * S;
+        const int ring0 = t0 & (kRing - 1);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int e = lane + j * kWave;
+            if (e < n_el) {
+                const int tt = e / S, ll = e - tt * S;
+                r_amt[(ring0 + tt) * S_MAX + ll] = pam[j];
+            }
+        }
+    };
+    double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
+    int32_t nobs = 0, nsame = 0, tail = 0;
+    auto chunk = [&](int32_t t0, int32_t (&onb)[kChunk], double (&oval)[kChunk]) {
+        int32_t cst[kChunk];
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) cst[j] = pst[j];
+        commit(t0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (t0 + kChunk < Lg) fetch(t0 + kChunk);  // in flight while this chunk is walked
+        const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const int32_t t = t0 + j;
+            if (t < L) {
+                const double v = r_amt[(t & (kRing - 1)) * S_MAX + l];
+                const int32_t st = cst[j];
+                if (st >= t) {  // start[i] >= end[i-1] (or i == 0): pandas re-initialises
+                    sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
+                } else {
+                    for (int32_t k = tail; k < st; ++k) {  // rows leaving the window (Kahan remove)
+                        int e = (k & (kRing - 1)) * S_MAX + l;
+                        if (k < oldest) {  // older than the ring: via this lane's miss slot
+                            e = kRing * S_MAX + lane;
+                            r_amt[e] = g_amt[(int64_t)k * S];
+                        }
+                        const double a = r_amt[e];
+                        if (a == a) {
+                            nobs -= 1;
+                            const double y = -a - c_rem;
+                            const double tt = sum + y;
+                            c_rem = (tt - sum) - y;
+                            sum = tt;
+                        }
+                    }
+                }
+                tail = st;
+                if (v == v) {  // Kahan add
+                    nobs += 1;
+                    const double y = v - c_add;
+                    const double tt = sum + y;
+                    c_add = (tt - sum) - y;
+                    sum = tt;
+                    nsame = (v == prev) ? nsame + 1 : 1;
+                    prev = v;
+                }
+                onb[j] = nobs;
+                oval[j] = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            if (t0 + j < L) {
+                nb[(int64_t)(t0 + j) * S] = onb[j];
+                sm[(int64_t)(t0 + j) * S] = oval[j];
+            }
+        }
+    };
+    int32_t nb_a[kChunk], nb_b[kChunk];
+    double val_a[kChunk], val_b[kChunk];
+    if (Lg > 0) fetch(0);
+    for (int32_t t0 = 0; t0 < Lg; t0 += 2 * kChunk) {
+        chunk(t0, nb_a, val_a);
+        if (t0 + kChunk < Lg) chunk(t0 + kChunk, nb_b, val_b);
+    }
+}
+
 // ------------------------------------------------------------------ terminal windows
 constexpr int kTermBlock = 256;
 constexpr int kTermWaves = kTermBlock / kWave;
@@ -438,12 +625,22 @@ __device__ __forceinline__ int64_t upper_bound_seg(const SegTs &a, int64_t lo, i
     return lo;
 }
 
+// RUNS: segments need not be in time order -- the multi-GPU owner side, where a terminal's
+// rows arrive as one time-sorted run per source rank.  The runs are found in the staged
+// segment (a run starts wherever ts descends) and every count of the closed form is summed
+// over the runs, each searched separately (a run is sorted; the prefix fraud counts of the
+// staged order serve each run): still exact and tie-order independent, no sort, records
+// written in place.  More than kMaxRuns runs, or segments longer than the LDS stage, are
+// counted directly (O(L^2), correct for any order).
+constexpr int kMaxRuns = 64;
+template <bool RUNS>
 __global__ void __launch_bounds__(kTermBlock) k_terminal(
     const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
     int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out) {
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
     __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
+    __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
@@ -455,37 +652,137 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
         const int64_t b = seg_off[seg], e = seg_off[seg + 1];
         const int64_t L = e - b;
         if (L <= 0) continue;
+        int nruns = 1;
         if (L <= kTermLdsRows) {
             int carry = 0;
             if (lane == 0) lf[0] = 0;
-            for (int64_t c = 0; c < L; c += kWave) {
-                const int64_t j = c + lane;
-                int f = 0;
-                if (j < L) {
-                    const int64_t src = rows ? rows[b + j] : b + j;
-                    lts[j] = ts[src];
-                    f = fraud[src] != 0;
+            if constexpr (RUNS) {
+                // stage + prefix (staging order), then the run starts: descents of ts
+                for (int64_t c = 0; c < L; c += kWave) {
+                    const int64_t j = c + lane;
+                    int f = 0;
+                    if (j < L) {
+                        const int64_t src = rows ? rows[b + j] : b + j;
+                        lts[j] = ts[src];
+                        f = fraud[src] != 0;
+                    }
+                    int inc = wave_incl_scan(f, lane) + carry;
+                    if (j < L) lf[j + 1] = inc;
+                    carry = __shfl(inc, kWave - 1, kWave);
                 }
-                int inc = wave_incl_scan(f, lane) + carry;
-                if (j < L) lf[j + 1] = inc;
-                carry = __shfl(inc, kWave - 1, kWave);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                int32_t *lr = s_runs[wv];
+                int nr = 1;
+                if (lane == 0) lr[0] = 0;
+                for (int64_t c = 0; c < L; c += kWave) {
+                    const int64_t j = c + lane;
+                    const bool d = j > 0 && j < L && lts[j] < lts[j - 1];
+                    const uint64_t m = __ballot(d);
+                    const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
+                    if (d && at < kMaxRuns) lr[at] = (int32_t)j;
+                    nr += __popcll(m);
+                }
+                if (lane == 0 && nr <= kMaxRuns) lr[nr] = (int32_t)L;
+                nruns = nr;
+            } else {
+                for (int64_t c = 0; c < L; c += kWave) {
+                    const int64_t j = c + lane;
+                    int f = 0;
+                    if (j < L) {
+                        const int64_t src = rows ? rows[b + j] : b + j;
+                        lts[j] = ts[src];
+                        f = fraud[src] != 0;
+                    }
+                    int inc = wave_incl_scan(f, lane) + carry;
+                    if (j < L) lf[j + 1] = inc;
+                    carry = __shfl(inc, kWave - 1, kWave);
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (RUNS && nruns > 1) {
+                const int32_t *lr = s_runs[RUNS ? wv : 0];
+                if (nruns <= kMaxRuns) {
+                    for (int64_t i = lane; i < L; i += kWave) {
+                        const int64_t t = lts[i];
+                        const int64_t row = rows ? rows[b + i] : b + i;
+                        int32_t nbh = 0, frh = 0;
+                        for (int r = 0; r < nruns; ++r) {
+                            const int64_t h = upper_bound(lts, lr[r], lr[r + 1], t - delay);
+                            nbh += (int32_t)(h - lr[r]);
+                            frh += lf[h] - lf[lr[r]];
+                        }
+                        for (int w = 0; w < n_win; ++w) {
+                            int32_t nbl = 0, frl = 0;
+                            for (int r = 0; r < nruns; ++r) {
+                                const int64_t lo = upper_bound(lts, lr[r], lr[r + 1], t - delay - win.w[w]);
+                                nbl += (int32_t)(lo - lr[r]);
+                                frl += lf[lo] - lf[lr[r]];
+                            }
+                            term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl, frh - frl);
+                        }
+                    }
+                } else {
+                    for (int64_t i = lane; i < L; i += kWave) {  // too many runs: direct counts
+                        const int64_t t = lts[i];
+                        const int64_t row = rows ? rows[b + i] : b + i;
+                        int32_t nbh = 0, frh = 0, nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
+                        for (int64_t j = 0; j < L; ++j) {
+                            const int64_t tj = lts[j];
+                            if (tj > t - delay) continue;
+                            const int fj = lf[j + 1] - lf[j];
+                            ++nbh;
+                            frh += fj;
+                            for (int w = 0; w < n_win; ++w)
+                                if (tj <= t - delay - win.w[w]) {
+                                    ++nbl[w];
+                                    frl[w] += fj;
+                                }
+                        }
+                        for (int w = 0; w < n_win; ++w)
+                            term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl[w], frh - frl[w]);
+                    }
+                }
+            } else {
+                for (int64_t i = lane; i < L; i += kWave) {
+                    const int64_t t = lts[i];
+                    const int64_t hi = upper_bound(lts, 0, i, t - delay);
+                    const int32_t fhi = lf[hi];
+                    const int64_t row = rows ? rows[b + i] : b + i;  // coalesced re-read
+                    for (int w = 0; w < n_win; ++w) {
+                        const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
+                        term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo),
+                                   fhi - lf[lo]);
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else if (RUNS) {  // long unsorted segment: direct counts over the segment
+            const SegTs gts{ts, rows, b};
             for (int64_t i = lane; i < L; i += kWave) {
-                const int64_t t = lts[i];
-                const int64_t hi = upper_bound(lts, 0, i, t - delay);
-                const int32_t fhi = lf[hi];
-                const int64_t row = rows ? rows[b + i] : b + i;  // coalesced re-read
-                for (int w = 0; w < n_win; ++w) {
-                    const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), fhi - lf[lo]);
+                const int64_t t = gts[i];
+                const int64_t row = rows ? rows[b + i] : b + i;
+                int32_t nb_hi = 0, fr_hi = 0, nb_lo[FDX_MAX_WINDOWS] = {}, fr_lo[FDX_MAX_WINDOWS] = {};
+                for (int64_t j = 0; j < L; ++j) {
+                    const int64_t tj = gts[j];
+                    if (tj > t - delay) continue;
+                    const int fj = fraud[rows ? rows[b + j] : b + j] != 0;
+                    ++nb_hi;
+                    fr_hi += fj;
+                    for (int w = 0; w < n_win; ++w)
+                        if (tj <= t - delay - win.w[w]) {
+                            ++nb_lo[w];
+                            fr_lo[w] += fj;
+                        }
                 }
+                for (int w = 0; w < n_win; ++w)
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nb_hi - nb_lo[w], fr_hi - fr_lo[w]);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {
             const SegTs gts{ts, rows, b};
             for (int64_t i = lane; i < L; i += kWave) {
@@ -597,17 +894,16 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     if (n_seg == 0 || n == 0) return FDX_OK;
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
+    hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
                        fraud_d, (const int32_t *)nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d,
                        risk_d, (int64_t *)nullptr);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
 }
 
-extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
-                                           const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
-                                           int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
-                                           int64_t *rec_d, void *stream) {
+static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
+                           const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                           const int64_t *window_ns, int32_t n_windows, int64_t *rec_d, bool sort, void *stream) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -616,11 +912,32 @@ extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t
     if (n_seg == 0 || n == 0) return FDX_OK;
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && rec_d, "null pointer");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    hipLaunchKernelGGL(k_terminal, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
-                       row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
-                       rec_d);
+    if (sort)
+        hipLaunchKernelGGL(k_terminal<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
+                           row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
+                           rec_d);
+    else
+        hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
+                           row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
+                           rec_d);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
+}
+
+extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                           const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                           int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
+                                           int64_t *rec_d, void *stream) {
+    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
+                           false, stream);
+}
+
+extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                                    const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg,
+                                                    int64_t n, int64_t delay_ns, const int64_t *window_ns,
+                                                    int32_t n_windows, int64_t *rec_d, void *stream) {
+    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
+                           true, stream);
 }
 
 extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
@@ -727,6 +1044,25 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
         return e ? atoi(e) : INT32_MAX;
     }();
     hipStream_t st = as_stream(stream);
+    static const int walk_env = [] {  // FDX_CUSTOMER_WALK=0: the one-pass ring kernel instead
+        const char *e = getenv("FDX_CUSTOMER_WALK");
+        return e ? atoi(e) : 1;
+    }();
+    if (walk_env && S <= 21) {
+        const int64_t n_rows = n_slots / S;
+        const int64_t waves = ceil_div(n_rows, (int64_t)kChunk);
+        hipLaunchKernelGGL(k_customer_starts, dim3((unsigned)ceil_div(waves * kWave, (int64_t)256)), dim3(256), 0, st,
+                           its_d, seg_off_d, sorder_d, goff_d, n_groups, n_seg, S, n_slots, wa, n_windows, nb_d);
+        FDX_LAUNCHED("k_customer_starts");
+        if (walk_env == 256)
+            hipLaunchKernelGGL((k_customer_walk<21, 256>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
+                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d);
+        else
+            hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
+                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d);
+        FDX_LAUNCHED("k_customer_walk");
+        return FDX_OK;
+    }
 #define FDX_RING(SM, RG, LO, HI)                                                                          \
     hipLaunchKernelGGL((k_customer_ring<SM, RG>), dim3((unsigned)n_groups), dim3(64), 0, st, its_d, iamt_d, seg_off_d, \
                        sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d, (int32_t)(LO), (int32_t)(HI))

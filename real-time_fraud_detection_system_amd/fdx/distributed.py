@@ -7,8 +7,9 @@ rows of a terminal on one rank: owner(t) = t % world.  Per step
 
   owner keys -> stable re-key by owner -> pack {ts, term|fraud|row} (16 B/row)
   -> all_to_all_single (splits exchanged first, 8 B per peer)
-  -> owner: unpack, time sort + re-key by local terminal id, terminal windows as count
-     records (W words/row: NB | FRAUD << 32) written straight to receive positions
+  -> owner: unpack, re-key by local terminal id (segments = per-rank time-sorted runs,
+     sorted inside the records kernel), terminal windows as count records (W words/row:
+     NB | FRAUD << 32) written straight to receive positions
   -> all_to_all_single back (splits mirrored) -> scatter into the local feature matrix
   -> scale + forest locally.
 
@@ -60,7 +61,8 @@ class GpuKernels:
 
     @staticmethod
     def terminal_records(ts, fraud, rows, seg, delay_days, windows_days):
-        return ops.terminal_windows_packed(ts, fraud, seg, delay_days, windows_days, rows=rows)
+        """count records of every segment, segments in any time order (sorted in-kernel)"""
+        return ops.terminal_windows_packed_unsorted(ts, fraud, seg, delay_days, windows_days, rows=rows)
 
     @staticmethod
     def reply_assemble(reply, perm, W, X, col0):
@@ -68,29 +70,43 @@ class GpuKernels:
                                              X.stride(0), col0, ops._s()), "fdx_reply_assemble")
 
 
-def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
-                               delay_days=7, group=None):
-    """Runs the re-key exchange and the owner-side terminal windows.  Returns
-    (reply [n_local, W] count records in send order, send_perm [n_local] send position ->
-    local row)."""
+def exchange_begin(K, term, world, group=None):
+    """Phase 1 (enqueue only, no host sync): owner keys, re-key by owner, split exchange."""
     owner = K.owner_keys(term, world)
     send_perm, send_seg = K.rekey(owner, world)
     send_counts = (send_seg[1:] - send_seg[:-1]).to(torch.int64)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
+    return send_perm, send_counts, recv_counts
+
+
+def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30), delay_days=7,
+                    group=None):
+    """Phase 2: all-to-all of the rows, owner-side terminal records, all-to-all back.
+    Returns (reply [n_local, W] count records in send order, send_perm)."""
+    send_perm, send_counts, recv_counts = state
     sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
     rec = K.exchange_pack(ts, term, fraud, send_perm)
     recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
     dist.all_to_all_single(recv, rec, output_split_sizes=rc, input_split_sizes=sc, group=group)
     rts, rterm, rfr = K.exchange_unpack(recv, world)
     n_local_terms = (n_terminals_total + world - 1) // world
-    tperm = K.argsort_i64(rts)                                  # time order (stable)
-    gperm, gseg = K.rekey(K.gather(rterm, tperm), n_local_terms)  # then by terminal (stable)
-    perm = K.gather(tperm, gperm)                               # grouped position -> receive index
+    # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
+    # the records kernel handles such segments itself (no global time sort of the receive buffer)
+    perm, gseg = K.rekey(rterm, n_local_terms)                  # grouped position -> receive index
     reply = K.terminal_records(rts, rfr, perm, gseg, delay_days, windows_days)  # indexed by receive index
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
     dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
     return back, send_perm
+
+
+def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
+                               delay_days=7, group=None):
+    """Runs the re-key exchange and the owner-side terminal windows.  Returns
+    (reply [n_local, W] count records in send order, send_perm [n_local] send position ->
+    local row)."""
+    state = exchange_begin(K, term, world, group)
+    return exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days, delay_days, group)
 
 
 class ShardedPipeline:
@@ -126,24 +142,42 @@ class ShardedPipeline:
         return X[:, : p.n_features]
 
     def run(self, ts, customer, terminal, amount, fraud, n_customers_total, proba, ws, events=None):
-        """featurize + score this rank's rows (customer-grouped scoring rows; the terminal
-        half comes back from the owners as packed reply records)."""
+        """featurize + score this rank's rows: the single-GPU scoring path (interleaved
+        customer layout, FraudPipeline.run_fused) for the customer half; the terminal half
+        comes back from the owners as packed count records in send order."""
         p = self.pipe
+        W = len(p.windows_days)
         n_local = n_customers_total // self.world
         base = self.rank * n_local if self.customer_base is None else self.customer_base
+        # The terminal exchange (RCCL all-to-all there and back + the owner-side windows)
+        # runs on a side stream, overlapped with the customer half on the main stream; the
+        # two meet at the scoring-row assembly.
+        main = torch.cuda.current_stream()
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=ts.device)
+        side = self._side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            state = exchange_begin(GpuKernels, terminal, self.world, self.group)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         cperm, cseg, _ = ops.rekey(cust, n_local)
-        cts, camt = ops.gather(ts, cperm), ops.gather(amount, cperm)
-        cnb, cavg = ops.customer_windows(cts, camt, cseg, p.windows_days)
-        back, send_perm = exchange_terminal_features(GpuKernels, ts, terminal, fraud, self.world,
-                                                     self.n_terminals_total, p.windows_days, p.delay_days,
-                                                     self.group)
-        sinv = ops.invert_perm(send_perm)
-        ops.forest_prepare_grouped(p.forest, p.flags_mode, cts, camt, cnb, cavg, cperm, sinv, back, ws)  # averages
+        lay = ops.customer_layout(cseg, cperm, ts, amount, W, None, p._slots_hint)  # (host sync on main)
+        p._slots_hint = lay.its.numel()
+        with torch.cuda.stream(side):
+            back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
+                                              self.n_terminals_total, p.windows_days, p.delay_days, self.group)
+            sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
+        inb, isum = ops.customer_windows_interleaved(lay, cseg, p.windows_days)
+        main.wait_stream(side)
+        back.record_stream(main)
+        sinv.record_stream(main)
+        ws = p._forest_ws(lay.n_slots, ws, ts.device)
+        ops.forest_prepare_grouped(p.forest, p.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, sinv, back, ws,
+                                   n=lay.n_slots, val_is_sum=True)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-        ops.forest_traverse_perm(p.forest, ts.numel(), ws, proba, cperm)
+        ops.forest_traverse_perm(p.forest, lay.n_slots, ws, proba, lay.irow)
         if events is not None:
             b.record()
             events.append((a, b))

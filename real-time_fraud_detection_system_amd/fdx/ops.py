@@ -230,6 +230,25 @@ def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1
     return rec
 
 
+def terminal_windows_packed_unsorted(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), rows=None,
+                                     stream=None):
+    """terminal_windows_packed for segments that are not in time order (each is sorted in
+    the kernel): the multi-GPU owner side, whose segments are concatenated per-rank runs."""
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
+    if rows is not None:
+        _dev(rows, torch.int32, "rows")
+        if rows.numel() != ts_ns.numel():
+            raise ValueError("rows must have one entry per transaction")
+    n = ts_ns.numel()
+    W = len(windows_days)
+    rec = torch.empty((n, W), dtype=torch.int64, device=ts_ns.device)
+    check(_lib.load().fdx_terminal_windows_packed_unsorted(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(seg_off),
+                                                           seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
+                                                           _win_ns(windows_days), W, _ptr(rec), _s(stream)),
+          "fdx_terminal_windows_packed_unsorted")
+    return rec
+
+
 def unpack_term_records(rec: torch.Tensor):
     """Count records -> (nb int32 [W, n], risk float64 [W, n]) with the kernels' division."""
     w = rec.T

@@ -58,8 +58,12 @@ class CpuKernels:
 
     @staticmethod
     def terminal_records(ts, fraud, rows, seg, delay_days, windows_days):
-        """count records (NB | FRAUD << 32) of grouped row q stored at rows[q]"""
+        """count records (NB | FRAUD << 32) of grouped row q stored at rows[q]; segments may
+        be out of time order (as the HIP kernel, each is time-sorted first, stably)"""
         r = rows.numpy()
+        sg = seg.numpy()
+        sid = np.repeat(np.arange(len(sg) - 1), np.diff(sg))
+        r = r[np.lexsort((ts.numpy()[r], sid))]
         nb, risk = oracle.terminal_windows(ts.numpy()[r], fraud.numpy()[r], seg.numpy(), delay_days, windows_days)
         fr = np.rint(risk * nb).astype(np.int64)  # counts are small integers: exact
         rec = np.zeros((len(r), len(windows_days)), np.int64)

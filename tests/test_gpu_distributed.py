@@ -74,3 +74,26 @@ def test_fused_scoring_paths_agree(dev, golden):
         np.testing.assert_array_equal(p2.cpu().numpy(), p_ref.cpu().numpy())
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("parts", [1, 4, 8, 100])
+def test_terminal_records_unsorted_runs(dev, parts):
+    """The owner side of the exchange: rows arrive as one time-sorted run per source rank,
+    so a stable re-key by terminal yields segments of concatenated runs.  The records of
+    fdx_terminal_windows_packed_unsorted must equal those of the time-sorted input row by
+    row -- for 1 run (sorted), a few runs, and more runs than the per-run search handles
+    (100 > kMaxRuns: direct counts)."""
+    d = synth.generate(n_customers=600, n_terminals=300, nb_days=80, r=30, seed=5)
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    n = len(d["ts"])
+    ts, term, fr = T(d["ts"], torch.int64), T(d["terminal"], torch.int32), T(d["fraud"], torch.uint8)
+    tperm, tseg, _ = ops.rekey(term, 300)
+    ref = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()   # by input row
+    # "receive buffer": rows grouped by source part (customer % parts), time order inside
+    order = np.argsort(d["customer"] % parts, kind="stable")
+    rts, rterm, rfr = T(d["ts"][order], torch.int64), T(d["terminal"][order], torch.int32), \
+        T(d["fraud"][order], torch.uint8)
+    gperm, gseg, _ = ops.rekey(rterm, 300)
+    got = ops.terminal_windows_packed_unsorted(rts, rfr, gseg, rows=gperm).cpu().numpy()  # by receive index
+    np.testing.assert_array_equal(got, ref[order])
+    assert n > 0
