@@ -35,6 +35,20 @@ def forest_bytes_per_row(variant, n_chunks):
     return row * n_chunks + 16 * (n_chunks - 1) + 8
 
 
+def pmc_traffic(variant):
+    """HBM bytes per forest launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_forest.json, FETCH_SIZE/WRITE_SIZE passes corrected as MI355X_MICROARCH.md
+    prescribes) when it was measured on this traversal variant; else (None, None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_forest.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    if d.get("variant") != variant:
+        return None, None
+    return d["hbm_bytes_per_launch"], d["source"]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +202,7 @@ def main():
     fvar = forest.variant if args.forest_variant < 0 else args.forest_variant
     bpr = forest_bytes_per_row(fvar, forest.n_chunks)
     achieved = bpr * n_local / (trav_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(fvar)
     out = {
         "metric": METRIC,
         "value": round(n_total * args.steps / dt, 1),
@@ -207,7 +222,9 @@ def main():
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)"},
         "roofline": {"kernel": "k_forest_rank" if fvar >= 16 else "k_forest_chunk", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "avg_launch_ms": round(launch_ms, 4),
+                     "traffic": traffic, "traffic_unit": "bytes per launch",
+                     "algorithmic_bytes_per_launch": round(bpr / forest.n_chunks * n_local),
+                     "traffic_source": traffic_src, "avg_launch_ms": round(launch_ms, 4),
                      "launches_per_step": launches,
                      "traverse_ms": round(trav_ms, 3),
                      "forest_variant": fvar,

@@ -135,6 +135,18 @@ int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, 
                                 const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
                                 void *stream);
 
+/* Same records, written to rec_d[dest_d[row]] instead of rec_d[row] (dest_d: input row ->
+ * output position, e.g. fdx_invert_slots of the interleaved customer layout, so that the
+ * terminal half of a scoring row sits at its slot and fdx_forest_prepare_grouped reads it
+ * sequentially: FDX_PREP_TERM_BY_SLOT).  rec_d: [max dest + 1][n_windows]. */
+int fdx_terminal_windows_packed_dest(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
+                                     const int32_t *dest_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                     int64_t delay_ns, const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
+                                     void *stream);
+/* slot_of_d[irow_d[s]] = s for every slot s < n_slots with 0 <= irow_d[s] < n_rows (inverse of
+ * the interleaved layout's slot -> row map; padding slots are skipped). */
+int fdx_invert_slots(const int32_t *irow_d, int64_t n_slots, int32_t *slot_of_d, int64_t n_rows, void *stream);
+
 /* Same records when the segments are NOT in time order (the multi-GPU owner side: a
  * terminal's rows arrive as one time-sorted run per source rank, so a stable re-key by
  * terminal gives segments of concatenated runs).  Each segment is time-sorted inside the
@@ -317,8 +329,12 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
  * with fdx_forest_traverse_perm(out_perm = cust_perm)
  * so that proba lands in row order.  The same call serves the interleaved customer layout
  * (cust_* = slot arrays, cust_perm = irow): slots with cust_perm < 0 are padding (zero
- * row, never written back).  cust_val_is_sum = 1: cust_avg_d holds rolling sums and the
- * average is computed here as sum / nb. */
+ * row, never written back).  cust_val_is_sum: FDX_PREP_* option bits (1 = cust_avg_d
+ * holds rolling sums and the average is computed here as sum / nb; 2 = terminal records
+ * by scoring row). */
+#define FDX_PREP_VAL_IS_SUM 1   /* cust_avg_d holds rolling sums: average = sum / nb here      */
+#define FDX_PREP_TERM_BY_SLOT 2 /* term_rec_d[i] is row i's record (fdx_terminal_windows_packed_
+                                   dest with the slot map); term_inv_d is ignored           */
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
                                int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                const int32_t *cust_nb_d, const double *cust_avg_d,

@@ -445,7 +445,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             q[15] = 0u;
             v[0] = zval(camt[i], mean, scale, 0);
             bool nan = v[0] != v[0];
-            const int64_t q_ = term_inv ? term_inv[r] : r;
+            const int64_t q_ = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
             const int64_t *rec = term_rec + q_ * W;
 #pragma unroll
             for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
@@ -453,12 +453,12 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                     const int32_t c = cnb[(int64_t)w * n + i];
                     const double cv = cval[(int64_t)w * n + i];
                     count(3 + 2 * w, c);
-                    v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
+                    v[4 + 2 * w] = zval((val_is_sum & 1) ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
                     const int64_t tw = rec[w];
                     const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
                     count(3 + 2 * W + 2 * w, tnb);
                     const int fr_ = 4 + 2 * W + 2 * w;
-                    if (tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb) {
+                    if (rt.rat && tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb) {
                         q[fr_] = rt.rat[((int64_t)fr_ * kRatN + tnb) * kRatN + tfr];
                     } else {
                         v[fr_] = zval(term_risk(tw), mean, scale, fr_);
@@ -470,7 +470,13 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                 }
             }
             if (nan) *nan_flag = 1;
-            if (W == 3) {  // the reference's layout: amount + 3 averages searched in fixed rounds
+            if (W == 3 && !rt.rat) {  // the reference's layout, risks searched too
+                constexpr int kFix[7] = {0, 4, 6, 8, 10, 12, 14};
+                rank_fixed<7>(v, kFix, rt, s_smp, q);
+                need &= ~((1u << 0) | (1u << 4) | (1u << 6) | (1u << 8) | (1u << 10) | (1u << 12) | (1u << 14));
+                need &= (1u << nf) - 1u;
+                if (__any(need != 0)) rank_row(v, nf, rt, s_smp, q, need);  // table overflows (rare)
+            } else if (W == 3) {  // the reference's layout: amount + 3 averages searched in fixed rounds
                 constexpr int kFix[4] = {0, 4, 6, 8};
                 rank_fixed<4>(v, kFix, rt, s_smp, q);
                 need &= ~((1u << 0) | (1u << 4) | (1u << 6) | (1u << 8));
@@ -488,7 +494,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         v[1] = zval((double)we, mean, scale, 1);
         v[2] = zval((double)ni, mean, scale, 2);
         bool nan = v[0] != v[0];
-        const int64_t q = term_inv ? term_inv[r] : r;
+        const int64_t q = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
         const int64_t *rec = term_rec + q * W;
 #pragma unroll
         for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
@@ -496,7 +502,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                 const int32_t c = cnb[(int64_t)w * n + i];
                 const double cv = cval[(int64_t)w * n + i];
                 v[3 + 2 * w] = zval((double)c, mean, scale, 3 + 2 * w);
-                v[4 + 2 * w] = zval(val_is_sum ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
+                v[4 + 2 * w] = zval((val_is_sum & 1) ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
                 const int64_t tw = rec[w];
                 v[3 + 2 * W + 2 * w] = zval((double)term_nb(tw), mean, scale, 3 + 2 * W + 2 * w);
                 v[4 + 2 * W + 2 * w] = zval(term_risk(tw), mean, scale, 4 + 2 * W + 2 * w);
@@ -1646,7 +1652,8 @@ static RankTab rank_tab(const fdx_forest_s *F) {
     rt.seg = F->rseg;
     rt.n_smp = F->rnsmp;
     rt.itab = F->ritab_d;
-    rt.rat = F->rrat_d;
+    static const bool no_rat = getenv("FDX_PREP_NORAT") != nullptr;  // A/B switch: search the risks
+    rt.rat = no_rat ? nullptr : F->rrat_d;
     return rt;
 }
 

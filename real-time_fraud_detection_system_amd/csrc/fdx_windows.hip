@@ -637,7 +637,8 @@ template <bool RUNS>
 __global__ void __launch_bounds__(kTermBlock) k_terminal(
     const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
-    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out) {
+    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
+    const int32_t *__restrict__ dest) {
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
     __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
     __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
@@ -648,6 +649,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
     int64_t *lts = s_ts[wv];
     int32_t *lf = s_f[wv];
 
+    auto dest_of = [&](int64_t r) -> int64_t { return dest ? (int64_t)dest[r] : r; };
     for (int64_t seg = gwave; seg < n_seg; seg += nwaves) {
         const int64_t b = seg_off[seg], e = seg_off[seg + 1];
         const int64_t L = e - b;
@@ -708,7 +710,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                 if (nruns <= kMaxRuns) {
                     for (int64_t i = lane; i < L; i += kWave) {
                         const int64_t t = lts[i];
-                        const int64_t row = rows ? rows[b + i] : b + i;
+                        const int64_t row = dest_of(rows ? rows[b + i] : b + i);
                         int32_t nbh = 0, frh = 0;
                         for (int r = 0; r < nruns; ++r) {
                             const int64_t h = upper_bound(lts, lr[r], lr[r + 1], t - delay);
@@ -728,7 +730,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                 } else {
                     for (int64_t i = lane; i < L; i += kWave) {  // too many runs: direct counts
                         const int64_t t = lts[i];
-                        const int64_t row = rows ? rows[b + i] : b + i;
+                        const int64_t row = dest_of(rows ? rows[b + i] : b + i);
                         int32_t nbh = 0, frh = 0, nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
                         for (int64_t j = 0; j < L; ++j) {
                             const int64_t tj = lts[j];
@@ -751,7 +753,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
                     const int64_t t = lts[i];
                     const int64_t hi = upper_bound(lts, 0, i, t - delay);
                     const int32_t fhi = lf[hi];
-                    const int64_t row = rows ? rows[b + i] : b + i;  // coalesced re-read
+                    const int64_t row = dest_of(rows ? rows[b + i] : b + i);  // coalesced re-read
                     for (int w = 0; w < n_win; ++w) {
                         const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
                         term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo),
@@ -766,7 +768,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
             const SegTs gts{ts, rows, b};
             for (int64_t i = lane; i < L; i += kWave) {
                 const int64_t t = gts[i];
-                const int64_t row = rows ? rows[b + i] : b + i;
+                const int64_t row = dest_of(rows ? rows[b + i] : b + i);
                 int32_t nb_hi = 0, fr_hi = 0, nb_lo[FDX_MAX_WINDOWS] = {}, fr_lo[FDX_MAX_WINDOWS] = {};
                 for (int64_t j = 0; j < L; ++j) {
                     const int64_t tj = gts[j];
@@ -788,7 +790,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
             for (int64_t i = lane; i < L; i += kWave) {
                 const int64_t t = gts[i];
                 const int64_t hi = upper_bound_seg(gts, 0, i, t - delay);
-                const int64_t row = rows ? rows[b + i] : b + i;
+                const int64_t row = dest_of(rows ? rows[b + i] : b + i);
                 for (int w = 0; w < n_win; ++w) {
                     const int64_t lo = upper_bound_seg(gts, 0, hi, t - delay - win.w[w]);
                     int32_t fr = 0;
@@ -896,14 +898,15 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
                        fraud_d, (const int32_t *)nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d,
-                       risk_d, (int64_t *)nullptr);
+                       risk_d, (int64_t *)nullptr, (const int32_t *)nullptr);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
 }
 
 static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
                            const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                           const int64_t *window_ns, int32_t n_windows, int64_t *rec_d, bool sort, void *stream) {
+                           const int64_t *window_ns, int32_t n_windows, int64_t *rec_d, bool sort, void *stream,
+                           const int32_t *dest_d = nullptr) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -915,11 +918,11 @@ static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const
     if (sort)
         hipLaunchKernelGGL(k_terminal<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
                            row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
-                           rec_d);
+                           rec_d, dest_d);
     else
         hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
                            row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
-                           rec_d);
+                           rec_d, dest_d);
     FDX_LAUNCHED("k_terminal");
     return FDX_OK;
 }
@@ -930,6 +933,35 @@ extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t
                                            int64_t *rec_d, void *stream) {
     return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
                            false, stream);
+}
+
+extern "C" int fdx_terminal_windows_packed_dest(const int64_t *ts_ns_d, const uint8_t *fraud_d,
+                                                const int32_t *row_d, const int32_t *dest_d, const int64_t *seg_off_d,
+                                                int64_t n_seg, int64_t n, int64_t delay_ns, const int64_t *window_ns,
+                                                int32_t n_windows, int64_t *rec_d, void *stream) {
+    FDX_REQUIRE(dest_d, "null dest");
+    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
+                           false, stream, dest_d);
+}
+
+__global__ void k_invert_slots(const int32_t *__restrict__ irow, int64_t n_slots, int32_t *__restrict__ slot_of,
+                               int64_t n_rows) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_slots;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = irow[s];
+        if (r >= 0 && r < n_rows) slot_of[r] = (int32_t)s;
+    }
+}
+
+extern "C" int fdx_invert_slots(const int32_t *irow_d, int64_t n_slots, int32_t *slot_of_d, int64_t n_rows,
+                                void *stream) {
+    FDX_REQUIRE(n_slots >= 0 && n_rows >= 0, "negative size");
+    if (n_slots == 0) return FDX_OK;
+    FDX_REQUIRE(irow_d && slot_of_d, "null pointer");
+    hipLaunchKernelGGL(k_invert_slots, dim3(stream_grid(n_slots, 256)), dim3(256), 0, as_stream(stream), irow_d,
+                       n_slots, slot_of_d, n_rows);
+    FDX_LAUNCHED("k_invert_slots");
+    return FDX_OK;
 }
 
 extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *fraud_d,

@@ -55,6 +55,8 @@ SIGNATURES = {
     "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
     "fdx_terminal_windows_packed_unsorted": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
+    "fdx_terminal_windows_packed_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
+    "fdx_invert_slots": (ctypes.c_int, [P, c_i64, P, c_i64, P]),
     "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),
     "fdx_rekey": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, c_sz, P]),

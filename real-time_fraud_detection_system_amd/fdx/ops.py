@@ -230,6 +230,34 @@ def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1
     return rec
 
 
+def terminal_windows_packed_dest(ts_ns, fraud, seg_off, rows, dest, n_out: int, delay_days=7,
+                                 windows_days=(1, 7, 30), stream=None):
+    """terminal_windows_packed with the record of input row r written at dest[r] (e.g. its
+    scoring slot: dest = invert_slots(layout.irow, n, layout.n_slots)); returns rec [n_out, W]."""
+    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
+    _dev(rows, torch.int32, "rows"); _dev(dest, torch.int32, "dest")
+    n = ts_ns.numel()
+    W = len(windows_days)
+    rec = torch.empty((int(n_out), W), dtype=torch.int64, device=ts_ns.device)
+    check(_lib.load().fdx_terminal_windows_packed_dest(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(dest), _ptr(seg_off),
+                                                       seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
+                                                       _win_ns(windows_days), W, _ptr(rec), _s(stream)),
+          "fdx_terminal_windows_packed_dest")
+    return rec
+
+
+def invert_slots(irow, n_rows: int, n_slots: int, stream=None):
+    """slot_of[irow[s]] = s for the interleaved layout's non-padding slots s < n_slots
+    (irow may be longer: the layout buffers are sized for the worst case)."""
+    _dev(irow, torch.int32, "irow")
+    if not 0 <= int(n_slots) <= irow.numel():
+        raise FdxError("n_slots out of range")
+    out = torch.empty(int(n_rows), dtype=torch.int32, device=irow.device)
+    check(_lib.load().fdx_invert_slots(_ptr(irow), int(n_slots), _ptr(out), int(n_rows), _s(stream)),
+          "fdx_invert_slots")
+    return out
+
+
 def terminal_windows_packed_unsorted(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), rows=None,
                                      stream=None):
     """terminal_windows_packed for segments that are not in time order (each is sorted in
@@ -380,11 +408,13 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False):
-    """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path)."""
+                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_by_slot: bool = False):
+    """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
+    term_by_slot: term_rec[i] is scoring row i's record (terminal_windows_packed_dest)."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
-    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), int(val_is_sum), _ptr(cts),
+    opts = (1 if val_is_sum else 0) | (2 if term_by_slot else 0)
+    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
                                                  _ptr(camt), _ptr(cnb),
                                                  _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),
                                                  ws.numel(), _s(stream)), "fdx_forest_prepare_grouped")

@@ -107,7 +107,8 @@ class FraudPipeline:
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
-        row, read by input row); the last forest launch writes proba back in input row order."""
+        slot, written there by the terminal kernel); the last forest launch writes proba back
+        in input row order."""
         W = len(self.windows_days)
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
         lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
@@ -115,7 +116,10 @@ class FraudPipeline:
         self.last_slots = lay.n_slots
         inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
-        # count records in input row order (the kernel reads ts/fraud through tperm)
+        # count records in input row order (the kernel reads ts/fraud through tperm).  Measured
+        # (r01): writing them at their scoring slots instead (terminal_windows_packed_dest +
+        # invert_slots, sequential reads in the row assembly) costs the terminal kernel one
+        # more random read per row than it saves the assembly: 3.23 ms vs 2.93 ms.
         trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days, rows=tperm,
                                            stream=stream)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)

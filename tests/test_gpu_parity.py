@@ -299,3 +299,27 @@ def test_forest_variants_bit_identical(dev, golden, variant):
     op, ol = oracle.forest_predict(Xr, arr, want_leaves=True)
     np.testing.assert_array_equal(l.cpu().numpy(), ol)
     np.testing.assert_array_equal(p.cpu().numpy(), op)
+
+
+def test_terminal_records_at_slots(dev):
+    """fdx_invert_slots + fdx_terminal_windows_packed_dest (records at scoring slots) equal the
+    row-order records gathered through the layout, and FDX_PREP_TERM_BY_SLOT scores the
+    same as the row-order path."""
+    from fdx import synth
+    from fdx.pipeline import FraudPipeline
+
+    d = synth.generate(n_customers=700, n_terminals=900, nb_days=70, seed=21)
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    ts, cust, term = T(d["ts"], torch.int64), T(d["customer"], torch.int32), T(d["terminal"], torch.int32)
+    amt, fr = T(d["amount"], torch.float64), T(d["fraud"], torch.uint8)
+    n = ts.numel()
+    cperm, cseg, _ = ops.rekey(cust, 700)
+    lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
+    tperm, tseg, _ = ops.rekey(term, 900)
+    by_row = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()
+    slot_of = ops.invert_slots(lay.irow, n, lay.n_slots)
+    by_slot = ops.terminal_windows_packed_dest(ts, fr, tseg, tperm, slot_of, lay.n_slots).cpu().numpy()
+    irow = lay.irow[: lay.n_slots].cpu().numpy()
+    valid = irow >= 0
+    np.testing.assert_array_equal(by_slot[valid], by_row[irow[valid]])
+    assert sorted(slot_of.cpu().numpy().tolist()) == sorted(np.nonzero(valid)[0].tolist())

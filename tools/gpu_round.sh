@@ -16,3 +16,4 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
 echo "rocprof exit $?"
+python tools/trace_summary.py gpurun_out/prof_$TAG gpurun_out/prof_$TAG/trace_summary.csv || true

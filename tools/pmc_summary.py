@@ -5,6 +5,7 @@ reads half the bytes of wide coalesced streaming reads, so traffic = 2*FETCH + W
 (upper estimate for the read side; ratios between variants are unaffected).
 
 usage: python tools/pmc_summary.py gpurun_out/pmc_r7 [kernel-substring ...]
+       python tools/pmc_summary.py --json out.json gpurun_out/pmc_r7   (per-kernel means)
 (reads <prefix>a ... <prefix>d directories)
 """
 import collections
@@ -27,7 +28,27 @@ def load(prefix):
     return per
 
 
+def to_json(prefix, out):
+    """{kernel: {counter: mean, ..., hbm_bytes_per_dispatch}} for bench.py's roofline.traffic"""
+    import json
+
+    per = load(prefix)
+    res = {}
+    for name, ctr in per.items():
+        mean = {k: sum(v) / len(v) for k, v in ctr.items()}
+        if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+            mean["hbm_bytes_per_dispatch"] = (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
+        res[name] = mean
+    with open(out, "w") as f:
+        json.dump({"source": prefix, "correction": "FETCH_SIZE, WRITE_SIZE in KiB; HBM bytes = "
+                   "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE reads half of wide streaming "
+                   "reads, MI355X_MICROARCH.md HBM section)", "kernels": res}, f, indent=1)
+
+
 def main():
+    if sys.argv[1] == "--json":
+        to_json(sys.argv[3], sys.argv[2])
+        return
     prefix = sys.argv[1]
     keys = sys.argv[2:] or ["k_forest_chunk", "k_customer", "k_zfill", "k_interleave", "k_terminal"]
     per = load(prefix)
