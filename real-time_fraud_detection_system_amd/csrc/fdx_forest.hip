@@ -527,7 +527,7 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 struct Variant {
     int block, rows, group, tile, rank, p16 = 0, pipe = 0;
 };
-constexpr int kDefaultRankVariant = 34;  // measured fastest on MI355X (r01: G=6 walks per lane, pipelined)
+constexpr int kDefaultRankVariant = 41;  // measured fastest on MI355X (r01: G=6 walks per lane, pipelined, paired waits)
 constexpr Variant kVariants[] = {
     {512, 1, 4, 0, 0},  {1024, 1, 4, 0, 0}, {512, 2, 4, 0, 0},  {512, 2, 2, 0, 0},  {256, 2, 4, 0, 0},
     {1024, 1, 3, 0, 0}, {512, 1, 3, 0, 0},  {768, 1, 3, 0, 0},  {768, 1, 4, 0, 0},  {1024, 1, 2, 0, 0},
@@ -540,7 +540,12 @@ constexpr Variant kVariants[] = {
     {1024, 2, 3, 0, 1, 1}, {1024, 2, 4, 0, 1, 1}, {1024, 2, 5, 0, 1, 1}, {512, 4, 3, 0, 1, 1}, {1024, 2, 2, 0, 1, 1},
     // + software-pipelined walk (each chain's next LDS read issued as soon as it can be): 31..
     {1024, 2, 3, 0, 1, 1, 1}, {1024, 2, 4, 0, 1, 1, 1}, {1024, 2, 5, 0, 1, 1, 1}, {1024, 1, 6, 0, 1, 0, 1},
-    {1024, 1, 4, 0, 1, 1, 1}};
+    {1024, 1, 4, 0, 1, 1, 1},
+    // 36.. pipelined shape sweep
+    {1024, 1, 6, 0, 1, 1, 1}, {1024, 1, 5, 0, 1, 0, 1}, {768, 1, 6, 0, 1, 0, 1}, {512, 2, 6, 0, 1, 0, 1},
+    {512, 2, 4, 0, 1, 0, 1},
+    // 41.. grouped waits (pipe = group width)
+    {1024, 1, 6, 0, 1, 0, 2}, {1024, 1, 6, 0, 1, 0, 3}, {1024, 1, 6, 0, 1, 0, 6}};
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -843,7 +848,11 @@ template <bool P16>
 __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
     return P16 ? lds16(lds, addr) : lds32(lds, addr);
 }
-template <bool P16, int K>
+// PW > 1: chains in groups of PW, the node reads of a group issued in reverse chain order
+// and its feature reads in forward order, so the first use in each group waits for the
+// group's last-issued read and one s_waitcnt covers the whole group (LDS reads of a wave
+// return in order): fewer issue slots per step.
+template <bool P16, int K, int PW>
 __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                                uint32_t (&nd)[K], int depth) {
     uint32_t x[K];
@@ -851,13 +860,19 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
     for (int k = 0; k < K; ++k) x[k] = rank_x<P16>(lds, (nd[k] & 0xF000u) | lane_base[k]);
     auto step = [&]() {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
-            uint32_t st;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
-            asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %0"
-                : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
-            nd[k] = lds32(lds, pa[k]);
-            __builtin_amdgcn_sched_barrier(0);
+        for (int g = 0; g < K; g += PW) {
+#pragma unroll
+            for (int j = PW - 1; j >= 0; --j) {
+                const int k = g + j;
+                if (k < K) {
+                    const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
+                    uint32_t st;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
+                    asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %0"
+                        : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
+                    nd[k] = lds32(lds, pa[k]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -877,7 +892,7 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
     for (; d < depth; ++d) step();
 }
 
-template <int R, int GG, bool P16, bool PIPE>
+template <int R, int GG, bool P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
                                            int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
@@ -900,7 +915,7 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
     if (any_nan)
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
     else if (PIPE)
-        rank_walk_pipe<P16, K>(lds, lane_base, pa, nd, dmax);
+        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
     else
         rank_walk<false, P16, K>(lds, lane_base, pa, nd, dmax, ml);
 }
@@ -945,7 +960,7 @@ __device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int6
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-template <int BLOCK, int R, int G, bool P16, bool PIPE>
+template <int BLOCK, int R, int G, bool P16, int PIPE>
 __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
@@ -1731,7 +1746,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
 #define FDX_LAUNCH_RANK(B, R, G, P, ...)                                                                      \
     do {                                                                                                      \
         const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), F->n_cu);      \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0 != 0>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
                            (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
                            F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last);     \
     } while (0)
@@ -1755,6 +1770,14 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                     case 33: FDX_LAUNCH_RANK(1024, 2, 5, true, 1); break;
                     case 34: FDX_LAUNCH_RANK(1024, 1, 6, false, 1); break;
                     case 35: FDX_LAUNCH_RANK(1024, 1, 4, true, 1); break;
+                    case 36: FDX_LAUNCH_RANK(1024, 1, 6, true, 1); break;
+                    case 37: FDX_LAUNCH_RANK(1024, 1, 5, false, 1); break;
+                    case 38: FDX_LAUNCH_RANK(768, 1, 6, false, 1); break;
+                    case 39: FDX_LAUNCH_RANK(512, 2, 6, false, 1); break;
+                    case 40: FDX_LAUNCH_RANK(512, 2, 4, false, 1); break;
+                    case 41: FDX_LAUNCH_RANK(1024, 1, 6, false, 2); break;
+                    case 42: FDX_LAUNCH_RANK(1024, 1, 6, false, 3); break;
+                    case 43: FDX_LAUNCH_RANK(1024, 1, 6, false, 6); break;
                     default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK
