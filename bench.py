@@ -292,9 +292,9 @@ def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
     mark("start")
     cperm, cseg, _ = ops.rekey(cust, args.customers)
     mark("rekey_customer")
-    lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
+    lay = ops.customer_layout(cseg, cperm, ts, amt, 3, windows_days=(1, 7, 30))
     mark("customer_layout")
-    inb, isum = ops.customer_windows_interleaved(lay, cseg)
+    inb, isum = ops.customer_windows_walk(lay, cseg)
     mark("customer_windows")
     tperm, tseg, _ = ops.rekey(term, args.terminals)
     mark("rekey_terminal")

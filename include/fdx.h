@@ -85,6 +85,23 @@ int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *
                         int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
                         int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *workspace_d,
                         size_t workspace_bytes, void *stream);
+/* fdx_customer_layout that also writes every row's window starts (pandas' variable-window
+ * start: the first row j of the segment with ts_j > ts_t - window_ns[w], closed='right'),
+ * computed in the same kernel from the freshly gathered timestamps, segment-contiguous:
+ * row t of segment l of group g at starts_d[w * n_slots + goff_d[g] + l * Lg + t] (Lg = the
+ * group's longest segment; starts_d: room for n_windows * max_slots int32).  Follow with
+ * fdx_customer_windows_walk. */
+int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                               const int64_t *ts_d, const double *amount_d, const int64_t *window_ns,
+                               int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
+                               double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
+                               int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes, void *stream);
+/* The sequential half of fdx_customer_windows_interleaved over the starts of
+ * fdx_customer_layout_starts: nb_d / sum_d as there ([W][n_slots] by slot; n_windows >= 3,
+ * i.e. <= 21 segments per wave). */
+int fdx_customer_windows_walk(const double *iamt_d, const int64_t *seg_off_d, const int32_t *sorder_d,
+                              const uint32_t *goff_d, int64_t n_seg, int64_t n_slots, int32_t n_windows,
+                              const int32_t *starts_d, int32_t *nb_d, double *sum_d, void *stream);
 /* fdx_customer_windows over that layout: nb_d / sum_d are [W][n_slots] indexed by slot, with
  * sum_d the rolling SUM (pandas roll_sum, bit-exact); the average is sum / nb (IEEE float64
  * division, done by the consumer -- fdx_forest_prepare_grouped with cust_val_is_sum = 1 --

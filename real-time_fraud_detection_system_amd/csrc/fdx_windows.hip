@@ -187,33 +187,77 @@ __global__ void k_group_slots(const int64_t *__restrict__ seg_off, const int32_t
 }
 
 // one block per group: slot (t, l) <- time-order row r = cperm[seg_off[s] + t]
+// STARTS: the block then also computes every row's window starts (pandas' variable-window
+// start, see k_customer_starts) -- one wave per segment, the segment's timestamps read back
+// from the just-written slots (L2) into LDS, binary searches in LDS -- written
+// segment-contiguous: starts[w * n_slots + goff[g] + l * Lg + t] (Lg = the group's longest
+// segment), so both this writer and k_customer_walk's per-lane reads are contiguous.
+constexpr int kStartLds = 1024;  // segment rows staged per wave for the start searches
+template <bool STARTS>
 __global__ void __launch_bounds__(256) k_interleave(
     const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder, const int32_t *__restrict__ cperm,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, const int64_t *__restrict__ ts,
     const double *__restrict__ amount, int64_t *__restrict__ its, double *__restrict__ iamt,
-    int32_t *__restrict__ irow) {
+    int32_t *__restrict__ irow, WinArgs win, int32_t n_win, int32_t *__restrict__ starts, int64_t n_slots) {
+    __shared__ int64_t s_ts[STARTS ? 4 : 1][STARTS ? kStartLds : 1];
     const int64_t g = blockIdx.x;
     const int rows_per_iter = blockDim.x / S;
     const int l = threadIdx.x % S, tt = threadIdx.x / S;
-    if (tt >= rows_per_iter) return;
-    const int64_t si = g * S + l;
-    const int64_t s = si < n_seg ? sorder[si] : -1;
-    const int64_t b = s >= 0 ? seg_off[s] : 0;
-    const int64_t L = s >= 0 ? seg_off[s + 1] - b : 0;
     const int64_t s0 = sorder[g * S];
     const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
     const int64_t base = goff[g];
-    for (int64_t t = tt; t < Lg; t += rows_per_iter) {
-        const int64_t slot = base + t * S + l;
-        if (t < L) {
-            const int32_t r = cperm[b + t];
-            its[slot] = ts[r];
-            iamt[slot] = amount[r];
-            irow[slot] = r;
-        } else {
-            its[slot] = 0;
-            iamt[slot] = 0.0;
-            irow[slot] = -1;
+    if (tt < rows_per_iter) {
+        const int64_t si = g * S + l;
+        const int64_t s = si < n_seg ? sorder[si] : -1;
+        const int64_t b = s >= 0 ? seg_off[s] : 0;
+        const int64_t L = s >= 0 ? seg_off[s + 1] - b : 0;
+        for (int64_t t = tt; t < Lg; t += rows_per_iter) {
+            const int64_t slot = base + t * S + l;
+            if (t < L) {
+                const int32_t r = cperm[b + t];
+                its[slot] = ts[r];
+                iamt[slot] = amount[r];
+                irow[slot] = r;
+            } else {
+                its[slot] = 0;
+                iamt[slot] = 0.0;
+                irow[slot] = -1;
+            }
+        }
+    }
+    if constexpr (STARTS) {
+        __threadfence_block();
+        __syncthreads();  // the block's slot writes are visible to the block (read back below)
+        const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+        int64_t *lts = s_ts[wv];
+        for (int ls = wv; ls < S; ls += (int)(blockDim.x / kWave)) {
+            const int64_t si = g * S + ls;
+            if (si >= n_seg) break;
+            const int64_t sg = sorder[si];
+            const int64_t L = seg_off[sg + 1] - seg_off[sg];
+            const int64_t *gts = its + base + ls;  // row t: gts[t * S]
+            const bool in_lds = L <= kStartLds;
+            if (in_lds)
+                for (int64_t t = lane; t < L; t += kWave) lts[t] = __builtin_nontemporal_load(gts + t * S);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int64_t t = lane; t < L; t += kWave) {
+                const int64_t tv = in_lds ? lts[t] : __builtin_nontemporal_load(gts + t * S);
+                for (int w = 0; w < n_win; ++w) {
+                    const int64_t bound = tv - win.w[w];
+                    int64_t a = 0, e = t;  // first k in [0, t] with ts_k > bound (k = t qualifies)
+                    while (a < e) {
+                        const int64_t m = (a + e) >> 1;
+                        const int64_t x = in_lds ? lts[m] : __builtin_nontemporal_load(gts + m * S);
+                        if (x > bound) e = m; else a = m + 1;
+                    }
+                    starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = (int32_t)a;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
 }
@@ -442,11 +486,13 @@ __global__ void __launch_bounds__(256) k_customer_starts(
     }
 }
 
+// starts == nullptr: the starts are in nb_out (k_customer_starts, slot layout) and are
+// overwritten by the counts; else segment-contiguous (k_interleave<true>).
 template <int S_MAX, int kRing>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
-    int32_t *__restrict__ nb_out, double *__restrict__ sum_out) {
+    int32_t *__restrict__ nb_out, double *__restrict__ sum_out, const int32_t *__restrict__ starts) {
     static_assert((kRing & (kRing - 1)) == 0 && kRing % kChunk == 0, "power-of-two ring of whole chunks");
     constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;  // chunk elements per lane
     constexpr int kRingEl = kRing * S_MAX + kWave;             // + one miss slot per lane
@@ -474,9 +520,16 @@ __global__ void __launch_bounds__(64) k_customer_walk(
             const int e = lane + j * kWave;
             if (e < n_el) pam[j] = iamt[src0 + e];
         }
+        if (starts) {
+            const int32_t *sp = starts + (int64_t)wi * n_slots + gbase + (int64_t)l * Lg + t0;
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j)
-            if (t0 + j < L) pst[j] = nb[(int64_t)(t0 + j) * S];
+            for (int j = 0; j < kChunk; ++j)
+                if (t0 + j < L) pst[j] = sp[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j)
+                if (t0 + j < L) pst[j] = nb[(int64_t)(t0 + j) * S];
+        }
     };
     auto commit = [&](int32_t t0) {
         const int n_el = min(kChunk, Lg - t0) * S;
@@ -1007,11 +1060,11 @@ extern "C" size_t fdx_customer_layout_workspace_size(int64_t n_seg) {
            fdx_exclusive_scan_u32_workspace_size(n_seg + 1) + 256;
 }
 
-extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
-                                   const int64_t *ts_d, const double *amount_d, int32_t n_windows,
-                                   int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
-                                   int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
-                                   size_t ws_bytes, void *stream) {
+static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                           const int64_t *ts_d, const double *amount_d, int32_t n_windows,
+                           int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                           int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                           size_t ws_bytes, void *stream, const WinArgs *wa, int32_t *starts_d) {
     FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64, "bad argument");
     FDX_REQUIRE(seg_off_d && cperm_d && ts_d && amount_d && sorder_d && goff_d && its_d && iamt_d && irow_d &&
                     n_slots_h && ws,
@@ -1047,9 +1100,53 @@ extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, cons
         set_error("interleaved layout needs %u slots > max_slots %lld", total, (long long)max_slots);
         return FDX_E_WORKSPACE;
     }
-    hipLaunchKernelGGL(k_interleave, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d, cperm_d,
-                       goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d);
+    if (starts_d)
+        hipLaunchKernelGGL(k_interleave<true>, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
+                           cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
+                           (int64_t)total);
+    else
+        hipLaunchKernelGGL(k_interleave<false>, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
+                           cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, WinArgs{}, n_windows,
+                           (int32_t *)nullptr, (int64_t)total);
     FDX_LAUNCHED("k_interleave");
+    return FDX_OK;
+}
+
+extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                   const int64_t *ts_d, const double *amount_d, int32_t n_windows,
+                                   int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                                   int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                                   size_t ws_bytes, void *stream) {
+    return customer_layout(seg_off_d, n_seg, cperm_d, ts_d, amount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
+                           irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, nullptr, nullptr);
+}
+
+extern "C" int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                          const int64_t *ts_d, const double *amount_d, const int64_t *window_ns,
+                                          int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
+                                          double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
+                                          int64_t *n_slots_h, void *ws, size_t ws_bytes, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(starts_d, "null pointer");
+    return customer_layout(seg_off_d, n_seg, cperm_d, ts_d, amount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
+                           irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, &wa, starts_d);
+}
+
+extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *seg_off_d, const int32_t *sorder_d,
+                                         const uint32_t *goff_d, int64_t n_seg, int64_t n_slots, int32_t n_windows,
+                                         const int32_t *starts_d, int32_t *nb_d, double *sum_d, void *stream) {
+    FDX_REQUIRE(n_seg >= 0 && n_slots >= 0, "negative size");
+    FDX_REQUIRE(n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad n_windows");
+    if (n_seg == 0) return FDX_OK;
+    FDX_REQUIRE(iamt_d && seg_off_d && sorder_d && goff_d && starts_d && nb_d && sum_d, "null pointer");
+    const int32_t S = kWave / n_windows;
+    FDX_REQUIRE(S <= 21, "the walk kernel is built for <= 21 segments per wave (>= 3 windows)");
+    const int64_t n_groups = ceil_div(n_seg, S);
+    hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), iamt_d,
+                       seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d);
+    FDX_LAUNCHED("k_customer_walk");
     return FDX_OK;
 }
 
@@ -1088,10 +1185,12 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
         FDX_LAUNCHED("k_customer_starts");
         if (walk_env == 256)
             hipLaunchKernelGGL((k_customer_walk<21, 256>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
-                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d);
+                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d,
+                               (const int32_t *)nullptr);
         else
             hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
-                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d);
+                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d,
+                               (const int32_t *)nullptr);
         FDX_LAUNCHED("k_customer_walk");
         return FDX_OK;
     }

@@ -50,6 +50,9 @@ SIGNATURES = {
     "fdx_assemble_features": (ctypes.c_int, [c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_i64, P]),
     "fdx_customer_layout_workspace_size": (c_sz, [c_i64]),
     "fdx_customer_layout": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),
+    "fdx_customer_layout_starts": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, P, P, P, P, c_i64, P, P, c_sz,
+                                                  P]),
+    "fdx_customer_windows_walk": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i32, P, P, P, P]),
     "fdx_customer_windows_interleaved": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_exclusive_scan_u32_workspace_size": (c_sz, [c_i64]),
     "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),

@@ -161,13 +161,14 @@ class ShardedPipeline:
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         cperm, cseg, _ = ops.rekey(cust, n_local)
-        lay = ops.customer_layout(cseg, cperm, ts, amount, W, None, p._slots_hint)  # (host sync on main)
+        lay = ops.customer_layout(cseg, cperm, ts, amount, W, None, p._slots_hint,
+                                  p.windows_days)  # (host sync on main)
         p._slots_hint = lay.its.numel()
         with torch.cuda.stream(side):
             back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
                                               self.n_terminals_total, p.windows_days, p.delay_days, self.group)
             sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
-        inb, isum = ops.customer_windows_interleaved(lay, cseg, p.windows_days)
+        inb, isum = ops.customer_windows_walk(lay, cseg)
         main.wait_stream(side)
         back.record_stream(main)
         sinv.record_stream(main)

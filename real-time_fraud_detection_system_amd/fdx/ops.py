@@ -161,13 +161,18 @@ def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30
 
 
 class CustomerLayout:
-    """The interleaved (lane-major) customer layout of the scoring pipeline (fdx.h)."""
+    """The interleaved (lane-major) customer layout of the scoring pipeline (fdx.h).
+    starts: the window starts [W * max_slots] int32 when built by customer_layout(windows_days=...)."""
 
-    def __init__(self, sorder, goff, its, iamt, irow, n_slots):
+    def __init__(self, sorder, goff, its, iamt, irow, n_slots, starts=None, windows_days=None):
         self.sorder, self.goff, self.its, self.iamt, self.irow, self.n_slots = sorder, goff, its, iamt, irow, n_slots
+        self.starts, self.windows_days = starts, windows_days
 
 
-def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, _slots_hint=None) -> CustomerLayout:
+def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, _slots_hint=None,
+                    windows_days=None) -> CustomerLayout:
+    """windows_days: also compute the window starts in the layout kernel (for
+    customer_windows_walk)."""
     _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(amount, torch.float64, "amount")
     n_seg = seg_off.numel() - 1
@@ -184,14 +189,41 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
         iamt = torch.empty(max_slots, dtype=torch.float64, device=dev)
         irow = torch.empty(max_slots, dtype=torch.int32, device=dev)
         ns = ctypes.c_int64(0)
-        rc = L.fdx_customer_layout(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount), int(n_windows),
-                                   _ptr(sorder), _ptr(goff), _ptr(its), _ptr(iamt), _ptr(irow), max_slots,
-                                   ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
+        if windows_days is None:
+            starts = None
+            rc = L.fdx_customer_layout(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount), int(n_windows),
+                                       _ptr(sorder), _ptr(goff), _ptr(its), _ptr(iamt), _ptr(irow), max_slots,
+                                       ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
+        else:
+            if len(windows_days) != int(n_windows):
+                raise FdxError("windows_days must have n_windows entries")
+            starts = torch.empty(int(n_windows) * max_slots, dtype=torch.int32, device=dev)
+            rc = L.fdx_customer_layout_starts(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount),
+                                              _win_ns(windows_days), int(n_windows), _ptr(sorder), _ptr(goff),
+                                              _ptr(its), _ptr(iamt), _ptr(irow), _ptr(starts), max_slots,
+                                              ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
         if rc == -4 and ns.value > max_slots:
             max_slots = ns.value
             continue
         check(rc, "fdx_customer_layout")
-        return CustomerLayout(sorder, goff, its, iamt, irow, ns.value)
+        return CustomerLayout(sorder, goff, its, iamt, irow, ns.value, starts,
+                              None if windows_days is None else tuple(windows_days))
+
+
+def customer_windows_walk(lay: CustomerLayout, seg_off, stream=None):
+    """The windows of a layout built with windows_days: (nb int32 [W, n_slots], rolling SUM
+    float64 [W, n_slots]) indexed by slot."""
+    if lay.starts is None:
+        raise FdxError("layout was built without window starts")
+    W = len(lay.windows_days)
+    dev = lay.its.device
+    nb = torch.empty((W, lay.n_slots), dtype=torch.int32, device=dev)
+    sm = torch.empty((W, lay.n_slots), dtype=torch.float64, device=dev)
+    check(_lib.load().fdx_customer_windows_walk(_ptr(lay.iamt), _ptr(seg_off), _ptr(lay.sorder), _ptr(lay.goff),
+                                                seg_off.numel() - 1, lay.n_slots, W, _ptr(lay.starts), _ptr(nb),
+                                                _ptr(sm), _s(stream)),
+          "fdx_customer_windows_walk")
+    return nb, sm
 
 
 def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 7, 30), stream=None):

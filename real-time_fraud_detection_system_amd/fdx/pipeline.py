@@ -111,10 +111,10 @@ class FraudPipeline:
         in input row order."""
         W = len(self.windows_days)
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
-        lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint)
+        lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint, self.windows_days)
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
-        inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, stream)
+        inb, isum = ops.customer_windows_walk(lay, cseg, stream)
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
         # count records in input row order (the kernel reads ts/fraud through tperm).  Measured
         # (r01): writing them at their scoring slots instead (terminal_windows_packed_dest +

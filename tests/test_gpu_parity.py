@@ -323,3 +323,28 @@ def test_terminal_records_at_slots(dev):
     valid = irow >= 0
     np.testing.assert_array_equal(by_slot[valid], by_row[irow[valid]])
     assert sorted(slot_of.cpu().numpy().tolist()) == sorted(np.nonzero(valid)[0].tolist())
+
+
+def test_layout_starts_walk_equals_interleaved(dev):
+    """fdx_customer_layout_starts + fdx_customer_windows_walk (window starts found in the
+    layout kernel) == fdx_customer_windows_interleaved, bit for bit, incl. a segment longer
+    than the 1,024-row LDS stage of the start search."""
+    from fdx import synth
+
+    d = synth.generate(n_customers=400, n_terminals=500, nb_days=120, seed=31)
+    # one very busy customer: > 1024 rows in its segment
+    busy = np.nonzero(d["customer"] < 40)[0]
+    cust = d["customer"].copy()
+    cust[busy] = 0
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    ts, c, amt = T(d["ts"], torch.int64), T(cust, torch.int32), T(d["amount"], torch.float64)
+    cperm, cseg, _ = ops.rekey(c, 400)
+    assert int((cseg[1:] - cseg[:-1]).max()) > 1024
+    lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
+    nb_ref, sm_ref = ops.customer_windows_interleaved(lay, cseg)
+    lay2 = ops.customer_layout(cseg, cperm, ts, amt, 3, windows_days=(1, 7, 30))
+    nb, sm = ops.customer_windows_walk(lay2, cseg)
+    n = lay.n_slots
+    valid = (lay.irow[:n] >= 0).cpu().numpy()
+    np.testing.assert_array_equal(nb.cpu().numpy()[:, valid], nb_ref.cpu().numpy()[:, valid])
+    np.testing.assert_array_equal(sm.cpu().numpy()[:, valid], sm_ref.cpu().numpy()[:, valid])
