@@ -362,6 +362,34 @@ int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, 
 int fdx_forest_traverse_perm(fdx_forest forest, int64_t n, double *proba_d, const int32_t *out_perm_d,
                              int32_t *leaf_d, void *workspace_d, size_t workspace_bytes, void *stream);
 
+/* ---- §8(f): callers and data formats either side of the path (csrc/fdx_aux.hip) ----------
+ * f-1 feature snapshots for the serving tables (feature_transformation.ipynb:2914-2918,
+ * :3606-3635, :4182).  Over a STABLE grouping (perm_d = fdx_rekey perm, seg_off_d) of the
+ * frame's rows -- i.e. frame order inside each segment; perm_d NULL = rows already grouped:
+ *   fdx_segment_latest:         out_row_d[k] = the first row of segment k holding its maximum
+ *                               ts (pandas groupby(key).TX_DATETIME.idxmax()), -1 if empty;
+ *   fdx_segment_first_in_range: out_row_d[k] = the first row of segment k with
+ *                               t_lo <= ts < t_hi (date filter + drop_duplicates keep='first'),
+ *                               -1 if none. */
+int fdx_segment_latest(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d, int64_t n_seg,
+                       int32_t *out_row_d, void *stream);
+int fdx_segment_first_in_range(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d,
+                               int64_t n_seg, int64_t t_lo, int64_t t_hi, int32_t *out_row_d, void *stream);
+/* f-2 Debezium CDC records of a micro-batch (pyspark/scripts/kafka_s3_sink_transactions.py):
+ *   fdx_cdc_decode: tx_amount bytes (record i = bytes_d[offsets_d[i] .. offsets_d[i+1]),
+ *     big-endian two's complement, 1..8 bytes; :64-71) -> unscaled_d (int64 cents) and
+ *     amount_d (= unscaled / 100.0, the double of Decimal(unscaled) / 10**2); tx_datetime
+ *     microseconds us_d -> ts_ns_d = whole seconds as from_unixtime(us / 1000000) (:167),
+ *     in ns.  Any output may be NULL; *bad_d = 1 if a record has 0 or > 8 bytes.
+ *   fdx_dedup_latest: ROW_NUMBER() OVER (PARTITION BY tx_id ORDER BY timestamp DESC) = 1
+ *     (:180): keep_d[i] = 1 for the record with the largest Kafka timestamp of each key (ties:
+ *     the last in batch order), 0 otherwise; sorted_perm_d = a STABLE argsort of key_d
+ *     (fdx_argsort_i64). */
+int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, const int64_t *us_d, int64_t n,
+                   int64_t *unscaled_d, double *amount_d, int64_t *ts_ns_d, int32_t *bad_d, void *stream);
+int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d, int64_t n,
+                     uint8_t *keep_d, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

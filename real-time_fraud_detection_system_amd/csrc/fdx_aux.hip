@@ -1,0 +1,189 @@
+// fdx_aux.hip -- SURVEY.md §8(f): the callers and data formats either side of the hot path.
+//
+//   f-1 feature-snapshot export (the serving tables the streaming job LEFT JOINs):
+//       latest row per terminal   feature_transformation.ipynb:2914-2918
+//           df.loc[df.groupby('TERMINAL_ID').TX_DATETIME.idxmax()]
+//       customer row of a date    :3606-3635, :4182
+//           df[df.tx_datetime.dt.date == d].drop_duplicates(subset=['customer_id'])  (keep='first')
+//   f-2 Debezium CDC decode + dedup of a micro-batch
+//       pyspark/scripts/kafka_s3_sink_transactions.py:64-71  tx_amount: big-endian two's-
+//           complement unscaled integer, scale 2 (Decimal(unscaled) / 10**2)
+//       :167  to_timestamp(from_unixtime(tx_datetime / 1000000))  (microseconds -> whole seconds)
+//       :180  ROW_NUMBER() OVER (PARTITION BY tx_id ORDER BY timestamp DESC) = 1
+//
+// All HBM-bound byte/integer work: one wave per segment (reductions) or one lane per record.
+#include "fdx_internal.h"
+
+namespace fdx {
+namespace {
+
+// (ts, pos) lexicographic "better" for idxmax: larger ts, then earlier position
+__device__ __forceinline__ bool better_latest(int64_t ta, int64_t pa, int64_t tb, int64_t pb) {
+    return ta > tb || (ta == tb && pa < pb);
+}
+
+// One wave per segment: the first position (segment order = frame order, stable grouping)
+// holding the segment's maximum timestamp -> out_row[k] = perm[pos] (-1: empty segment).
+__global__ void __launch_bounds__(256) k_segment_latest(const int64_t *__restrict__ ts,
+                                                        const int32_t *__restrict__ perm,
+                                                        const int64_t *__restrict__ seg_off, int64_t n_seg,
+                                                        int32_t *__restrict__ out_row) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / kWave);
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; k < n_seg; k += nw) {
+        const int64_t b = seg_off[k], e = seg_off[k + 1];
+        int64_t bt = INT64_MIN, bp = INT64_MAX;
+        for (int64_t p = b + lane; p < e; p += kWave) {
+            const int64_t t = ts[perm ? perm[p] : p];
+            if (better_latest(t, p, bt, bp)) {
+                bt = t;
+                bp = p;
+            }
+        }
+#pragma unroll
+        for (int d = kWave / 2; d > 0; d >>= 1) {
+            const int64_t ot = __shfl_xor(bt, d, kWave), op = __shfl_xor(bp, d, kWave);
+            if (better_latest(ot, op, bt, bp)) {
+                bt = ot;
+                bp = op;
+            }
+        }
+        if (lane == 0) out_row[k] = e > b ? (perm ? perm[bp] : (int32_t)bp) : -1;
+    }
+}
+
+// One wave per segment: the first position with t_lo <= ts < t_hi (-1: none).
+__global__ void __launch_bounds__(256) k_segment_first_in_range(const int64_t *__restrict__ ts,
+                                                                const int32_t *__restrict__ perm,
+                                                                const int64_t *__restrict__ seg_off, int64_t n_seg,
+                                                                int64_t t_lo, int64_t t_hi,
+                                                                int32_t *__restrict__ out_row) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / kWave);
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave; k < n_seg; k += nw) {
+        const int64_t b = seg_off[k], e = seg_off[k + 1];
+        int64_t first = INT64_MAX;
+        for (int64_t c = b; c < e && first == INT64_MAX; c += kWave) {  // chunks in order: stop at a hit
+            const int64_t p = c + lane;
+            bool hit = false;
+            if (p < e) {
+                const int64_t t = ts[perm ? perm[p] : p];
+                hit = t >= t_lo && t < t_hi;
+            }
+            const uint64_t m = __ballot(hit);
+            if (m) first = c + __ffsll((long long)m) - 1;
+        }
+        if (lane == 0) out_row[k] = first == INT64_MAX ? -1 : (perm ? perm[first] : (int32_t)first);
+    }
+}
+
+// Debezium DECIMAL(10,2) bytes -> unscaled int64 (big-endian two's complement, 1..8 bytes),
+// amount = unscaled / 100.0 (the IEEE-correctly-rounded double of Decimal(unscaled) / 100,
+// as float(Decimal) gives); microseconds -> whole seconds as Spark's
+// from_unixtime(us / 1000000) (double division, truncation) -> ns.
+__global__ void __launch_bounds__(256) k_cdc_decode(const uint8_t *__restrict__ bytes,
+                                                    const int64_t *__restrict__ offsets, const int64_t *__restrict__ us,
+                                                    int64_t n, int64_t *__restrict__ unscaled,
+                                                    double *__restrict__ amount, int64_t *__restrict__ ts_ns,
+                                                    int32_t *__restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (bytes && offsets) {
+            const int64_t b = offsets[i], e = offsets[i + 1];
+            const int64_t len = e - b;
+            int64_t v = 0;
+            if (len >= 1 && len <= 8) {
+                uint64_t u = 0;
+                for (int64_t j = b; j < e; ++j) u = (u << 8) | bytes[j];
+                const int sh = 64 - 8 * (int)len;  // sign-extend from the top byte
+                v = (int64_t)(u << sh) >> sh;
+            } else {
+                *bad = 1;
+            }
+            if (unscaled) unscaled[i] = v;
+            if (amount) amount[i] = (double)v / 100.0;
+        }
+        if (us && ts_ns) {
+            const double q = (double)us[i] / 1000000.0;
+            ts_ns[i] = (int64_t)q * 1000000000LL;
+        }
+    }
+}
+
+// Latest record per key over a stable argsort of the keys (sorted position i -> record
+// perm[i]): the run head scans its run and keeps the record with the largest Kafka
+// timestamp (ties: the last one in batch order).  keep[record] = 1 for the kept ones (the
+// host zeroes keep first).
+__global__ void __launch_bounds__(256) k_dedup_latest(const int64_t *__restrict__ key, const int64_t *__restrict__ kts,
+                                                      const int32_t *__restrict__ perm, int64_t n,
+                                                      uint8_t *__restrict__ keep) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = perm[i];
+        const int64_t k = key[r];
+        if (i > 0 && key[perm[i - 1]] == k) continue;  // not a run head
+        int32_t best = r;
+        int64_t bt = kts[r];
+        for (int64_t j = i + 1; j < n; ++j) {
+            const int32_t q = perm[j];
+            if (key[q] != k) break;
+            if (kts[q] >= bt) {  // stable sort: q is later in batch order than best
+                bt = kts[q];
+                best = q;
+            }
+        }
+        keep[best] = 1;
+    }
+}
+
+}  // namespace
+}  // namespace fdx
+
+using namespace fdx;
+
+extern "C" int fdx_segment_latest(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d, int64_t n_seg,
+                                  int32_t *out_row_d, void *stream) {
+    FDX_REQUIRE(n_seg >= 0, "negative size");
+    if (n_seg == 0) return FDX_OK;
+    FDX_REQUIRE(ts_d && seg_off_d && out_row_d, "null pointer");
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg * kWave, 256), 256 * 16);
+    hipLaunchKernelGGL(k_segment_latest, dim3(grid), dim3(256), 0, as_stream(stream), ts_d, perm_d, seg_off_d, n_seg,
+                       out_row_d);
+    FDX_LAUNCHED("k_segment_latest");
+    return FDX_OK;
+}
+
+extern "C" int fdx_segment_first_in_range(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d,
+                                          int64_t n_seg, int64_t t_lo, int64_t t_hi, int32_t *out_row_d,
+                                          void *stream) {
+    FDX_REQUIRE(n_seg >= 0, "negative size");
+    if (n_seg == 0) return FDX_OK;
+    FDX_REQUIRE(ts_d && seg_off_d && out_row_d, "null pointer");
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg * kWave, 256), 256 * 16);
+    hipLaunchKernelGGL(k_segment_first_in_range, dim3(grid), dim3(256), 0, as_stream(stream), ts_d, perm_d, seg_off_d,
+                       n_seg, t_lo, t_hi, out_row_d);
+    FDX_LAUNCHED("k_segment_first_in_range");
+    return FDX_OK;
+}
+
+extern "C" int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, const int64_t *us_d, int64_t n,
+                              int64_t *unscaled_d, double *amount_d, int64_t *ts_ns_d, int32_t *bad_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "negative size");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(bad_d, "null pointer");
+    FDX_REQUIRE((bytes_d != nullptr) == (offsets_d != nullptr), "bytes and offsets go together");
+    hipLaunchKernelGGL(k_cdc_decode, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), bytes_d, offsets_d,
+                       us_d, n, unscaled_d, amount_d, ts_ns_d, bad_d);
+    FDX_LAUNCHED("k_cdc_decode");
+    return FDX_OK;
+}
+
+extern "C" int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d,
+                                int64_t n, uint8_t *keep_d, void *stream) {
+    FDX_REQUIRE(n >= 0, "negative size");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(key_d && kafka_ts_d && sorted_perm_d && keep_d, "null pointer");
+    FDX_HIP(hipMemsetAsync(keep_d, 0, (size_t)n, as_stream(stream)));
+    hipLaunchKernelGGL(k_dedup_latest, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), key_d, kafka_ts_d,
+                       sorted_perm_d, n, keep_d);
+    FDX_LAUNCHED("k_dedup_latest");
+    return FDX_OK;
+}

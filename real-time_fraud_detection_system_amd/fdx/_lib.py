@@ -60,6 +60,10 @@ SIGNATURES = {
     "fdx_terminal_windows_packed_unsorted": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
     "fdx_terminal_windows_packed_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
     "fdx_invert_slots": (ctypes.c_int, [P, c_i64, P, c_i64, P]),
+    "fdx_segment_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
+    "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
+    "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),
+    "fdx_dedup_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
     "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),
     "fdx_rekey": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, c_sz, P]),
