@@ -389,6 +389,28 @@ int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, const int64
                    int64_t *unscaled_d, double *amount_d, int64_t *ts_ns_d, int32_t *bad_d, void *stream);
 int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d, int64_t n,
                      uint8_t *keep_d, void *stream);
+/* f-4 delay-aware split and Card-Precision@k (shared_functions.py:133-188, :352-411).
+ * fdx_train_test_split: train_d[i] = t_lo <= ts_d[i] < t_hi; test_d[i] = the row is on test
+ *   day d = day_d[i] - (min train day + delta_train + delta_delay), 0 <= d < delta_test, and
+ *   its customer (dense id < n_cust) has no fraud among the train rows nor on the days
+ *   min train day + delta_train - 1 + [0, d] (the reference's growing known-defrauded set).
+ *   workspace: n_cust * 5 + 64 bytes; *day_min_h = the min train day (host; one sync).
+ * fdx_card_precision_top_k: for each day days_h[k] (ascending), customers max(prediction),
+ *   max(TX_FRAUD) over the day's rows of customers not yet detected; the top_k customers by
+ *   (prediction desc, customer asc) that are compromised are detected (carried over when
+ *   remove_detected); nb_compromised_h[k] = compromised customers of the day, cp_h[k] =
+ *   detected / top_k.  Predictions must be >= 0.  The reference sorts with pandas' default
+ *   (unstable) quicksort: equal predictions straddling the k-th place may order differently.
+ *   workspace: fdx_card_precision_workspace_size(n_cust); one host sync per day. */
+int fdx_train_test_split(const int64_t *ts_d, const int32_t *day_d, const int32_t *cust_d, const uint8_t *fraud_d,
+                         int64_t n, int32_t n_cust, int64_t t_lo, int64_t t_hi, int32_t delta_train,
+                         int32_t delta_delay, int32_t delta_test, uint8_t *train_d, uint8_t *test_d,
+                         void *workspace_d, size_t workspace_bytes, int32_t *day_min_h, void *stream);
+size_t fdx_card_precision_workspace_size(int32_t n_cust);
+int fdx_card_precision_top_k(const int32_t *day_d, const int32_t *cust_d, const double *pred_d,
+                             const uint8_t *fraud_d, int64_t n, int32_t n_cust, const int32_t *days_h,
+                             int32_t n_days, int32_t top_k, int32_t remove_detected, int32_t *nb_compromised_h,
+                             double *cp_h, void *workspace_d, size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

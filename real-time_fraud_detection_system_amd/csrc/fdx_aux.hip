@@ -10,6 +10,9 @@
 //           complement unscaled integer, scale 2 (Decimal(unscaled) / 10**2)
 //       :167  to_timestamp(from_unixtime(tx_datetime / 1000000))  (microseconds -> whole seconds)
 //       :180  ROW_NUMBER() OVER (PARTITION BY tx_id ORDER BY timestamp DESC) = 1
+//   f-4 delay-aware train/test split and Card-Precision@k (model-quality parity on GPU outputs)
+//       shared_functions.py:133-188  get_train_test_set
+//       shared_functions.py:352-411  card_precision_top_k_day / card_precision_top_k
 //
 // All HBM-bound byte/integer work: one wave per segment (reductions) or one lane per record.
 #include "fdx_internal.h"
@@ -134,10 +137,167 @@ __global__ void __launch_bounds__(256) k_dedup_latest(const int64_t *__restrict_
     }
 }
 
+// ---------------------------------------------------------------- f-4: split, CP@k
+// get_train_test_set: train rows t_lo <= ts < t_hi; per customer: a fraud among the train
+// rows (train_fraud) and the first delay-period day index d' (TX_TIME_DAYS == day_base - 1
+// + d', 0 <= d' < delta_test) with a fraud (delay_first); test day d keeps a row of day
+// day_base + delta_delay + d iff its customer is known neither from training nor by day d.
+__global__ void __launch_bounds__(256) k_split_pass1(const int64_t *__restrict__ ts, const int32_t *__restrict__ day,
+                                                     const int32_t *__restrict__ cust, const uint8_t *__restrict__ fraud,
+                                                     int64_t n, int64_t t_lo, int64_t t_hi, int32_t *__restrict__ day_min,
+                                                     uint8_t *__restrict__ train) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const bool tr = ts[i] >= t_lo && ts[i] < t_hi;
+        train[i] = tr;
+        if (tr) atomicMin(day_min, day[i]);
+    }
+}
+__global__ void __launch_bounds__(256) k_split_pass2(const int32_t *__restrict__ day, const int32_t *__restrict__ cust,
+                                                     const uint8_t *__restrict__ fraud, const uint8_t *__restrict__ train,
+                                                     int64_t n, int32_t day_base, int32_t delta_test,
+                                                     uint8_t *__restrict__ train_fraud, int32_t *__restrict__ delay_first) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!fraud[i]) continue;
+        const int32_t c = cust[i];
+        if (train[i]) train_fraud[c] = 1;
+        const int32_t dp = day[i] - (day_base - 1);
+        if (dp >= 0 && dp < delta_test) atomicMin(&delay_first[c], dp);
+    }
+}
+__global__ void __launch_bounds__(256) k_split_pass3(const int32_t *__restrict__ day, const int32_t *__restrict__ cust,
+                                                     int64_t n, int32_t test_day0, int32_t delta_test,
+                                                     const uint8_t *__restrict__ train_fraud,
+                                                     const int32_t *__restrict__ delay_first, uint8_t *__restrict__ test) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t d = day[i] - test_day0;
+        const int32_t c = cust[i];
+        test[i] = d >= 0 && d < delta_test && !train_fraud[c] && delay_first[c] > d;
+    }
+}
+
+// card_precision_top_k_day over the rows of one day, customers not yet detected:
+// per customer max(prediction) (order-preserving u64 keys; predictions are >= 0) and max(label)
+__global__ void __launch_bounds__(256) k_cpk_day_max(const int32_t *__restrict__ day, const int32_t *__restrict__ cust,
+                                                     const double *__restrict__ pred, const uint8_t *__restrict__ fraud,
+                                                     int64_t n, int32_t d, const uint8_t *__restrict__ detected,
+                                                     unsigned long long *__restrict__ cmax, uint8_t *__restrict__ cfraud,
+                                                     uint8_t *__restrict__ present) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (day[i] != d) continue;
+        const int32_t c = cust[i];
+        if (detected[c]) continue;
+        present[c] = 1;
+        atomicMax(&cmax[c], (unsigned long long)__double_as_longlong(pred[i]));
+        if (fraud[i]) cfraud[c] = 1;
+    }
+}
+// rank of every present customer in (prediction desc, customer asc) order; the top k are
+// "detected" when compromised.  out[0] += compromised customers of the day, out[1] += top-k hits.
+__global__ void __launch_bounds__(256) k_cpk_day_topk(const unsigned long long *__restrict__ cmax,
+                                                      const uint8_t *__restrict__ cfraud,
+                                                      const uint8_t *__restrict__ present, int32_t n_cust,
+                                                      int32_t top_k, uint8_t *__restrict__ detected,
+                                                      int32_t *__restrict__ out) {
+    for (int32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n_cust; c += gridDim.x * blockDim.x) {
+        if (!present[c]) continue;
+        if (cfraud[c]) atomicAdd(&out[0], 1);
+        const unsigned long long v = cmax[c];
+        int32_t rank = 0;
+        for (int32_t o = 0; o < n_cust && rank < top_k; ++o)
+            if (present[o] && (cmax[o] > v || (cmax[o] == v && o < c))) ++rank;
+        if (rank < top_k && cfraud[c]) {
+            atomicAdd(&out[1], 1);
+            detected[c] = 1;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace fdx
 
 using namespace fdx;
+
+extern "C" int fdx_train_test_split(const int64_t *ts_d, const int32_t *day_d, const int32_t *cust_d,
+                                    const uint8_t *fraud_d, int64_t n, int32_t n_cust, int64_t t_lo, int64_t t_hi,
+                                    int32_t delta_train, int32_t delta_delay, int32_t delta_test, uint8_t *train_d,
+                                    uint8_t *test_d, void *workspace_d, size_t workspace_bytes, int32_t *day_min_h,
+                                    void *stream) {
+    FDX_REQUIRE(n >= 0 && n_cust >= 0 && delta_test >= 0, "bad argument");
+    FDX_REQUIRE(workspace_bytes >= (size_t)n_cust * 5 + 64, "workspace too small");
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(ts_d && day_d && cust_d && fraud_d && train_d && test_d && workspace_d && day_min_h, "null pointer");
+    hipStream_t st = as_stream(stream);
+    char *w = reinterpret_cast<char *>(workspace_d);
+    int32_t *day_min = reinterpret_cast<int32_t *>(w);
+    int32_t *delay_first = reinterpret_cast<int32_t *>(w + 64);
+    uint8_t *train_fraud = reinterpret_cast<uint8_t *>(w + 64 + (size_t)n_cust * 4);
+    const int32_t big = INT32_MAX;
+    FDX_HIP(hipMemcpyAsync(day_min, &big, 4, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemsetAsync(delay_first, 0x7F, (size_t)n_cust * 4, st));  // 0x7F7F7F7F: "never"
+    FDX_HIP(hipMemsetAsync(train_fraud, 0, (size_t)n_cust, st));
+    const unsigned grid = stream_grid(n, 256);
+    hipLaunchKernelGGL(k_split_pass1, dim3(grid), dim3(256), 0, st, ts_d, day_d, cust_d, fraud_d, n, t_lo, t_hi,
+                       day_min, train_d);
+    FDX_LAUNCHED("k_split_pass1");
+    FDX_HIP(hipMemcpyAsync(day_min_h, day_min, 4, hipMemcpyDeviceToHost, st));
+    FDX_HIP(hipStreamSynchronize(st));
+    if (*day_min_h == INT32_MAX) {  // empty training set: no test days either
+        FDX_HIP(hipMemsetAsync(test_d, 0, (size_t)n, st));
+        return FDX_OK;
+    }
+    const int32_t day_base = *day_min_h + delta_train;
+    hipLaunchKernelGGL(k_split_pass2, dim3(grid), dim3(256), 0, st, day_d, cust_d, fraud_d, train_d, n, day_base,
+                       delta_test, train_fraud, delay_first);
+    FDX_LAUNCHED("k_split_pass2");
+    hipLaunchKernelGGL(k_split_pass3, dim3(grid), dim3(256), 0, st, day_d, cust_d, n, day_base + delta_delay,
+                       delta_test, train_fraud, delay_first, test_d);
+    FDX_LAUNCHED("k_split_pass3");
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_card_precision_workspace_size(int32_t n_cust) {
+    return (size_t)(n_cust < 0 ? 0 : n_cust) * 12 + 256;
+}
+
+extern "C" int fdx_card_precision_top_k(const int32_t *day_d, const int32_t *cust_d, const double *pred_d,
+                                        const uint8_t *fraud_d, int64_t n, int32_t n_cust, const int32_t *days_h,
+                                        int32_t n_days, int32_t top_k, int32_t remove_detected,
+                                        int32_t *nb_compromised_h, double *cp_h, void *workspace_d,
+                                        size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n_cust >= 0 && n_days >= 0 && top_k >= 1, "bad argument");
+    FDX_REQUIRE(workspace_bytes >= fdx_card_precision_workspace_size(n_cust), "workspace too small");
+    if (n_days == 0) return FDX_OK;
+    FDX_REQUIRE(day_d && cust_d && pred_d && fraud_d && days_h && nb_compromised_h && cp_h && workspace_d,
+                "null pointer");
+    hipStream_t st = as_stream(stream);
+    char *w = reinterpret_cast<char *>(workspace_d);
+    int32_t *out = reinterpret_cast<int32_t *>(w);
+    unsigned long long *cmax = reinterpret_cast<unsigned long long *>(w + 256);
+    uint8_t *detected = reinterpret_cast<uint8_t *>(w + 256 + (size_t)n_cust * 8);
+    uint8_t *cfraud = detected + n_cust;
+    uint8_t *present = cfraud + n_cust;
+    uint8_t *scratch = present + n_cust;  // the day's detections when they are not carried over
+    FDX_HIP(hipMemsetAsync(detected, 0, (size_t)n_cust, st));
+    const unsigned grid = stream_grid(n, 256);
+    const unsigned cgrid = stream_grid(n_cust, 256);
+    for (int32_t k = 0; k < n_days; ++k) {
+        FDX_HIP(hipMemsetAsync(out, 0, 8, st));
+        FDX_HIP(hipMemsetAsync(cmax, 0, (size_t)n_cust * 8, st));
+        FDX_HIP(hipMemsetAsync(cfraud, 0, (size_t)n_cust * 2, st));  // cfraud + present
+        hipLaunchKernelGGL(k_cpk_day_max, dim3(grid), dim3(256), 0, st, day_d, cust_d, pred_d, fraud_d, n, days_h[k],
+                           detected, cmax, cfraud, present);
+        FDX_LAUNCHED("k_cpk_day_max");
+        hipLaunchKernelGGL(k_cpk_day_topk, dim3(cgrid), dim3(256), 0, st, cmax, cfraud, present, n_cust, top_k,
+                           remove_detected ? detected : scratch, out);
+        FDX_LAUNCHED("k_cpk_day_topk");
+        int32_t o[2];
+        FDX_HIP(hipMemcpyAsync(o, out, 8, hipMemcpyDeviceToHost, st));
+        FDX_HIP(hipStreamSynchronize(st));
+        nb_compromised_h[k] = o[0];
+        cp_h[k] = (double)o[1] / (double)top_k;
+    }
+    return FDX_OK;
+}
 
 extern "C" int fdx_segment_latest(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d, int64_t n_seg,
                                   int32_t *out_row_d, void *stream) {

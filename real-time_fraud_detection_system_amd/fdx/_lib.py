@@ -64,6 +64,11 @@ SIGNATURES = {
     "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
     "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),
     "fdx_dedup_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
+    "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,
+                                            c_sz, P, P]),
+    "fdx_card_precision_workspace_size": (ctypes.c_size_t, [c_i32]),
+    "fdx_card_precision_top_k": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, P, c_i32, c_i32, c_i32, P, P, P, c_sz,
+                                                P]),
     "fdx_invert_perm": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_rekey_workspace_size": (c_sz, [c_i64, c_i32]),
     "fdx_rekey": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, c_sz, P]),
