@@ -389,6 +389,40 @@ int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, const int64
                    int64_t *unscaled_d, double *amount_d, int64_t *ts_ns_d, int32_t *bad_d, void *stream);
 int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d, int64_t n,
                      uint8_t *keep_d, void *stream);
+/* ---- config 5: streaming micro-batches with incremental window state ------------------
+ * BASELINE.json config 5 ("micro-batches of 64k CDC transactions: incremental window-state
+ * update + scoring").  The reference's streaming job (pyspark/scripts/fraud_detection.py:
+ * 88-201) joins each micro-batch against snapshot tables; this engine instead keeps, per
+ * customer and per terminal, the state the batch recurrences of fdx_customer_windows /
+ * fdx_terminal_windows hold at a key's last row, so that feeding a history batch by batch
+ * yields the same features, bit for bit, as one fdx_customer_windows / fdx_terminal_windows
+ * call over the whole history (rows of one key in (ts, batch row) order).
+ * fdx_stream_create allocates the state (customer_ring / terminal_ring rows of recent history
+ * per key, powers of two: a key's rows of the longest window, resp. of delay + the longest
+ * window, must fit, else fdx_stream_status reports a ring overflow).  window_ns: n_windows
+ * customer windows = terminal windows (ns); delay_ns: the terminal label delay.
+ * fdx_stream_update(rows ts/cust/amount/term/fraud, n <= max_batch): customer ids in
+ *   [0, n_customers), terminal ids in [0, n_terminals); a key's rows must not go back in time
+ *   across batches.  cust_d == NULL skips the customer half, term_d == NULL the terminal half.
+ *   Writes X_d row r (leading dimension ld): [amount, weekend, night, (NB_w, AVG_w) x W] from
+ *   the customer half and (NB_w, RISK_w) x W at column term_col0 (-1 = 3 + 2W) from the
+ *   terminal half -- or, when term_rec_d != NULL, the terminal half as count records
+ *   term_rec_d[r][W] (NB | FRAUD << 32, as fdx_terminal_windows_packed) for the multi-GPU
+ *   return exchange.  Asynchronous; errors inside the kernels are collected as bits:
+ * fdx_stream_status: synchronises, returns and clears them (1 customer ring overflow, 2
+ *   terminal ring overflow, 4 key out of range, 8 rows out of time order). */
+typedef struct fdx_stream_s *fdx_stream;
+int fdx_stream_create(int64_t n_customers, int64_t n_terminals, int32_t customer_ring, int32_t terminal_ring,
+                      int32_t n_windows, const int64_t *window_ns, int64_t delay_ns, int32_t flags_mode,
+                      int64_t max_batch, fdx_stream *out, void *stream);
+int fdx_stream_reset(fdx_stream s, void *stream);
+int fdx_stream_memory(fdx_stream s, size_t *bytes);
+int fdx_stream_update(fdx_stream s, const int64_t *ts_d, const int32_t *cust_d, const double *amount_d,
+                      const int32_t *term_d, const uint8_t *fraud_d, int64_t n, double *X_d, int64_t ld,
+                      int32_t term_col0, int64_t *term_rec_d, void *stream);
+int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream);
+int fdx_stream_destroy(fdx_stream s);
+
 /* f-4 delay-aware split and Card-Precision@k (shared_functions.py:133-188, :352-411).
  * fdx_train_test_split: train_d[i] = t_lo <= ts_d[i] < t_hi; test_d[i] = the row is on test
  *   day d = day_d[i] - (min train day + delta_train + delta_delay), 0 <= d < delta_test, and

@@ -64,6 +64,12 @@ SIGNATURES = {
     "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
     "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),
     "fdx_dedup_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
+    "fdx_stream_create": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, c_i32, P, c_i64, c_i32, c_i64, P, P]),
+    "fdx_stream_reset": (ctypes.c_int, [P, P]),
+    "fdx_stream_memory": (ctypes.c_int, [P, P]),
+    "fdx_stream_update": (ctypes.c_int, [P, P, P, P, P, P, c_i64, P, c_i64, c_i32, P, P]),
+    "fdx_stream_status": (ctypes.c_int, [P, P, P]),
+    "fdx_stream_destroy": (ctypes.c_int, [P]),
     "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,
                                             c_sz, P, P]),
     "fdx_card_precision_workspace_size": (ctypes.c_size_t, [c_i32]),

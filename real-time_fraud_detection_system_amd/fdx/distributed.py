@@ -81,15 +81,22 @@ def exchange_begin(K, term, world, group=None):
 
 
 def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30), delay_days=7,
-                    group=None):
+                    group=None, records=None):
     """Phase 2: all-to-all of the rows, owner-side terminal records, all-to-all back.
-    Returns (reply [n_local, W] count records in send order, send_perm)."""
+    Returns (reply [n_local, W] count records in send order, send_perm).
+    records(rts, rterm_local, rfraud) -> [m, W] count records by receive position replaces
+    the owner-side batch windows (the streaming engine passes its incremental update)."""
     send_perm, send_counts, recv_counts = state
     sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
     rec = K.exchange_pack(ts, term, fraud, send_perm)
     recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
     dist.all_to_all_single(recv, rec, output_split_sizes=rc, input_split_sizes=sc, group=group)
     rts, rterm, rfr = K.exchange_unpack(recv, world)
+    if records is not None:
+        reply = records(rts, rterm, rfr)
+        back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
+        dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
+        return back, send_perm
     n_local_terms = (n_terminals_total + world - 1) // world
     # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
     # the records kernel handles such segments itself (no global time sort of the receive buffer)

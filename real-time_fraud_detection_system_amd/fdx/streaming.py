@@ -1,0 +1,173 @@
+"""BASELINE.json config 5: streaming micro-batches with incremental window state + scoring.
+
+The reference's streaming job (pyspark/scripts/fraud_detection.py:88-201) reads Debezium
+micro-batches from Kafka, LEFT JOINs them against feature snapshot tables written by the
+batch notebooks, scales and scores them in a pandas UDF.  Config 5 asks for the real-time
+version of that: each micro-batch updates the customer / terminal window state and is
+scored on fresh features.  The state lives in HBM (csrc/fdx_stream.hip) and is exactly the
+batch recurrences' state at each key's last row, so streaming a history batch by batch gives
+the same 15 features, bit for bit, as the batch path over the whole history
+(get_customer_spending_behaviour_features feature_transformation.ipynb:601-628,
+get_count_risk_rolling_window :1495-1522, tests/test_gpu_stream.py).
+
+  StreamState          device state + fdx_stream_update (features of a batch)
+  StreamScorer         StreamState + the forest (scale + predict_proba) per batch
+  ShardedStreamScorer  one process per GPU: customers sharded by id range, terminals owned
+                       by id % world, one RCCL all-to-all there and back per batch (the
+                       exchange of fdx.distributed, with the owner running its incremental
+                       terminal state instead of the batch windows)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib, ops
+from ._lib import FdxError, FdxUnsupported, check
+
+_STATUS = {1: "customer ring overflow (raise customer_ring)", 2: "terminal ring overflow (raise terminal_ring)",
+           4: "customer or terminal id outside the state's capacity", 8: "a key's rows went back in time"}
+
+
+class StreamState:
+    """Per-customer and per-terminal window state on the current GPU."""
+
+    def __init__(self, n_customers: int, n_terminals: int, windows_days=(1, 7, 30), delay_days=7,
+                 customer_ring=256, terminal_ring=256, max_batch=65536, flags_mode=_lib.FDX_FLAGS_NOTEBOOK,
+                 stream=None):
+        self.device = ops.require_gpu()
+        self.windows_days = tuple(int(d) for d in windows_days)
+        self.W = len(self.windows_days)
+        self.max_batch = int(max_batch)
+        h = ctypes.c_void_p()
+        check(_lib.load().fdx_stream_create(int(n_customers), int(n_terminals), int(customer_ring), int(terminal_ring),
+                                            self.W, ops._win_ns(self.windows_days), int(delay_days) * ops.NS_PER_DAY,
+                                            int(flags_mode), self.max_batch, ctypes.byref(h), ops._s(stream)),
+              "fdx_stream_create")
+        self._h = h
+        b = ctypes.c_size_t()
+        check(_lib.load().fdx_stream_memory(h, ctypes.byref(b)), "fdx_stream_memory")
+        self.memory_bytes = b.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib._lib.fdx_stream_destroy(h)
+            self._h = None
+
+    def reset(self, stream=None):
+        check(_lib.load().fdx_stream_reset(self._h, ops._s(stream)), "fdx_stream_reset")
+
+    def update(self, ts, customer=None, amount=None, terminal=None, fraud=None, X=None, term_col0=-1,
+               term_records=None, stream=None):
+        """One micro-batch (device tensors; int64 ns, int32 ids, f64, int32 ids, u8).  Writes and
+        returns X [n, >= 3 + 4W] float64 (columns in `input_features` order) unless the
+        terminal half goes to term_records [n, W] int64 (count records)."""
+        ops._dev(ts, torch.int64, "ts")
+        n = ts.numel()
+        if n > self.max_batch:
+            raise FdxError(f"batch of {n} rows > max_batch {self.max_batch}")
+        for t, dt, name in ((customer, torch.int32, "customer"), (amount, torch.float64, "amount"),
+                            (terminal, torch.int32, "terminal"), (fraud, torch.uint8, "fraud")):
+            if t is not None:
+                ops._dev(t, dt, name)
+                if t.numel() != n:
+                    raise FdxError(f"{name} has {t.numel()} rows, ts has {n}")
+        W = self.W
+        if X is None and (customer is not None or term_records is None):
+            X = torch.empty((n, 3 + 4 * W), dtype=torch.float64, device=ts.device)
+        if X is not None and (X.dtype != torch.float64 or X.stride(1) != 1):
+            raise FdxError("X must be float64 with unit column stride")
+        check(_lib.load().fdx_stream_update(self._h, ops._ptr(ts), ops._ptr(customer), ops._ptr(amount),
+                                            ops._ptr(terminal), ops._ptr(fraud), n, ops._ptr(X),
+                                            X.stride(0) if X is not None else 0, int(term_col0),
+                                            ops._ptr(term_records), ops._s(stream)), "fdx_stream_update")
+        return X
+
+    def check(self, stream=None):
+        """Synchronise and raise if a kernel reported a problem since the last check."""
+        f = ctypes.c_int32()
+        check(_lib.load().fdx_stream_status(self._h, ctypes.byref(f), ops._s(stream)), "fdx_stream_status")
+        if f.value:
+            raise FdxUnsupported("stream state: " + "; ".join(m for b, m in _STATUS.items() if f.value & b))
+
+
+class StreamScorer:
+    """Features + scaler + forest per micro-batch on one GPU (config 5 at N = 1)."""
+
+    def __init__(self, forest: ops.Forest, n_customers: int, n_terminals: int, windows_days=(1, 7, 30),
+                 delay_days=7, customer_ring=256, terminal_ring=256, max_batch=65536,
+                 flags_mode=_lib.FDX_FLAGS_NOTEBOOK):
+        self.forest = forest
+        self.state = StreamState(n_customers, n_terminals, windows_days, delay_days, customer_ring, terminal_ring,
+                                 max_batch, flags_mode)
+        W = self.state.W
+        if forest.n_features != 3 + 4 * W:
+            raise FdxError(f"forest has {forest.n_features} features, the stream makes {3 + 4 * W}")
+        dev = self.state.device
+        self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
+        self.ws = ops.workspace(forest.workspace_size(max_batch), dev)
+        self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
+
+    def score(self, ts, customer, amount, terminal, fraud):
+        """-> predict_proba[:, 1] of the batch (device view, valid until the next call)."""
+        n = ts.numel()
+        X = self.state.update(ts, customer, amount, terminal, fraud, X=self.X[:n])
+        return self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+
+
+def stream_terminal_exchange(K, records, ts, terminal, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
+                             delay_days=7, group=None):
+    """The per-batch terminal exchange of the sharded stream: rows to their terminal's owner
+    (RCCL all-to-all), the owner's incremental update `records(rts, rterm_local, rfraud)`,
+    count records back.  -> (records [n, W] in send order, send_perm).  K: the kernel set
+    (fdx.distributed.GpuKernels; the CPU tests pass numpy stand-ins)."""
+    from . import distributed as D
+
+    st = D.exchange_begin(K, terminal, world, group)
+    return D.exchange_finish(K, st, ts, terminal, fraud, world, n_terminals_total, windows_days, delay_days, group,
+                             records=records)
+
+
+class ShardedStreamScorer:
+    """Config 5 over `world` GPUs (this process = `rank`).  Each rank receives the rows of its
+    customers [customer_base, customer_base + n_customers_local) (Kafka partitions keyed by
+    customer); terminal t's state lives on rank t % world as local id t // world."""
+
+    def __init__(self, forest: ops.Forest, world: int, rank: int, n_customers_local: int, customer_base: int,
+                 n_terminals_total: int, windows_days=(1, 7, 30), delay_days=7, customer_ring=256,
+                 terminal_ring=256, max_batch=65536, max_recv=None, flags_mode=_lib.FDX_FLAGS_NOTEBOOK,
+                 group=None):
+        self.forest, self.world, self.rank, self.group = forest, world, rank, group
+        self.customer_base = int(customer_base)
+        self.n_terminals_total = int(n_terminals_total)
+        n_term_local = (self.n_terminals_total + world - 1) // world
+        # the owner side sees up to every rank's rows of its terminals in one batch
+        self.state = StreamState(n_customers_local, n_term_local, windows_days, delay_days, customer_ring,
+                                 terminal_ring, max(max_batch, max_recv or max_batch * world), flags_mode)
+        self.windows_days, self.delay_days = self.state.windows_days, int(delay_days)
+        W = self.state.W
+        dev = self.state.device
+        self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
+        self.ws = ops.workspace(forest.workspace_size(max_batch), dev)
+        self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
+
+    def _owner_records(self, rts, rterm, rfr):
+        rec = torch.empty((rts.numel(), self.state.W), dtype=torch.int64, device=rts.device)
+        self.state.update(rts, terminal=rterm, fraud=rfr, term_records=rec)
+        return rec
+
+    def score(self, ts, customer, amount, terminal, fraud):
+        from . import distributed as D
+
+        n = ts.numel()
+        W = self.state.W
+        K = D.GpuKernels
+        cust = ops.key_map(customer, _lib.FDX_KEY_SUB, self.customer_base) if self.customer_base else customer
+        X = self.state.update(ts, cust, amount, X=self.X[:n])            # customer half, local
+        back, send_perm = stream_terminal_exchange(K, self._owner_records, ts, terminal, fraud, self.world,
+                                                   self.n_terminals_total, self.windows_days, self.delay_days,
+                                                   self.group)
+        K.reply_assemble(back, send_perm, W, X, 3 + 2 * W)
+        return self.forest.predict(X, ws=self.ws, out=self.proba[:n])

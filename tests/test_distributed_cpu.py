@@ -140,3 +140,90 @@ def test_terminal_exchange_matches_single_process(world):
         for k, w in enumerate((1, 7, 30)):
             np.testing.assert_array_equal(nb[:, k], f[f"TERMINAL_ID_NB_TX_{w}DAY_WINDOW"][idx])
             np.testing.assert_array_equal(risk[:, k], f[f"TERMINAL_ID_RISK_{w}DAY_WINDOW"][idx])
+
+
+class NumpyStreamOwner:
+    """Stand-in for the owner's incremental terminal state (fdx_stream_update, terminal half):
+    keeps every local terminal's history and counts the delayed windows by brute force."""
+
+    def __init__(self, windows_days=(1, 7, 30), delay_days=7):
+        self.win = [w * 86400 * 10**9 for w in windows_days]
+        self.delay = delay_days * 86400 * 10**9
+        self.hist = {}
+
+    def __call__(self, rts, rterm, rfr):
+        ts, tl, fr = rts.numpy(), rterm.numpy(), rfr.numpy()
+        rec = np.zeros((len(ts), len(self.win)), np.int64)
+        for i in np.lexsort((np.arange(len(ts)), ts)):
+            h = self.hist.setdefault(int(tl[i]), ([], []))
+            ht, hf = np.array(h[0], np.int64), np.array(h[1], np.int64)
+            t = int(ts[i])
+            for k, w in enumerate(self.win):
+                m = (ht <= t - self.delay) & (ht > t - self.delay - w)
+                rec[i, k] = int(m.sum()) | (int(hf[m].sum()) << 32)
+            h[0].append(t)
+            h[1].append(int(fr[i]))
+        return torch.from_numpy(rec)
+
+
+def _stream_worker(rank, world, port, shards, cuts, n_terms, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fdx.streaming import stream_terminal_exchange
+
+    d = shards[rank]
+    owner = NumpyStreamOwner()
+    nb_all, risk_all = np.zeros((len(d["ts"]), 3)), np.zeros((len(d["ts"]), 3))
+    for a_t, b_t in zip(cuts[:-1], cuts[1:]):        # the same time cuts on every rank
+        sel = np.flatnonzero((d["ts"] >= a_t) & (d["ts"] < b_t))
+        back, send_perm = stream_terminal_exchange(
+            CpuKernels, owner, torch.from_numpy(d["ts"][sel]), torch.from_numpy(d["terminal"][sel]),
+            torch.from_numpy(d["fraud"][sel]), world, n_terms)
+        nb, risk = CpuKernels.unpack_reply(back, 3)
+        rows = sel[send_perm.numpy()]
+        nb_all[rows], risk_all[rows] = nb, risk
+    q.put((rank, nb_all, risk_all))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stream_terminal_exchange_matches_single_process():
+    """config 5 routing over 2 ranks: micro-batches cut at the same times on every rank, rows to
+    their terminal's owner, the owner's incremental state, records back -- equal to the
+    single-process terminal features of the whole history"""
+    from fdx import synth
+
+    world, n_terms = 2, 120
+    shards = [synth.generate(n_customers=80, n_terminals=n_terms, nb_days=50, r=30, seed=21 + r,
+                             customer_offset=80 * r) for r in range(world)]
+    t0 = min(s["ts"].min() for s in shards)
+    t1 = max(s["ts"].max() for s in shards) + 1
+    cuts = np.unique(np.r_[t0, np.random.default_rng(4).integers(t0, t1, 25), t1])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, shards, cuts, n_terms, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, nb, risk = q.get(timeout=300)
+        res[r] = (nb, risk)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allc = {k: np.concatenate([s[k] for s in shards]) for k in shards[0]}
+    order = np.argsort(allc["ts"], kind="stable")
+    g = {k: v[order] for k, v in allc.items()}
+    f = oracle.featurize_arrays(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
+    inv = np.empty_like(order); inv[order] = np.arange(len(order))
+    start = 0
+    for r in range(world):
+        n = len(shards[r]["ts"])
+        idx = inv[start:start + n]
+        start += n
+        nb, risk = res[r]
+        for k, w in enumerate((1, 7, 30)):
+            np.testing.assert_array_equal(nb[:, k], f[f"TERMINAL_ID_NB_TX_{w}DAY_WINDOW"][idx])
+            np.testing.assert_array_equal(risk[:, k], f[f"TERMINAL_ID_RISK_{w}DAY_WINDOW"][idx])
