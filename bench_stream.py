@@ -1,0 +1,189 @@
+"""Config 5 benchmark (BASELINE.json configs[4]): streaming micro-batches of 64k CDC
+transactions -- incremental customer / terminal window state update + StandardScaler +
+RandomForest(100, depth 20) predict_proba -- p50 / p99 batch latency.
+
+Workload: the tail of config 4 (1M customers / 2M terminals, handbook distributions,
+fdx.synth).  History: --history-days days streamed into the state first (day-sized batches,
+untimed), so every ring holds a realistic 30 / 37-day window; then the next day is cut into
+micro-batches of --batch transactions (global) and each is timed end to end:
+  host batch (pinned) -> HBM -> fdx_stream_update (2 launches) -> forest -> proba -> host.
+Also reported: the device-only time of the update + scoring (HIP events) and the rate.
+
+N GPUs (torch.distributed.run, one process per GPU): customers sharded by contiguous id
+range, each micro-batch split by customer owner, terminals owned by id % N, one RCCL
+all-to-all there and back per batch (fdx.streaming.ShardedStreamScorer); the batch latency
+is the max over ranks.  Rank 0 prints one JSON line.
+
+usage: python bench_stream.py [--gpus N] [--batches K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--customers", type=int, default=1_000_000)
+    ap.add_argument("--terminals", type=int, default=2_000_000)
+    ap.add_argument("--history-days", type=int, default=38)
+    ap.add_argument("--batch", type=int, default=65536, help="global transactions per micro-batch")
+    ap.add_argument("--batches", type=int, default=0, help="timed batches (0 = the whole streamed day)")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed micro-batches before the timed ones")
+    ap.add_argument("--customer-ring", type=int, default=256)
+    ap.add_argument("--terminal-ring", type=int, default=256)
+    ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from bench import load_model
+    from fdx import ops, synth
+    from fdx.streaming import ShardedStreamScorer, StreamScorer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n_c = args.customers // world
+    base = rank * n_c
+    t_gen = time.perf_counter()
+    d = synth.generate(n_c, args.terminals, args.history_days + 1, seed=4321 + rank, customer_offset=base)
+    t_gen = time.perf_counter() - t_gen
+    split = synth.START_NS + args.history_days * 86400 * synth.NS
+    h = int(np.searchsorted(d["ts"], split))
+    day_ns = 86400 * synth.NS
+
+    arrays, mean, scale, check_X, check_proba = load_model(args.model)
+    forest = ops.Forest(arrays, 15, mean, scale)
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    if not np.array_equal(forest.predict(T(check_X, torch.float64)).cpu().numpy(), check_proba):
+        raise SystemExit("forest parity check against sklearn failed")
+
+    # history batches: one per day (untimed); the state's batch capacity covers them
+    day_cuts = np.searchsorted(d["ts"][:h], synth.START_NS + np.arange(args.history_days + 1) * day_ns)
+    max_day = int(np.diff(day_cuts).max()) if h else 0
+    per_rank = args.batch // world
+    # common micro-batch time cuts: every per_rank-th timestamp of rank 0's streamed day
+    s_ts = d["ts"][h:]
+    if rank == 0:
+        cuts = s_ts[::per_rank].astype(np.int64)
+        cuts = np.r_[cuts, s_ts[-1] + 1] if len(s_ts) else np.array([split, split + 1])
+        hdr = torch.tensor([len(cuts)], dtype=torch.int64, device=dev)
+    else:
+        hdr = torch.zeros(1, dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.broadcast(hdr, 0)
+    cut_t = torch.zeros(int(hdr.item()), dtype=torch.int64, device=dev)
+    if rank == 0:
+        cut_t.copy_(torch.from_numpy(cuts))
+    if world > 1:
+        dist.broadcast(cut_t, 0)
+    cuts = cut_t.cpu().numpy()
+    bounds = np.searchsorted(s_ts, cuts) + h
+    bounds[0], bounds[-1] = h, len(d["ts"])
+    max_mb = int(np.diff(bounds).max())
+    cap = max(max_day, max_mb, 1)
+
+    if world > 1:
+        sc = ShardedStreamScorer(forest, world, rank, n_c, base, args.terminals, customer_ring=args.customer_ring,
+                                 terminal_ring=args.terminal_ring, max_batch=cap, max_recv=cap * world * 2)
+    else:
+        sc = StreamScorer(forest, n_c, args.terminals, customer_ring=args.customer_ring,
+                          terminal_ring=args.terminal_ring, max_batch=cap)
+    cols = [("ts", torch.int64), ("customer", torch.int32), ("amount", torch.float64), ("terminal", torch.int32),
+            ("fraud", torch.uint8)]
+    # pinned host copies of the whole input (the "arriving" micro-batches are slices)
+    pin = {k: torch.from_numpy(np.ascontiguousarray(d[k])).pin_memory() for k, _ in cols}
+    dcols = {k: torch.empty(cap, dtype=t, device=dev) for k, t in cols}
+    out_h = torch.empty(cap, dtype=torch.float64).pin_memory()
+
+    def run(a, b, ev=None):
+        n = b - a
+        for k, _ in cols:
+            dcols[k][:n].copy_(pin[k][a:b], non_blocking=True)
+        if ev is not None:
+            ev[0].record()
+        p = sc.score(*(dcols[k][:n] for k, _ in cols))
+        if ev is not None:
+            ev[1].record()
+        out_h[:n].copy_(p, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return n
+
+    t_hist = time.perf_counter()
+    for k in range(args.history_days):
+        run(int(day_cuts[k]), int(day_cuts[k + 1]))
+    sc.state.check()
+    t_hist = time.perf_counter() - t_hist
+
+    nb = len(bounds) - 1
+    n_warm = min(args.warmup, max(nb - 1, 0))
+    n_timed = nb - n_warm if args.batches <= 0 else min(args.batches, nb - n_warm)
+    for k in range(n_warm):
+        run(int(bounds[k]), int(bounds[k + 1]))
+    if world > 1:
+        dist.barrier()
+    lat, dev_ms, rows = [], [], 0
+    for k in range(n_warm, n_warm + n_timed):
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        t0 = time.perf_counter()
+        rows += run(int(bounds[k]), int(bounds[k + 1]), ev)
+        lat.append((time.perf_counter() - t0) * 1e3)
+        dev_ms.append(ev[0].elapsed_time(ev[1]))
+    sc.state.check()
+    lat, dev_ms = np.array(lat), np.array(dev_ms)
+    total_rows = rows
+    if world > 1:
+        t = torch.tensor(np.stack([lat, dev_ms]), dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lat, dev_ms = t[0].cpu().numpy(), t[1].cpu().numpy()
+        r = torch.tensor([rows], dtype=torch.int64, device=dev)
+        dist.all_reduce(r)
+        total_rows = int(r.item())
+    out = {
+        "metric": "config 5: micro-batch latency, incremental window-state update + RF(100, d20) scoring",
+        "value": round(float(np.percentile(lat, 50)), 3),
+        "unit": "ms (p50 per micro-batch, host batch in -> probabilities on host)",
+        "p99_ms": round(float(np.percentile(lat, 99)), 3),
+        "max_ms": round(float(lat.max()), 3),
+        "device_p50_ms": round(float(np.percentile(dev_ms, 50)), 3),
+        "device_p99_ms": round(float(np.percentile(dev_ms, 99)), 3),
+        "tx_per_s": round(total_rows / (lat.sum() * 1e-3), 1),
+        "higher_is_better": False,
+        "n_gpus": world,
+        "batches": int(n_timed),
+        "warmup": int(n_warm),
+        "mean_batch_tx": round(total_rows / max(n_timed, 1), 1),
+        "dtype": "f64",
+        "data": "synthetic: handbook-distribution generator (fdx.synth, seed 4321+rank)",
+        "config": {"workload": f"configs[4]: tail of configs[3] ({args.customers} customers / {args.terminals} "
+                               f"terminals), {args.history_days} days of history in the state, then day "
+                               f"{args.history_days} as micro-batches of {args.batch} tx",
+                   "parallelism": f"customer-sharded x{world}, terminal owner = id % {world}",
+                   "state_bytes_per_gpu": sc.state.memory_bytes,
+                   "rings": [args.customer_ring, args.terminal_ring]},
+        "setup_s": {"generate": round(t_gen, 1), "history_stream": round(t_hist, 1)},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

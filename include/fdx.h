@@ -290,7 +290,12 @@ int fdx_forest_pack_rank(const fdx_forest_desc *desc, uint32_t *nodes_out, int32
 int fdx_forest_destroy(fdx_forest forest);
 int fdx_forest_info(fdx_forest forest, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
                     int32_t *n_chunks);
+/* Workspace for a traversal of n_rows rows.  Small batches (that cannot fill the CUs with
+ * one LDS chunk at a time) also get room for per-tree values, so that every chunk runs in
+ * one launch; a workspace without that room still works (chunk-sequential launches).
+ * fdx_forest_workspace_size_max: one workspace for every batch size up to n_rows. */
 size_t fdx_forest_workspace_size(fdx_forest forest, int64_t n_rows);
+size_t fdx_forest_workspace_size_max(fdx_forest forest, int64_t n_rows);
 /* X element (r, f) is X_d[r*row_stride + f*col_stride] (float64, raw unscaled features;
  * NaN allowed = missing).  proba_d[r] = predict_proba(X)[r, 1]; leaf_d (optional) is
  * [n][n_trees] int32 sklearn node ids (tree_.apply). */

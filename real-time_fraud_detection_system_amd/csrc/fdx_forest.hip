@@ -952,6 +952,30 @@ __device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int6
     }
 }
 
+// concurrent-chunk mode: tree t's value of row r at tv[t * tv_n + r] (lanes = consecutive rows)
+template <int R, int GG>
+__device__ __forceinline__ void rank_tree_values(const double (&v)[R * GG], int t, const int64_t (&row)[R],
+                                                 const bool (&ok)[R], double *__restrict__ tv, int64_t tv_n) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;
+#pragma unroll
+        for (int g = 0; g < GG; ++g) tv[(int64_t)(t + g) * tv_n + row[r]] = v[r * GG + g];
+    }
+}
+
+// proba[row] = (sum of the row's tree values in tree order) / n_trees: the same float64
+// additions, in the same order, as the chunk-sequential launches' running sum.
+__global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv, int64_t n, int32_t n_trees,
+                                                  const int32_t *__restrict__ out_perm, double *__restrict__ proba) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        double a = 0.0;
+        for (int t = 0; t < n_trees; ++t) a += tv[(int64_t)t * n + r];
+        const int64_t dst = out_perm ? (int64_t)out_perm[r] : r;
+        if (dst >= 0) proba[dst] = a / (double)n_trees;
+    }
+}
+
 // One launch = trees [t0, t1) of one LDS chunk over rows [r0, r1), rank layout; one block
 // per CU (the LDS holds one block), grid-striding over row tiles of BLOCK*R rows.  Each lane
 // walks G trees for each of its R rows at once (K = R*G chains); a chunk's last t1-t0 mod G
@@ -967,8 +991,18 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1, const double *__restrict__ lval,
     const uint8_t *__restrict__ mleft, double *__restrict__ acc, double *__restrict__ proba,
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
-    int32_t n_trees, int first, int last) {
+    int32_t n_trees, int first, int last, const int32_t *__restrict__ chunk_t,
+    const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n) {
     constexpr int kPlaneRows = P16 ? 2 * kRankPlaneRows : kRankPlaneRows;  // both: 4 KiB per plane
+    if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
+        const int c = blockIdx.y;
+        t0 = chunk_t[c];
+        t1 = chunk_t[c + 1];
+        node_base = chunk_base[c];
+        chunk_nodes = (int32_t)(chunk_base[c + 1] - node_base);
+        first = 1;
+        last = 0;
+    }
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
@@ -1039,6 +1073,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
             rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
             if (pending) rank_accumulate<R, G>(a, pv);
             rank_leaf_values<K>(pa, node_base, lval, pv);
+            if (tv) rank_tree_values<R, G>(pv, t, row, ok, tv, tv_n);
             pending = true;
             if (leaf_out) rank_leaf_ids<R, G>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees);
         }
@@ -1052,6 +1087,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
             if (pending) rank_accumulate<R, G>(a, pv);                                                     \
             pending = false;                                                                               \
             rank_leaf_values<R * NT>(pt, node_base, lval, vt);                                             \
+            if (tv) rank_tree_values<R, NT>(vt, t, row, ok, tv, tv_n);                                     \
             rank_accumulate<R, NT>(a, vt);                                                                 \
             if (leaf_out) rank_leaf_ids<R, NT>(pt, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees); \
         }                                                                                                  \
@@ -1065,6 +1101,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
         FDX_RANK_TAIL(7)
 #undef FDX_RANK_TAIL
         if (pending) rank_accumulate<R, G>(a, pv);
+        if (tv) continue;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!ok[r]) continue;
@@ -1375,7 +1412,7 @@ int upload_chunks(fdx_forest_s *F) {
         cb[c] = F->chunks[c].node_base;
     }
     ct.back() = F->n_trees;
-    cb.back() = F->n_nodes;
+    cb.back() = F->chunks.empty() ? 0 : F->chunks.back().node_base + F->chunks.back().nodes;
     FDX_HIP(hipMemcpy(F->chunk_t_d, ct.data(), sizeof(int32_t) * ct.size(), hipMemcpyHostToDevice));
     FDX_HIP(hipMemcpy(F->chunk_base_d, cb.data(), sizeof(int64_t) * cb.size(), hipMemcpyHostToDevice));
     return FDX_OK;
@@ -1646,10 +1683,35 @@ extern "C" int fdx_forest_info(fdx_forest F, int32_t *n_trees, int32_t *n_featur
     return FDX_OK;
 }
 
+// Batches of at most this many rows (a sequential chunk launch would leave CUs idle: one
+// block per CU) run every LDS chunk at once and need per-tree values in the workspace.
+static int64_t concurrent_rows(const fdx_forest_s *F) {
+    if (!rank_mode(F)) return 0;
+    const Variant v = kVariants[F->variant];
+    return (int64_t)F->n_cu * v.block * v.rows / 2;
+}
+
+extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows);
+
+// a workspace that serves every batch of up to n_rows rows at full speed
+extern "C" size_t fdx_forest_workspace_size_max(fdx_forest F, int64_t n_rows) {
+    if (!F || n_rows <= 0) return 256;
+    const size_t a = fdx_forest_workspace_size(F, n_rows);
+    const size_t b = fdx_forest_workspace_size(F, std::min<int64_t>(n_rows, concurrent_rows(F)));
+    return a > b ? a : b;
+}
+
+// rows + running sums + NaN flag word: what every traversal needs
+static size_t ws_base(const fdx_forest_s *F, int64_t n_rows) {
+    return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows) + 256;
+}
+
 extern "C" size_t fdx_forest_workspace_size(fdx_forest F, int64_t n_rows) {
     if (!F || n_rows <= 0) return 256;
-    return align_up(sizeof(float) * F->zstride * (size_t)n_rows) + align_up(sizeof(double) * (size_t)n_rows) +
-           256;  // + NaN flag word
+    size_t b = ws_base(F, n_rows);
+    if (n_rows <= concurrent_rows(F) && F->chunks.size() > 1)
+        b += align_up(sizeof(double) * (size_t)n_rows * F->n_trees);  // per-tree values
+    return b;
 }
 
 static RankTab rank_tab(const fdx_forest_s *F) {
@@ -1687,7 +1749,7 @@ static RankTab rank_tab(const fdx_forest_s *F) {
 
 static int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, double **acc,
                      int32_t **nan_flag = nullptr) {
-    size_t need = fdx_forest_workspace_size(F, n);
+    size_t need = ws_base(F, n);  // (a smaller batch's per-tree values are optional: see forest_traverse)
     if (!ws || ws_bytes < need) {
         set_error("forest workspace too small: %zu < %zu", ws_bytes, need);
         return FDX_E_WORKSPACE;
@@ -1735,20 +1797,28 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
     // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
     // features and running sums stay in the 256 MiB Infinity Cache.
     if (rank_mode(F)) {
-        const int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
+        int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
         const size_t nc = F->chunks.size();
         const uint16_t *zr = reinterpret_cast<const uint16_t *>(z);
+        // small batch: all chunks in one launch (grid.y = chunk) + k_tree_sum
+        double *tv = nullptr;
+        if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n)) {
+            tv = reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + align_up(sizeof(double) * (size_t)n) + 256);
+            slab = n;
+        }
         for (int64_t s0 = 0; s0 < n; s0 += slab) {
             const int64_t s1 = std::min<int64_t>(n, s0 + slab);
-            for (size_t c = 0; c < nc; ++c) {
+            for (size_t c = 0; c < (tv ? 1 : nc); ++c) {
                 const auto &ch = F->chunks[c];
                 const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_RANK(B, R, G, P, ...)                                                                      \
     do {                                                                                                      \
-        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), F->n_cu);      \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0>), dim3(grid), dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
+        const int64_t tiles_ = ceil_div(s1 - s0, (int64_t)(B) * (R));                                         \
+        const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu), tv ? (unsigned)nc : 1u); \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
                            (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
-                           F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last);     \
+                           F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last,     \
+                           F->chunk_t_d, F->chunk_base_d, tv, n);                                                \
     } while (0)
                 switch (F->variant) {
                     case 17: FDX_LAUNCH_RANK(1024, 1, 2, false); break;
@@ -1783,6 +1853,11 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
 #undef FDX_LAUNCH_RANK
                 FDX_LAUNCHED("k_forest_rank");
             }
+        }
+        if (tv) {
+            hipLaunchKernelGGL(k_tree_sum, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, st, tv, n, F->n_trees,
+                               out_perm_d, proba_d);
+            FDX_LAUNCHED("k_tree_sum");
         }
         return FDX_OK;
     }

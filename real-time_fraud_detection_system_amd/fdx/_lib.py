@@ -95,6 +95,7 @@ SIGNATURES = {
     "fdx_forest_destroy": (ctypes.c_int, [P]),
     "fdx_forest_info": (ctypes.c_int, [P, P, P, P, P]),
     "fdx_forest_workspace_size": (c_sz, [P, c_i64]),
+    "fdx_forest_workspace_size_max": (ctypes.c_size_t, [P, c_i64]),
     "fdx_forest_predict": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, P, P, c_sz, P]),
     "fdx_forest_prepare": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, c_sz, P]),
     "fdx_forest_traverse": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),

@@ -396,6 +396,10 @@ class Forest:
     def workspace_size(self, n: int) -> int:
         return int(_lib.load().fdx_forest_workspace_size(self._h, int(n)))
 
+    def workspace_size_max(self, n: int) -> int:
+        """one workspace for every batch of up to n rows (small batches' fast path included)"""
+        return int(_lib.load().fdx_forest_workspace_size_max(self._h, int(n)))
+
     def predict(self, X: torch.Tensor, want_leaves: bool = False, ws: torch.Tensor | None = None,
                 out: torch.Tensor | None = None, stream=None):
         """X: float64 GPU tensor [n, n_features] (any strides).  Returns proba (and leaves)."""
@@ -407,7 +411,7 @@ class Forest:
         proba = out if out is not None else torch.empty(n, dtype=torch.float64, device=X.device)
         leaves = torch.empty((n, self.n_trees), dtype=torch.int32, device=X.device) if want_leaves else None
         need = self.workspace_size(n)
-        if ws is None or ws.numel() < need:
+        if ws is None:
             ws = workspace(need, X.device)
         check(_lib.load().fdx_forest_predict(self._h, _ptr(X), n, X.stride(0), X.stride(1), _ptr(proba),
                                              _ptr(leaves), _ptr(ws), ws.numel(), _s(stream)),

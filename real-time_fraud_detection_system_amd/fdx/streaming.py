@@ -107,7 +107,7 @@ class StreamScorer:
             raise FdxError(f"forest has {forest.n_features} features, the stream makes {3 + 4 * W}")
         dev = self.state.device
         self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
-        self.ws = ops.workspace(forest.workspace_size(max_batch), dev)
+        self.ws = ops.workspace(forest.workspace_size_max(max_batch), dev)
         self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
 
     def score(self, ts, customer, amount, terminal, fraud):
@@ -150,7 +150,7 @@ class ShardedStreamScorer:
         W = self.state.W
         dev = self.state.device
         self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
-        self.ws = ops.workspace(forest.workspace_size(max_batch), dev)
+        self.ws = ops.workspace(forest.workspace_size_max(max_batch), dev)
         self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
 
     def _owner_records(self, rts, rterm, rfr):

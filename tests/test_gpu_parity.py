@@ -181,6 +181,32 @@ def test_forest_matches_sklearn_golden(dev, golden, name):
     np.testing.assert_array_equal(f.predict(Xc).cpu().numpy(), z["proba"])
 
 
+@pytest.mark.parametrize("n_rows", [1, 777, 20_000, 131_072])
+def test_forest_small_batch_concurrent_chunks(dev, n_rows):
+    """batches that cannot fill the CUs run all LDS chunks in one launch and sum the per-tree
+    values in tree order (k_tree_sum): same bits as the chunk-sequential launches (forced by
+    a workspace without room for the per-tree values) and as the oracle"""
+    rng = np.random.default_rng(n_rows)
+    arr = random_forest(rng, 80, 11)
+    X = rng.normal(size=(n_rows, 15))
+    X[rng.random(X.shape) < 0.01] = np.nan
+    mean, scale = rng.normal(size=15) * 0.1, rng.uniform(0.5, 2.0, size=15)
+    f = ops.Forest(arr, 15, mean, scale)
+    assert f.n_chunks >= 2
+    Xd = T(X, torch.float64, dev)
+    p1, l1 = f.predict(Xd, want_leaves=True)                      # full workspace: concurrent chunks
+    base = 4 * 16 * n_rows + 8 * n_rows + 1024
+    ws = ops.workspace(base, dev)
+    assert ws.numel() < f.workspace_size(n_rows)
+    p2, l2 = f.predict(Xd, want_leaves=True, ws=ws)              # sequential chunk launches
+    np.testing.assert_array_equal(p1.cpu().numpy(), p2.cpu().numpy())
+    np.testing.assert_array_equal(l1.cpu().numpy(), l2.cpu().numpy())
+    if n_rows <= 20_000:
+        op, ol = oracle.forest_predict(X, arr, mean, scale, want_leaves=True)
+        np.testing.assert_array_equal(p1.cpu().numpy(), op)
+        np.testing.assert_array_equal(l1.cpu().numpy(), ol)
+
+
 @pytest.mark.parametrize("n_trees,depth", [(60, 10), (2, 15)])
 def test_forest_chunks_and_global_path(dev, n_trees, depth):
     rng = np.random.default_rng(depth)
