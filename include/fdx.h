@@ -413,7 +413,11 @@ int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int3
  *   the customer half and (NB_w, RISK_w) x W at column term_col0 (-1 = 3 + 2W) from the
  *   terminal half -- or, when term_rec_d != NULL, the terminal half as count records
  *   term_rec_d[r][W] (NB | FRAUD << 32, as fdx_terminal_windows_packed) for the multi-GPU
- *   return exchange.  Asynchronous; errors inside the kernels are collected as bits:
+ *   return exchange.  When cust_nb_d / cust_sum_d are given, the customer half goes there
+ *   instead ([W][n] planes: NB int32 and the rolling SUM, bit-exact pandas roll_sum), and X_d
+ *   may be NULL: the scoring layout of fdx_forest_prepare_grouped (cust_val_is_sum = 1,
+ *   cust_perm_d = NULL, term_inv_d = NULL, cust_ts_d / cust_amount_d = the batch's ts / amount).
+ *   Asynchronous; errors inside the kernels are collected as bits:
  * fdx_stream_status: synchronises, returns and clears them (1 customer ring overflow, 2
  *   terminal ring overflow, 4 key out of range, 8 rows out of time order). */
 typedef struct fdx_stream_s *fdx_stream;
@@ -424,7 +428,8 @@ int fdx_stream_reset(fdx_stream s, void *stream);
 int fdx_stream_memory(fdx_stream s, size_t *bytes);
 int fdx_stream_update(fdx_stream s, const int64_t *ts_d, const int32_t *cust_d, const double *amount_d,
                       const int32_t *term_d, const uint8_t *fraud_d, int64_t n, double *X_d, int64_t ld,
-                      int32_t term_col0, int64_t *term_rec_d, void *stream);
+                      int32_t term_col0, int32_t *cust_nb_d, double *cust_sum_d, int64_t *term_rec_d,
+                      void *stream);
 int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream);
 int fdx_stream_destroy(fdx_stream s);
 

@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         float v[FS];
 #pragma unroll
         for (int f = 0; f < FS; ++f) v[f] = 0.0f;
-        const int32_t r = cust_perm[i];
+        const int32_t r = cust_perm ? cust_perm[i] : (int32_t)i;
         if (r < 0) {  // padding slot of the interleaved layout: never written back
             if constexpr (RANK) {
                 uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
@@ -2019,8 +2019,7 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
                 3 + 4 * n_windows);
     if (n == 0) return FDX_OK;
-    FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && cust_perm_d && term_rec_d,
-                "null pointer");
+    FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && term_rec_d, "null pointer");
     float *z;
     double *acc;
     int32_t *flag;

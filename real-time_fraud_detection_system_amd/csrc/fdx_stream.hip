@@ -116,10 +116,12 @@ __global__ void __launch_bounds__(256) k_stream_link(
             } else {
                 cnext[i] = atomicExch(&chead[c], (int32_t)i);
             }
-            double we, ni;
-            time_flags(ts[i], mode, we, ni);
-            double *x = X + i * ld;
-            x[0] = amount[i]; x[1] = we; x[2] = ni;
+            if (X) {
+                double we, ni;
+                time_flags(ts[i], mode, we, ni);
+                double *x = X + i * ld;
+                x[0] = amount[i]; x[1] = we; x[2] = ni;
+            }
         }
         if (term) {
             const int32_t t = term[i];
@@ -163,7 +165,8 @@ template <int W>
 __device__ void customer_key(int32_t c, int32_t head, const int32_t *__restrict__ cnext,
                              const int64_t *__restrict__ ts, const double *__restrict__ amount,
                              const StreamWin &sw, int64_t *__restrict__ cstate, CEnt *__restrict__ cring,
-                             int32_t C, double *__restrict__ X, int64_t ld, int32_t *__restrict__ status) {
+                             int32_t C, double *__restrict__ X, int64_t ld, int32_t *__restrict__ cnb_out,
+                             double *__restrict__ csum_out, int64_t n_rows, int32_t *__restrict__ status) {
     int64_t *rec = cstate + (int64_t)c * (2 + 6 * W);
     CEnt *ring = cring + (int64_t)c * C;
     const int64_t mask = C - 1;
@@ -190,7 +193,7 @@ __device__ void customer_key(int32_t c, int32_t head, const int32_t *__restrict_
 #pragma unroll
         for (int w = 0; w < W; ++w) e[w] = tail[w] < n ? ring[tail[w] & mask] : CEnt{INT64_MAX, 0.0};
         int64_t tmin = n;
-        double *x = X + (int64_t)row * ld + 3;
+        double *x = cnb_out ? nullptr : X + (int64_t)row * ld + 3;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const int64_t bound = t - sw.win[w];
@@ -207,8 +210,13 @@ __device__ void customer_key(int32_t c, int32_t head, const int32_t *__restrict_
             s[w].add(v);
             tail[w] = nt;
             tmin = nt < tmin ? nt : tmin;
-            x[2 * w] = (double)s[w].nobs;
-            x[2 * w + 1] = s[w].value() / (double)s[w].nobs;
+            if (cnb_out) {  // scoring planes: NB and the rolling SUM (the consumer divides)
+                cnb_out[(int64_t)w * n_rows + row] = s[w].nobs;
+                csum_out[(int64_t)w * n_rows + row] = s[w].value();
+            } else {
+                x[2 * w] = (double)s[w].nobs;
+                x[2 * w + 1] = s[w].value() / (double)s[w].nobs;
+            }
         }
         if (n >= C && n - C >= tmin) bad |= kStCustRing;
         ring[n & mask] = CEnt{t, v};
@@ -291,17 +299,23 @@ __global__ void __launch_bounds__(256) k_stream_process(
     StreamWin sw, int32_t *__restrict__ chead, const int32_t *__restrict__ cnext, int32_t *__restrict__ thead,
     const int32_t *__restrict__ tnext, int64_t *__restrict__ cstate, CEnt *__restrict__ cring, int32_t C,
     int64_t *__restrict__ tstate, int64_t *__restrict__ tring, int32_t T, double *__restrict__ X, int64_t ld,
-    int32_t tcol0, int64_t *__restrict__ rec_out, int32_t *__restrict__ status) {
+    int32_t tcol0, int32_t *__restrict__ cnb_out, double *__restrict__ csum_out, int64_t *__restrict__ rec_out,
+    int32_t *__restrict__ status) {
+    // grid.y = 2 when both halves run: the customer and terminal keys of a row are walked by
+    // different threads, so their dependent-load chains overlap instead of adding up
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (cust) {
+    const bool do_c = cust && (gridDim.y == 1 || blockIdx.y == 0);
+    const bool do_t = term && (gridDim.y == 1 || blockIdx.y == 1);
+    if (do_c) {
         const int32_t c = cust[i];
         if (c >= 0 && c < n_cust && chead[c] == (int32_t)i) {
-            customer_key<W>(c, (int32_t)i, cnext, ts, amount, sw, cstate, cring, C, X, ld, status);
+            customer_key<W>(c, (int32_t)i, cnext, ts, amount, sw, cstate, cring, C, X, ld, cnb_out, csum_out, n,
+                            status);
             chead[c] = -1;
         }
     }
-    if (term) {
+    if (do_t) {
         const int32_t t = term[i];
         if (t >= 0 && t < n_term && thead[t] == (int32_t)i) {
             terminal_key<W>(t, (int32_t)i, tnext, ts, fraud, sw, tstate, tring, T, X, ld, tcol0, rec_out, status);
@@ -424,15 +438,16 @@ extern "C" int fdx_stream_memory(fdx_stream s, size_t *bytes) {
 
 #define FDX_STREAM_PROCESS(WW)                                                                                   \
     case WW:                                                                                                     \
-        hipLaunchKernelGGL(k_stream_process<WW>, dim3(grid), dim3(256), 0, st, ts_d, cust_d, amount_d, term_d,   \
+        hipLaunchKernelGGL(k_stream_process<WW>, grid, dim3(256), 0, st, ts_d, cust_d, amount_d, term_d,         \
                            fraud_d, n, s->n_cust, s->n_term, s->sw, s->chead_d, s->cnext_d, s->thead_d,          \
                            s->tnext_d, s->cstate_d, s->cring_d, s->C, s->tstate_d, s->tring_d, s->T, X_d, ld,     \
-                           tcol, term_rec_d, s->status_d);                                                       \
+                           tcol, cust_nb_d, cust_sum_d, term_rec_d, s->status_d);                                \
         break;
 
 extern "C" int fdx_stream_update(fdx_stream s, const int64_t *ts_d, const int32_t *cust_d, const double *amount_d,
                                  const int32_t *term_d, const uint8_t *fraud_d, int64_t n, double *X_d, int64_t ld,
-                                 int32_t term_col0, int64_t *term_rec_d, void *stream) {
+                                 int32_t term_col0, int32_t *cust_nb_d, double *cust_sum_d, int64_t *term_rec_d,
+                                 void *stream) {
     FDX_REQUIRE(s, "null stream state");
     FDX_REQUIRE(n >= 0 && n <= s->max_batch, "batch of %lld rows exceeds max_batch %lld", (long long)n,
                 (long long)s->max_batch);
@@ -442,14 +457,16 @@ extern "C" int fdx_stream_update(fdx_stream s, const int64_t *ts_d, const int32_
     FDX_REQUIRE(!term_d || (fraud_d && s->n_term), "terminal half needs fraud labels and terminal state");
     const int W = s->W;
     const int32_t tcol = term_col0 < 0 ? 3 + 2 * W : term_col0;
-    FDX_REQUIRE(!cust_d || (X_d && ld >= 3 + 2 * W), "X needs ld >= 3 + 2 * n_windows");
+    FDX_REQUIRE(!cust_nb_d == !cust_sum_d, "cust_nb_d and cust_sum_d go together");
+    FDX_REQUIRE(!cust_d || cust_nb_d || (X_d && ld >= 3 + 2 * W), "X needs ld >= 3 + 2 * n_windows");
+    FDX_REQUIRE(!X_d || ld >= 3, "X needs ld >= 3");
     FDX_REQUIRE(!term_d || term_rec_d || (X_d && ld >= tcol + 2 * W), "terminal columns do not fit ld");
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_stream_link, dim3(stream_grid(n, 256)), dim3(256), 0, st, ts_d, cust_d, amount_d, term_d, n,
                        s->n_cust, s->n_term, s->chead_d, s->cnext_d, s->thead_d, s->tnext_d, s->mode, X_d, ld,
                        s->status_d);
     FDX_LAUNCHED("k_stream_link");
-    const unsigned grid = (unsigned)ceil_div(n, 256);
+    const dim3 grid((unsigned)ceil_div(n, 256), cust_d && term_d ? 2u : 1u);
     switch (W) {
         FDX_STREAM_PROCESS(1)
         FDX_STREAM_PROCESS(2)

@@ -67,7 +67,7 @@ SIGNATURES = {
     "fdx_stream_create": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, c_i32, P, c_i64, c_i32, c_i64, P, P]),
     "fdx_stream_reset": (ctypes.c_int, [P, P]),
     "fdx_stream_memory": (ctypes.c_int, [P, P]),
-    "fdx_stream_update": (ctypes.c_int, [P, P, P, P, P, P, c_i64, P, c_i64, c_i32, P, P]),
+    "fdx_stream_update": (ctypes.c_int, [P, P, P, P, P, P, c_i64, P, c_i64, c_i32, P, P, P, P]),
     "fdx_stream_status": (ctypes.c_int, [P, P, P]),
     "fdx_stream_destroy": (ctypes.c_int, [P]),
     "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,

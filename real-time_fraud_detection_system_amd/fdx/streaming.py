@@ -60,10 +60,12 @@ class StreamState:
         check(_lib.load().fdx_stream_reset(self._h, ops._s(stream)), "fdx_stream_reset")
 
     def update(self, ts, customer=None, amount=None, terminal=None, fraud=None, X=None, term_col0=-1,
-               term_records=None, stream=None):
+               term_records=None, cust_nb=None, cust_sum=None, stream=None):
         """One micro-batch (device tensors; int64 ns, int32 ids, f64, int32 ids, u8).  Writes and
         returns X [n, >= 3 + 4W] float64 (columns in `input_features` order) unless the
-        terminal half goes to term_records [n, W] int64 (count records)."""
+        terminal half goes to term_records [n, W] int64 (count records) and the customer half
+        to the planes cust_nb [W, n] int32 / cust_sum [W, n] float64 (rolling SUM; the scoring
+        layout of ops.forest_prepare_grouped with val_is_sum) -- then X is None."""
         ops._dev(ts, torch.int64, "ts")
         n = ts.numel()
         if n > self.max_batch:
@@ -75,14 +77,25 @@ class StreamState:
                 if t.numel() != n:
                     raise FdxError(f"{name} has {t.numel()} rows, ts has {n}")
         W = self.W
-        if X is None and (customer is not None or term_records is None):
+        if (cust_nb is None) != (cust_sum is None):
+            raise FdxError("cust_nb and cust_sum go together")
+        if cust_nb is not None:
+            ops._dev(cust_nb, torch.int32, "cust_nb")
+            ops._dev(cust_sum, torch.float64, "cust_sum")
+            if cust_nb.numel() < W * n or cust_sum.numel() < W * n or not (cust_nb.is_contiguous()
+                                                                           and cust_sum.is_contiguous()):
+                raise FdxError(f"cust_nb / cust_sum need {W} x {n} contiguous elements")
+        cust_planes = customer is not None and cust_nb is not None
+        if X is None and ((customer is not None and not cust_planes) or (terminal is not None
+                                                                         and term_records is None)):
             X = torch.empty((n, 3 + 4 * W), dtype=torch.float64, device=ts.device)
         if X is not None and (X.dtype != torch.float64 or X.stride(1) != 1):
             raise FdxError("X must be float64 with unit column stride")
         check(_lib.load().fdx_stream_update(self._h, ops._ptr(ts), ops._ptr(customer), ops._ptr(amount),
                                             ops._ptr(terminal), ops._ptr(fraud), n, ops._ptr(X),
                                             X.stride(0) if X is not None else 0, int(term_col0),
-                                            ops._ptr(term_records), ops._s(stream)), "fdx_stream_update")
+                                            ops._ptr(cust_nb), ops._ptr(cust_sum), ops._ptr(term_records),
+                                            ops._s(stream)), "fdx_stream_update")
         return X
 
     def check(self, stream=None):
@@ -98,7 +111,7 @@ class StreamScorer:
 
     def __init__(self, forest: ops.Forest, n_customers: int, n_terminals: int, windows_days=(1, 7, 30),
                  delay_days=7, customer_ring=256, terminal_ring=256, max_batch=65536,
-                 flags_mode=_lib.FDX_FLAGS_NOTEBOOK):
+                 flags_mode=_lib.FDX_FLAGS_NOTEBOOK, fused=True):
         self.forest = forest
         self.state = StreamState(n_customers, n_terminals, windows_days, delay_days, customer_ring, terminal_ring,
                                  max_batch, flags_mode)
@@ -106,15 +119,31 @@ class StreamScorer:
         if forest.n_features != 3 + 4 * W:
             raise FdxError(f"forest has {forest.n_features} features, the stream makes {3 + 4 * W}")
         dev = self.state.device
-        self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
+        self.flags_mode = int(flags_mode)
+        self.fused = fused
+        if fused:  # state kernels -> NB / SUM planes + count records -> scoring rows (no X matrix)
+            self.cnb = torch.empty(W * max_batch, dtype=torch.int32, device=dev)
+            self.csum = torch.empty(W * max_batch, dtype=torch.float64, device=dev)
+            self.trec = torch.empty(max_batch * W, dtype=torch.int64, device=dev)
+        else:
+            self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
         self.ws = ops.workspace(forest.workspace_size_max(max_batch), dev)
         self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
 
     def score(self, ts, customer, amount, terminal, fraud):
         """-> predict_proba[:, 1] of the batch (device view, valid until the next call)."""
         n = ts.numel()
-        X = self.state.update(ts, customer, amount, terminal, fraud, X=self.X[:n])
-        return self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+        if not self.fused:
+            X = self.state.update(ts, customer, amount, terminal, fraud, X=self.X[:n])
+            return self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+        W = self.state.W
+        cnb, csum = self.cnb[:W * n].view(W, n), self.csum[:W * n].view(W, n)
+        trec = self.trec[:n * W].view(n, W)
+        self.state.update(ts, customer, amount, terminal, fraud, term_records=trec, cust_nb=cnb, cust_sum=csum)
+        # flags (from ts), averages = SUM / NB, risks = FRAUD / NB, scaling, threshold ranks
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, ts, amount, cnb, csum, None, None, trec, self.ws,
+                                   n=n, val_is_sum=True)
+        return ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
 
 
 def stream_terminal_exchange(K, records, ts, terminal, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
@@ -149,7 +178,9 @@ class ShardedStreamScorer:
         self.windows_days, self.delay_days = self.state.windows_days, int(delay_days)
         W = self.state.W
         dev = self.state.device
-        self.X = torch.empty((max_batch, 3 + 4 * W), dtype=torch.float64, device=dev)
+        self.flags_mode = int(flags_mode)
+        self.cnb = torch.empty(W * max_batch, dtype=torch.int32, device=dev)
+        self.csum = torch.empty(W * max_batch, dtype=torch.float64, device=dev)
         self.ws = ops.workspace(forest.workspace_size_max(max_batch), dev)
         self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
 
@@ -165,9 +196,13 @@ class ShardedStreamScorer:
         W = self.state.W
         K = D.GpuKernels
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, self.customer_base) if self.customer_base else customer
-        X = self.state.update(ts, cust, amount, X=self.X[:n])            # customer half, local
+        cnb, csum = self.cnb[:W * n].view(W, n), self.csum[:W * n].view(W, n)
+        self.state.update(ts, cust, amount, cust_nb=cnb, cust_sum=csum)  # customer half, local
         back, send_perm = stream_terminal_exchange(K, self._owner_records, ts, terminal, fraud, self.world,
                                                    self.n_terminals_total, self.windows_days, self.delay_days,
                                                    self.group)
-        K.reply_assemble(back, send_perm, W, X, 3 + 2 * W)
-        return self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+        # row r's count record is back[inv[r]] (send order -> row order through the inverse)
+        inv = ops.invert_perm(send_perm)
+        ops.forest_prepare_grouped(self.forest, self.flags_mode, ts, amount, cnb, csum, None, inv, back, self.ws,
+                                   n=n, val_is_sum=True)
+        return ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])

@@ -57,6 +57,37 @@ def test_stream_matches_reference_golden(dev, golden, batch):
         np.testing.assert_array_equal(X[:, j], g[c].astype(np.float64), err_msg=c)
 
 
+@pytest.mark.parametrize("batch", [1000, 1 << 20])
+def test_stream_planes_match_reference_golden(dev, golden, batch):
+    """The scoring-layout outputs (NB / SUM planes, count records; no X matrix) hold the same
+    features: NB_w, SUM_w / NB_w = AVG_w, FRAUD_w / NB_w = RISK_w (0 when NB_w = 0)."""
+    g, cols = _golden_cols(golden)
+    n = len(cols["ts"])
+    st = StreamState(int(cols["customer"].max()) + 1, int(cols["terminal"].max()) + 1, max_batch=min(batch, n))
+    W = st.W
+    nb, sm, rec = np.empty((W, n), np.int32), np.empty((W, n)), np.empty((n, W), np.int64)
+    for a in range(0, n, batch):
+        b = min(a + batch, n)
+        m = b - a
+        cnb = torch.empty((W, m), dtype=torch.int32, device=dev)
+        csum = torch.empty((W, m), dtype=torch.float64, device=dev)
+        trec = torch.empty((m, W), dtype=torch.int64, device=dev)
+        x = st.update(T(cols["ts"][a:b], torch.int64, dev), T(cols["customer"][a:b], torch.int32, dev),
+                      T(cols["amount"][a:b], torch.float64, dev), T(cols["terminal"][a:b], torch.int32, dev),
+                      T(cols["fraud"][a:b], torch.uint8, dev), term_records=trec, cust_nb=cnb, cust_sum=csum)
+        assert x is None
+        nb[:, a:b], sm[:, a:b], rec[a:b] = cnb.cpu().numpy(), csum.cpu().numpy(), trec.cpu().numpy()
+    st.check()
+    tnb, tfr = rec & 0xFFFFFFFF, rec >> 32
+    for w, d in enumerate((1, 7, 30)):
+        np.testing.assert_array_equal(nb[w], g[f"CUSTOMER_ID_NB_TX_{d}DAY_WINDOW"])
+        np.testing.assert_array_equal(sm[w] / nb[w], g[f"CUSTOMER_ID_AVG_AMOUNT_{d}DAY_WINDOW"])
+        np.testing.assert_array_equal(tnb[:, w], g[f"TERMINAL_ID_NB_TX_{d}DAY_WINDOW"])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            risk = np.where(tnb[:, w] > 0, tfr[:, w] / tnb[:, w], 0.0)
+        np.testing.assert_array_equal(risk, g[f"TERMINAL_ID_RISK_{d}DAY_WINDOW"])
+
+
 @pytest.mark.parametrize("windows,delay,seed", [((1, 7, 30), 7, 0), ((2, 5), 3, 1), ((3,), 1, 2),
                                                 ((1, 2, 4, 8, 16, 32), 7, 3)])
 def test_stream_random_batches_vs_oracle(dev, windows, delay, seed):
@@ -132,11 +163,13 @@ def _forest(golden):
     return ops.Forest(arrays, 15, z["mean"], z["scale"])
 
 
-def test_stream_scorer_equals_batch_scoring(dev, golden):
+@pytest.mark.parametrize("fused", [True, False])
+def test_stream_scorer_equals_batch_scoring(dev, golden, fused):
     g, cols = _golden_cols(golden)
     n = len(cols["ts"])
     forest = _forest(golden)
-    sc = StreamScorer(forest, int(cols["customer"].max()) + 1, int(cols["terminal"].max()) + 1, max_batch=2048)
+    sc = StreamScorer(forest, int(cols["customer"].max()) + 1, int(cols["terminal"].max()) + 1, max_batch=2048,
+                      fused=fused)
     got = np.empty(n)
     for a in range(0, n, 2048):
         b = min(a + 2048, n)
