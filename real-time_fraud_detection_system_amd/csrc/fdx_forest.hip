@@ -514,6 +514,175 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     }
 }
 
+// k_zfill_grouped for the reference's layout (W = 3, rank rows, ratio table, 16-float search
+// segments), restructured for memory-level parallelism.  The general kernel is bound by
+// dependent round trips per row at 3 waves/SIMD (cust_perm -> term record -> ratio table;
+// amount/average -> one search segment per feature, each behind its own branch).  Here the
+// next row's loads (scoring-order columns + its term record, whose row index is fetched two
+// rows ahead) are in flight while the current row is ranked, and the current row's four
+// segment reads and three ratio-table reads are issued together, unconditionally (clamped
+// addresses; the host pads useg by one segment), so a row costs about one round trip.
+// Results are bit-identical to k_zfill_grouped<16, true> (same arithmetic, same fallbacks).
+struct PrepRow {
+    int64_t t;
+    double a;
+    int32_t c[3];
+    double cv[3];
+    int64_t tw[3];
+    int32_t r;
+};
+
+__global__ void __launch_bounds__(256) k_zfill_grouped_w3(
+    const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
+    const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
+    const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
+    const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
+    int32_t *__restrict__ nan_flag, RankTab rt) {
+    constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
+    constexpr int W = 3, nf = 15;
+    constexpr int kFix[4] = {0, 4, 6, 8};  // amount + the three averages: searched
+    __shared__ float s_smp[kMaxRankSamples];
+    __shared__ uint16_t s_itab[16 * kIntTab];
+    for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
+    stage_samples(s_smp, rt);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    auto row_of = [&](int64_t j) -> int32_t { return j < n ? (cust_perm ? cust_perm[j] : (int32_t)j) : -1; };
+    auto load = [&](int64_t j, int32_t r, PrepRow &L) {
+        L.r = r;
+        if (j >= n || r < 0) return;
+        L.t = cts[j];
+        L.a = camt[j];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            L.c[w] = cnb[(int64_t)w * n + j];
+            L.cv[w] = cval[(int64_t)w * n + j];
+        }
+        const int64_t q_ = (val_is_sum & 2) ? j : (term_inv ? term_inv[r] : r);
+#pragma unroll
+        for (int w = 0; w < W; ++w) L.tw[w] = term_rec[q_ * W + w];
+    };
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    PrepRow cur;
+    load(i, row_of(i), cur);
+    int32_t r_next = row_of(i + stride);
+    for (; i < n; i += stride) {
+        PrepRow nxt;
+        load(i + stride, r_next, nxt);  // next row's loads in flight during this row
+        r_next = row_of(i + 2 * stride);
+        if (cur.r < 0) {  // padding slot of the interleaved layout
+            uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
+            dst[0] = make_uint4(0, 0, 0, 0);
+            dst[1] = make_uint4(0, 0, 0, 0);
+            cur = nxt;
+            continue;
+        }
+        const int64_t t = cur.t;
+        int64_t day = t / kDay;
+        if (t % kDay != 0 && t < 0) --day;
+        const int64_t hour = (t - day * kDay) / kHour;
+        int64_t wd = (day + 3) % 7;
+        if (wd < 0) wd += 7;
+        const bool we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
+        const bool ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+        float v[16];
+        uint32_t q[16];
+#pragma unroll
+        for (int f = 0; f < 16; ++f) {
+            v[f] = 0.0f;
+            q[f] = 0u;
+        }
+        uint32_t need = 0u;
+        auto count = [&](int f, int32_t c) {
+            if (c >= 0 && c < kIntTab) {
+                q[f] = s_itab[f * kIntTab + c];
+            } else {
+                v[f] = zval((double)c, mean, scale, f);
+                need |= 1u << f;
+            }
+        };
+        q[1] = s_itab[1 * kIntTab + (we ? 1 : 0)];
+        q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
+        v[0] = zval(cur.a, mean, scale, 0);
+        bool nan = v[0] != v[0];
+        uint16_t rq[W];
+        bool rat_ok[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const int32_t c = cur.c[w];
+            count(3 + 2 * w, c);
+            v[4 + 2 * w] = zval((val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w], mean, scale, 4 + 2 * w);
+            nan |= v[4 + 2 * w] != v[4 + 2 * w];
+            const int64_t tw = cur.tw[w];
+            const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
+            count(3 + 2 * W + 2 * w, tnb);
+            const int fr_ = 4 + 2 * W + 2 * w;
+            rat_ok[w] = tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb;
+            // unconditional read (index clamped to 0 when the table does not apply)
+            rq[w] = rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
+        }
+        // two-level search of the 4 continuous features: LDS samples, then all segments at once
+        int32_t lo[4], cnt[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            lo[s] = rt.soff[kFix[s]];
+            cnt[s] = rt.scnt[kFix[s]];
+        }
+        int32_t nmax = max(max(cnt[0], cnt[1]), max(cnt[2], cnt[3]));
+        while (nmax > 1) {
+            nmax = 0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (cnt[s] > 1) {
+                    const int32_t h = cnt[s] >> 1;
+                    lo[s] = (s_smp[lo[s] + h] < v[kFix[s]]) ? lo[s] + h : lo[s];
+                    cnt[s] -= h;
+                }
+                nmax = max(nmax, cnt[s]);
+            }
+        }
+        int32_t cs[4];
+        float4 sg[4][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int f = kFix[s];
+            cs[s] = cnt[s] > 0 ? lo[s] - rt.soff[f] + (s_smp[lo[s]] < v[f] ? 1 : 0) : 0;
+            const float4 *p = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)max(cs[s] - 1, 0) * 16);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sg[s][k] = p[k];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int f = kFix[s];
+            uint32_t k = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                k += (uint32_t)(sg[s][e].x < v[f]) + (uint32_t)(sg[s][e].y < v[f]) + (uint32_t)(sg[s][e].z < v[f]) +
+                     (uint32_t)(sg[s][e].w < v[f]);
+            const uint32_t r = cs[s] > 0 ? (uint32_t)(cs[s] - 1) * 16u + k : 0u;
+            q[f] = v[f] != v[f] ? 0xFFFFu : r;
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const int fr_ = 4 + 2 * W + 2 * w;
+            if (rat_ok[w]) {
+                q[fr_] = rq[w];
+            } else {
+                v[fr_] = zval(term_risk(cur.tw[w]), mean, scale, fr_);
+                need |= 1u << fr_;
+                nan |= v[fr_] != v[fr_];
+            }
+        }
+        if (nan) *nan_flag = 1;
+        need &= (1u << nf) - 1u;
+        if (__any(need != 0)) rank_row(v, nf, rt, s_smp, q, need);  // table overflows (rare)
+        q[15] = 0u;
+        uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
+        dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
+        dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
+        cur = nxt;
+    }
+}
+
 template <bool LDS>
 __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char *gbase, uint32_t byte_off) {
     if (LDS) return *reinterpret_cast<const uint64_t *>(reinterpret_cast<const char *>(s_nodes) + byte_off);
@@ -1577,7 +1746,9 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
             for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
         }
         F->rnsmp = (int32_t)smp.size();
-        if (useg.empty()) useg.push_back(INFINITY);
+        // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every
+        // searched feature unconditionally (a feature without thresholds points here)
+        for (int j = 0; j < 16; ++j) useg.push_back(INFINITY);
         if (smp.empty()) smp.push_back(INFINITY);
         // integer rank table: the same float64 scaling and float32 cast as zval(), then the
         // lower_bound the device search computes (bit-identical arithmetic on the host)
@@ -2028,6 +2199,15 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
+    static const bool generic = getenv("FDX_PREP_GENERIC") != nullptr;  // A/B switch
+    const RankTab rt = rank_tab(F);
+    if (!generic && rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat) {
+        hipLaunchKernelGGL(k_zfill_grouped_w3, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
+                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,
+                           F->mean_d, F->scale_d, (void *)z, flag, rt);
+        FDX_LAUNCHED("k_zfill_grouped_w3");
+        return FDX_OK;
+    }
     FDX_PREP(k_zfill_grouped, dim3(grid), st, cust_ts_d, cust_amount_d, cust_nb_d, cust_avg_d, cust_perm_d,
              term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum, F->mean_d, F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill_grouped");
