@@ -23,6 +23,30 @@ sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
 
 METRIC = "transactions/sec featurized+scored (1/2/4/8 GPU) + % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# LDS-issue roofline of the forest walk: a node step = 2 dependent ds_read (node word + the
+# row's feature rank), each 2 LDS-array cycles per wave64 instruction (MI355X_MICROARCH.md
+# §LDS table, ds_read_b32); one LDS-array cycle per clock per CU, 256 CUs at 2.4 GHz
+LDS_PEAK_STEPS = 256 * 2.4e9 / 4 * 64
+
+
+def walk_steps_per_row(arrays):
+    """Steps a row's walks take at most: sum over trees of the tree's max leaf depth (the
+    rank walk runs a tree group to its deepest leaf, with a wave-wide early exit every 4 steps
+    once all chains sit at leaves -- so this is an upper bound of the executed steps)."""
+    import numpy as np
+
+    left, right, off = arrays["left"], arrays["right"], arrays["node_offsets"]
+    total = 0
+    for t in range(len(off) - 1):
+        lo, hi = int(off[t]), int(off[t + 1])
+        d = np.zeros(hi - lo, dtype=np.int32)
+        lt, rt = left[lo:hi], right[lo:hi]
+        for i in range(hi - lo):  # pre-order: a parent precedes its children
+            if lt[i] >= 0:
+                d[lt[i]] = d[i] + 1
+                d[rt[i]] = d[i] + 1
+        total += int(d.max())
+    return total
 # algorithmic bytes per row of the forest launches (DESIGN.md §4): every launch reads the row
 # (rank layout: 16 x u16 = 32 B; wide layout: 16 x float32 = 64 B), the running float64 sum
 # crosses launches (8 B in, 8 B out except the first / last), the last launch writes proba.
@@ -230,6 +254,13 @@ def main():
                      "forest_variant": fvar,
                      "bytes_per_row_per_launch": round(bpr / forest.n_chunks, 2)},
     }
+    steps = walk_steps_per_row(arrays)
+    ach_steps = steps * n_local / (trav_ms * 1e-3)
+    out["roofline_lds"] = {"kernel": out["roofline"]["kernel"], "bound": "lds", "unit": "node steps/s",
+                           "achieved": float(f"{ach_steps:.4g}"), "peak": float(f"{LDS_PEAK_STEPS:.4g}"),
+                           "frac": round(ach_steps / LDS_PEAK_STEPS, 4), "node_steps_per_row_max": steps,
+                           "note": "2 ds_read per step at 2 LDS cycles each; steps = sum of tree depths (upper "
+                                   "bound: wave-wide early exit), so frac is an upper bound"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, args.cpu_sample_customers)
     if args.sweep_slab and rank == 0:
