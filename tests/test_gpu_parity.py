@@ -374,3 +374,34 @@ def test_layout_starts_walk_equals_interleaved(dev):
     valid = (lay.irow[:n] >= 0).cpu().numpy()
     np.testing.assert_array_equal(nb.cpu().numpy()[:, valid], nb_ref.cpu().numpy()[:, valid])
     np.testing.assert_array_equal(sm.cpu().numpy()[:, valid], sm_ref.cpu().numpy()[:, valid])
+
+
+def test_fused_scoring_rank_table_overflows(dev):
+    """The scoring-row assembly of the fused path (k_zfill_grouped_w3: integer rank table for
+    counts < 256, ratio table for terminal windows with NB < 128, searched otherwise) scores
+    bit-identically to the float64-X path (full two-level search of every feature) when
+    customer counts reach >= 256 and terminal counts >= 128, with thresholds placed there."""
+    from fdx import synth
+
+    d = synth.generate(n_customers=400, n_terminals=500, nb_days=60, seed=41)
+    rng = np.random.default_rng(3)
+    cust, term = d["customer"].copy(), d["terminal"].copy()
+    day = d["ts"] // DAY
+    cust[rng.choice(np.flatnonzero((day >= 10) & (day < 40)), 700, replace=False)] = 0
+    term[rng.choice(np.flatnonzero((day >= 5) & (day < 45)), 900, replace=False)] = 0
+    arrays = random_forest(np.random.default_rng(5), 12, 9)
+    mean = np.array([50, .5, .5, 2, 50, 10, 50, 280, 50, 20, .1, 130, .1, 150, .1], np.float64)
+    scale = np.array([30, .5, .5, 2, 30, 10, 30, 30, 30, 10, .1, 20, .1, 20, .1], np.float64)
+    forest = ops.Forest(arrays, 15, mean, scale)
+    args = (T(d["ts"], torch.int64, dev), T(cust, torch.int32, dev), T(term, torch.int32, dev),
+            T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    n = len(d["ts"])
+    pipe = FraudPipeline(forest=forest)
+    f, p_ref = pipe.run(*args, 400, 500)
+    X = f.X.cpu().numpy()
+    assert X[:, 7].max() >= 256 and X[:, 13].max() >= 128  # both table overflows occur
+    ws = ops.workspace(forest.workspace_size(n), dev)
+    p1 = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 400, 500, p1, ws)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p_ref.cpu().numpy())
+    np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
