@@ -386,7 +386,7 @@ def test_fused_scoring_rank_table_overflows(dev):
     d = synth.generate(n_customers=400, n_terminals=500, nb_days=60, seed=41)
     rng = np.random.default_rng(3)
     cust, term = d["customer"].copy(), d["terminal"].copy()
-    day = d["ts"] // DAY
+    day = (d["ts"] - d["ts"].min()) // DAY
     cust[rng.choice(np.flatnonzero((day >= 10) & (day < 40)), 700, replace=False)] = 0
     term[rng.choice(np.flatnonzero((day >= 5) & (day < 45)), 900, replace=False)] = 0
     arrays = random_forest(np.random.default_rng(5), 12, 9)
