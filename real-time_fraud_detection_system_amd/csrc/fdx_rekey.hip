@@ -17,8 +17,8 @@
 namespace fdx {
 namespace {
 
-constexpr int kRadixBits = 8;
-constexpr int kBins = 1 << kRadixBits;
+constexpr int kRadixBits = 8;   // default digit; 9-bit digits when they save a pass (17-18-bit keys)
+constexpr int kMaxBins = 512;
 constexpr int kBlock = 256;
 constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096 keys per tile
@@ -122,15 +122,16 @@ int exclusive_scan(uint32_t *data, int64_t m, uint32_t *part, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------- radix passes
-template <typename K>
+template <typename K, int BITS>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
-    return (uint32_t)(((k ^ flip) >> shift) & (K)(kBins - 1));
+    return (uint32_t)(((k ^ flip) >> shift) & (K)((1 << BITS) - 1));
 }
 
-template <typename K>
+template <typename K, int BITS>
 __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ keys, int64_t n, int shift,
                                                        K flip, int64_t n_tiles,
                                                        uint32_t *__restrict__ hist) {
+    constexpr int kBins = 1 << BITS;
     __shared__ uint32_t s_h[kBins];
     for (int d = threadIdx.x; d < kBins; d += kBlock) s_h[d] = 0;
     __syncthreads();
@@ -138,18 +139,20 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         int64_t i = base + (int64_t)k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&s_h[digit_of(keys[i], shift, flip)], 1u);
+        if (i < n) atomicAdd(&s_h[digit_of<K, BITS>(keys[i], shift, flip)], 1u);
     }
     __syncthreads();
     for (int d = threadIdx.x; d < kBins; d += kBlock) hist[(int64_t)d * n_tiles + blockIdx.x] = s_h[d];
 }
 
 // Stable scatter of one tile.  vals_in == nullptr means "the value is the row index".
-template <typename K>
+template <typename K, int BITS>
 __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
     int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
     uint32_t *__restrict__ vals_out) {
+    constexpr int kBins = 1 << BITS, kPer = kBins / kBlock;
+    static_assert(kBins % kBlock == 0, "digit bins must be a multiple of the block");
     __shared__ uint32_t s_run[kBins];                  // digit counts of earlier rounds
     __shared__ uint32_t s_wcnt[kWavesPerBlock][kBins]; // this round's per-wave counts
     __shared__ uint32_t s_start[kBins];                // tile-local digit starts
@@ -174,11 +177,11 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         const bool valid = i < n;
         key[r] = valid ? keys_in[i] : (K)0;
         val[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-        const uint32_t d = digit_of(key[r], shift, flip);
+        const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
         // peers: lanes of this wave holding the same digit (wave multisplit by ballots)
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < kRadixBits; ++b) {
+        for (int b = 0; b < BITS; ++b) {
             const bool bit = (d >> b) & 1u;
             const uint64_t bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
@@ -203,18 +206,29 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         }
         __syncthreads();
     }
-    // tile-local digit starts = exclusive scan of s_run over digits (kBins == kBlock)
+    // tile-local digit starts = exclusive scan of s_run over digits (kPer consecutive
+    // digits per thread)
     {
+        uint32_t c[kPer], sum = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            c[q] = s_run[tid * kPer + q];
+            sum += c[q];
+        }
         uint32_t tot;
-        uint32_t ex = block_excl_scan(s_run[tid], &tot);
-        s_start[tid] = ex;
+        uint32_t ex = block_excl_scan(sum, &tot);
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            s_start[tid * kPer + q] = ex;
+            ex += c[q];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const int64_t i = base + (int64_t)r * kBlock + tid;
         if (i < n) {
-            const uint32_t d = digit_of(key[r], shift, flip);
+            const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
             const uint32_t p = s_start[d] + rank[r];
             s_key[p] = key[r];
             s_val[p] = val[r];
@@ -224,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     const int64_t cnt = std::min<int64_t>(kTile, n - base);
     for (int p = tid; p < cnt; p += kBlock) {
         const K k = s_key[p];
-        const uint32_t d = digit_of(k, shift, flip);
+        const uint32_t d = digit_of<K, BITS>(k, shift, flip);
         const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
         keys_out[dst] = k;
         vals_out[dst] = s_val[p];
@@ -293,7 +307,7 @@ struct SortWs {
 template <typename K>
 size_t sort_ws(int64_t n, SortWs<K> *w, char *base) {
     const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kTile));
-    const int64_t hm = tiles * kBins;
+    const int64_t hm = tiles * kMaxBins;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char *p = base ? base + off : nullptr;
@@ -318,7 +332,10 @@ template <typename K>
 int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t *vals_out,
                const SortWs<K> &w, hipStream_t st, const K **sorted) {
     const int64_t tiles = ceil_div(n, kTile);
-    const int passes = (bits + kRadixBits - 1) / kRadixBits;
+    // 9-bit digits when they need fewer passes than 8-bit ones (17- and 18-bit keys: 2, not 3)
+    static const bool only8 = getenv("FDX_RADIX_8BIT") != nullptr;  // A/B switch
+    const int dbits = (!only8 && (bits + 8) / 9 < (bits + kRadixBits - 1) / kRadixBits) ? 9 : kRadixBits;
+    const int passes = (bits + dbits - 1) / dbits;
     const K *kin = keys;
     const uint32_t *vin = nullptr;  // identity on the first pass
     if (passes == 0) {
@@ -328,18 +345,26 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         return FDX_OK;
     }
     for (int p = 0; p < passes; ++p) {
-        const int shift = p * kRadixBits;
+        const int shift = p * dbits;
         const bool last = p == passes - 1;
         K *kout = (p & 1) ? w.k1 : w.k0;
         if (last && keys_out) kout = keys_out;
         uint32_t *vout = last ? vals_out : ((p & 1) ? w.v1 : w.v0);
-        hipLaunchKernelGGL(k_radix_hist<K>, dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
-                           tiles, w.hist);
+        if (dbits == 9)
+            hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
+                               tiles, w.hist);
+        else
+            hipLaunchKernelGGL((k_radix_hist<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n,
+                               shift, flip, tiles, w.hist);
         FDX_LAUNCHED("k_radix_hist");
-        int rc = exclusive_scan(w.hist, tiles * kBins, w.part, st);
+        int rc = exclusive_scan(w.hist, tiles * ((int64_t)1 << dbits), w.part, st);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_radix_scatter<K>, dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n, shift,
-                           flip, tiles, w.hist, kout, vout);
+        if (dbits == 9)
+            hipLaunchKernelGGL((k_radix_scatter<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
+                               shift, flip, tiles, w.hist, kout, vout);
+        else
+            hipLaunchKernelGGL((k_radix_scatter<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin,
+                               n, shift, flip, tiles, w.hist, kout, vout);
         FDX_LAUNCHED("k_radix_scatter");
         kin = kout;
         vin = vout;
