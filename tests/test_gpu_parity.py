@@ -41,7 +41,8 @@ def test_time_flags(dev, n):
 
 # ---------------------------------------------------------------------------- re-key
 @pytest.mark.parametrize("n,n_keys", [(0, 5), (1, 1), (5000, 1), (4096, 256), (4097, 257),
-                                      (100_000, 50_000), (300_001, 100_000), (2_000_000, 1 << 21)])
+                                      (100_000, 50_000), (300_001, 100_000), (2_000_000, 1 << 21),
+                                      (200_000, 1 << 18), (70_000, 1 << 25)])  # 9-bit digits: 2 and 3 passes
 def test_rekey_stable(dev, n, n_keys):
     rng = np.random.default_rng(n + n_keys)
     keys = rng.integers(0, n_keys, size=n).astype(np.int32)
