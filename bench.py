@@ -1,20 +1,30 @@
 """Headline benchmark: transactions/s featurized + scored, and % of the HBM roofline.
 
 A step = one pass of the hot path over one batch already resident in HBM:
-  time flags -> re-key by CUSTOMER_ID -> customer 1/7/30-day windows -> re-key by
-  TERMINAL_ID -> terminal delayed-risk windows -> assemble the 15 input_features ->
-  StandardScaler + RandomForest(100 trees, depth 20) predict_proba.
+  re-key by CUSTOMER_ID -> customer 1/7/30-day windows -> re-key by TERMINAL_ID ->
+  terminal delayed-risk windows -> time flags + assemble the 15 input_features +
+  StandardScaler -> RandomForest(100 trees, depth 20) predict_proba.
 Workload per GPU (BASELINE.json configs[1]): 50k customers / 100k terminals / 183 days
 (~17.7M tx), synthetic data from the handbook distributions (fdx.synth), scored with the
 config-3 model (bench_assets/rf100_d20.npz, trained with sklearn on config-1 features).
 
-N GPUs (torch.distributed.run, one process per GPU): weak scaling, each rank owns its own
-50k customers; terminals are shared ids hashed to owner ranks and the terminal half runs
-after an RCCL all-to-all re-key (fdx.distributed).  Rank 0 prints one JSON line.
+N GPUs: one process per GPU.  Launched by torch.distributed.run (RANK / WORLD_SIZE set) or,
+when `--gpus N > 1` is given without WORLD_SIZE, this script starts the N ranks itself
+(child processes, before anything touches the GPU) and exits with their status.  Weak
+scaling: each rank owns its own 50k customers (a contiguous CUSTOMER_ID range); terminals
+are shared ids hashed to owner ranks and the terminal half runs after an RCCL all-to-all
+re-key (fdx.distributed).  Rank 0 prints one JSON line.
+
+Per-kernel roofline: every stage of a step is bracketed by HIP events on
+the stream it runs on, inside the timed steps; the JSON line carries, per stage, the
+§8(d) algorithmic bytes per transaction, the mean time, the achieved GB/s and its fraction
+of the 8 TB/s HBM peak, plus the HBM traffic rocprofv3 measured for its kernels
+(profiles/pmc_kernels.json) when that file covers them.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,6 +37,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # row's feature rank), each 2 LDS-array cycles per wave64 instruction (MI355X_MICROARCH.md
 # §LDS table, ds_read_b32); one LDS-array cycle per clock per CU, 256 CUs at 2.4 GHz
 LDS_PEAK_STEPS = 256 * 2.4e9 / 4 * 64
+
+# SURVEY.md §8(d) algorithmic bytes per transaction (compact logical I/O, read once + write once)
+ALG = {"K2": 30, "K1-cust": 58, "K1-term": 49, "K3": 90, "end-to-end": 107}
+# bench stages (marks of FraudPipeline.run_fused) -> §8(d) unit and the kernels they launch
+# (substring of the rocprofv3 kernel name, dispatches per step; "chunks" = forest chunks)
+STAGES = [
+    ("rekey_customer", "K2", [("k_radix_hist<unsigned int, 8>", 2), ("k_radix_scatter<unsigned int, 8>", 2)]),
+    ("customer_layout", "K1-cust", [("k_interleave<true>", 1)]),
+    ("customer_walk", "K1-cust", [("k_customer_walk", 1)]),
+    ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 2), ("k_radix_scatter<unsigned int, 9>", 2)]),
+    ("terminal_windows", "K1-term", [("k_terminal<false>", 1)]),
+    ("assemble_rows", "K3", [("k_zfill_grouped_w3", 1)]),
+    ("forest_traverse", "K3", [("k_forest_rank", "chunks")]),
+]
 
 
 def walk_steps_per_row(arrays):
@@ -47,30 +71,18 @@ def walk_steps_per_row(arrays):
                 d[rt[i]] = d[i] + 1
         total += int(d.max())
     return total
-# algorithmic bytes per row of the forest launches: every launch reads the row
-# (rank layout: 16 x u16 = 32 B; wide layout: 16 x float32 = 64 B), the running float64 sum
-# crosses launches (8 B in, 8 B out except the first / last), the last launch writes proba.
-RANK_ROW_BYTES, WIDE_ROW_BYTES = 32, 64
-# (16 x 4 B slots) in + running float64 sum in + float64 sum/proba out
 
 
-def forest_bytes_per_row(variant, n_chunks):
-    row = RANK_ROW_BYTES if variant >= 16 else WIDE_ROW_BYTES
-    return row * n_chunks + 16 * (n_chunks - 1) + 8
-
-
-def pmc_traffic(variant):
-    """HBM bytes per forest launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_forest.json, FETCH_SIZE/WRITE_SIZE passes corrected as MI355X_MICROARCH.md
-    prescribes) when it was measured on this traversal variant; else (None, None)."""
-    p = os.path.join(ROOT, "profiles", "pmc_forest.json")
+def pmc_table():
+    """{kernel name: HBM bytes per dispatch} from the committed rocprofv3 PMC summary
+    (FETCH_SIZE / WRITE_SIZE passes; correction as stated in that file), or {}."""
+    p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     if not os.path.exists(p):
-        return None, None
+        return {}, None
     with open(p) as f:
         d = json.load(f)
-    if d.get("variant") != variant:
-        return None, None
-    return d["hbm_bytes_per_launch"], d["source"]
+    return {k: v["hbm_bytes_per_dispatch"] for k, v in d["kernels"].items() if "hbm_bytes_per_dispatch" in v}, \
+        d.get("source")
 
 
 def parse():
@@ -83,16 +95,34 @@ def parse():
     ap.add_argument("--days", type=int, default=183)
     ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-customers", type=int, default=2500)
-    ap.add_argument("--breakdown", action="store_true", help="per-stage HIP-event times to stderr")
-    ap.add_argument("--slab-rows", type=int, default=0, help="forest traversal slab rows (0 = all rows)")
-    ap.add_argument("--sweep-slab", default="", help="comma list of slab sizes to time (stderr)")
+    ap.add_argument("--cpu-score-rows", type=int, default=200_000,
+                    help="rows of the sklearn predict_proba sample in the CPU baseline")
     ap.add_argument("--forest-variant", type=int, default=-1,
                     help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
+
+
+def spawn_ranks(n):
+    """Start n ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), wait, return
+    the worst exit status.  Runs before this process touches the GPU."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, abs(p.wait()))
+    return rc
 
 
 def load_model(path):
@@ -104,29 +134,125 @@ def load_model(path):
     return arrays, z["mean"], z["scale"], z["check_X"], z["check_proba"]
 
 
-def cpu_baseline(data, arrays, mean, scale, sample_customers):
-    """The CPU oracle (C port of the reference's pandas/sklearn arithmetic, 1 thread) on a
-    bounded sample: every transaction of customers [0, sample_customers)."""
+def host_info():
+    """The GPU box's host CPUs as this process sees them."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0))
+    try:
+        import joblib
+
+        jobs = int(joblib.cpu_count())  # respects cgroup CPU quotas (the box's CPU share)
+    except Exception:  # noqa: BLE001
+        jobs = usable
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": usable, "joblib_cpus": jobs}
+
+
+def sklearn_forest(arrays, n_features=15):
+    """A fitted sklearn RandomForestClassifier rebuilt from the saved node arrays (the bench
+    model is stored as arrays, not a pickle): Tree.__setstate__ with sklearn's own node
+    record layout.  Its predict_proba[:, 1] is checked against the saved sklearn output."""
+    import numpy as np
+    import sklearn.ensemble
+    import sklearn.tree
+    from sklearn.tree._tree import Tree
+
+    off = arrays["node_offsets"]
+    ests = []
+    for t in range(len(off) - 1):
+        lo, hi = int(off[t]), int(off[t + 1])
+        n = hi - lo
+        tree = Tree(n_features, np.array([2], dtype=np.intp), 1)
+        dt = tree.__getstate__()["nodes"].dtype
+        nodes = np.zeros(n, dtype=dt)
+        nodes["left_child"] = arrays["left"][lo:hi]
+        nodes["right_child"] = arrays["right"][lo:hi]
+        leaf = nodes["left_child"] < 0
+        nodes["feature"] = np.where(leaf, -2, arrays["feature"][lo:hi])
+        nodes["threshold"] = np.where(leaf, -2.0, arrays["threshold"][lo:hi])
+        nodes["n_node_samples"] = 1
+        nodes["weighted_n_node_samples"] = 1.0
+        if "missing_go_to_left" in dt.names:
+            nodes["missing_go_to_left"] = arrays["missing_left"][lo:hi]
+        v1 = arrays["value1"][lo:hi]
+        values = np.stack([1.0 - v1, v1], axis=1).reshape(n, 1, 2)
+        depth = np.zeros(n, np.int64)
+        for i in range(n):
+            if nodes["left_child"][i] >= 0:
+                depth[nodes["left_child"][i]] = depth[nodes["right_child"][i]] = depth[i] + 1
+        tree.__setstate__({"max_depth": int(depth.max()), "node_count": n, "nodes": nodes,
+                           "values": np.ascontiguousarray(values)})
+        est = sklearn.tree.DecisionTreeClassifier()
+        est.tree_, est.n_outputs_, est.n_classes_, est.classes_ = tree, 1, 2, np.array([0, 1])
+        est.n_features_in_, est.max_features_ = n_features, n_features
+        ests.append(est)
+    rf = sklearn.ensemble.RandomForestClassifier(n_estimators=len(ests))
+    rf.estimators_, rf.n_outputs_, rf.n_classes_, rf.classes_ = ests, 1, 2, np.array([0, 1])
+    rf.n_features_in_ = n_features
+    return rf
+
+
+def cpu_baseline(data, arrays, mean, scale, check_X, check_proba, score_rows):
+    """The reference CPU path on this host, on bounded samples of the same workload:
+      featurization -- the C port of the reference's pandas arithmetic (oracle/fdx_oracle.c,
+        1 thread; FASTER than pandas' per-group apply, so a conservative baseline) over the
+        WHOLE table (customer and terminal windows see every row);
+      scoring -- scikit-learn itself (the reference's library): StandardScaler.transform +
+        RandomForest predict_proba of the bench model, n_jobs=1 and n_jobs=-1, whole batch and
+        in 10k-row Spark-UDF-shaped batches (fraud_detection.py:183-195, Arrow maxRecordsPerBatch).
+    value = 1 / (featurize s/tx + scoring s/tx at n_jobs=-1 whole batch)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
+    import sklearn.preprocessing
 
-    m = data["customer"] < sample_customers
-    s = {k: v[m] for k, v in data.items()}
+    info = host_info()
+    n = len(data["ts"])
     t0 = time.perf_counter()
-    f = oracle.featurize_arrays(s["ts"], s["customer"], s["terminal"], s["amount"], s["fraud"])
+    f = oracle.featurize_arrays(data["ts"], data["customer"], data["terminal"], data["amount"], data["fraud"])
+    t_feat = time.perf_counter() - t0
     names = ["TX_DURING_WEEKEND", "TX_DURING_NIGHT"] + oracle.CUSTOMER_COLS + oracle.TERMINAL_COLS
-    X = np.column_stack([s["amount"]] + [f[k] for k in names])
-    oracle.forest_predict(X, arrays, mean, scale)
-    dt = time.perf_counter() - t0
-    return {"value": round(len(s["ts"]) / dt, 1), "unit": "tx/s", "cores": 1, "kind": "port",
-            "sample": f"all {len(s['ts'])} tx of customers [0,{sample_customers}) of rank 0's batch: "
-                      f"flags + customer/terminal windows + scale + RF(100,d20) predict_proba, "
-                      f"C oracle (oracle/fdx_oracle.c), {dt:.1f} s"}
+    m = min(score_rows, n)
+    X = np.column_stack([data["amount"][:m]] + [f[k][:m] for k in names])
+    rf = sklearn_forest(arrays)
+    sc = sklearn.preprocessing.StandardScaler()
+    sc.mean_, sc.scale_, sc.var_ = mean, scale, scale * scale
+    sc.n_features_in_, sc.n_samples_seen_ = 15, 1
+    rf.set_params(n_jobs=1)
+    if not np.array_equal(rf.predict_proba(sc.transform(check_X))[:, 1], check_proba):
+        raise SystemExit("rebuilt sklearn forest disagrees with the saved sklearn output")
+    res = {}
+    for jobs in (1, -1):
+        rf.set_params(n_jobs=jobs)
+        t0 = time.perf_counter()
+        rf.predict_proba(sc.transform(X))
+        res[f"whole_n_jobs{jobs}"] = m / (time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        for a in range(0, m, 10_000):
+            rf.predict_proba(sc.transform(X[a:a + 10_000]))
+        res[f"udf10k_n_jobs{jobs}"] = m / (time.perf_counter() - t0)
+    feat_rate = n / t_feat
+    value = 1.0 / (1.0 / feat_rate + 1.0 / res["whole_n_jobs-1"])
+    return {"value": round(value, 1), "unit": "tx/s", "cores": info["joblib_cpus"], "kind": "port",
+            "sample": f"featurize: C port of the pandas windows (1 thread) over all {n} tx of rank 0's batch, "
+                      f"{t_feat:.1f} s; score: sklearn StandardScaler + RandomForest(100, d20) predict_proba on "
+                      f"the first {m} rows (n_jobs=-1 = {info['joblib_cpus']} threads)",
+            "featurize_tx_per_s": round(feat_rate, 1),
+            "sklearn_rows_per_s": {k: round(v, 1) for k, v in res.items()},
+            "host": info}
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -141,18 +267,20 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus, f"world {dist.get_world_size()} != --gpus {args.gpus}"
     elif args.sharded:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
-    # weak scaling: every rank adds its own customers and terminals to one shared map
+    # weak scaling: rank r owns customers [r * C, (r + 1) * C) and adds its own terminals to
+    # one shared terminal map
+    base = rank * args.customers
     data = synth.generate(args.customers, args.terminals * world, args.days, seed=1234 + rank,
-                          customer_offset=rank * args.customers)
+                          customer_offset=base)
     n_local = len(data["ts"])
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
-    forest.set_slab_rows(args.slab_rows)
     default_variant = forest.variant
     if args.forest_variant >= 0:
         forest.set_variant(args.forest_variant)
@@ -167,32 +295,34 @@ def main():
     pipe = FraudPipeline(forest=forest)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
-    ev = []
+    marks_all = []   # per timed step: [(stage, event), ...]
+    trav = []        # per timed step: (start, end) of the forest traversal
 
     if world > 1 or args.sharded:
         from fdx.distributed import ShardedPipeline
 
-        sp = ShardedPipeline(pipe, world, rank, args.terminals * world)
-        n_cust_total = args.customers * world
+        sp = ShardedPipeline(pipe, world, rank, args.terminals * world, customer_base=base,
+                             n_customers_local=args.customers)
 
         def step(record):
-            sp.run(ts, cust, term, amt, fr, n_cust_total, proba, ws, ev if record else None)
-
-        if rank == 0:
-            print(f"rank0 tx={n_local}", file=sys.stderr)
+            sp.run(ts, cust, term, amt, fr, proba, ws, trav if record else None)
     else:
+        lcust = cust  # rank 0 of a 1-GPU run: base 0
+
         def step(record):
             marks = []
 
-            def mark(i):
+            def mark(name):
                 if record:
                     e = torch.cuda.Event(enable_timing=True)
                     e.record()
-                    marks.append(e)
+                    marks.append((name, e))
 
-            pipe.run_fused(ts, cust, term, amt, fr, args.customers, args.terminals, proba, ws, on_traverse=mark)
+            mark("start")
+            pipe.run_fused(ts, lcust, term, amt, fr, args.customers, args.terminals, proba, ws, mark=mark)
             if record:
-                ev.append(tuple(marks))
+                marks_all.append(marks)
+                trav.append((marks[-2][1], marks[-1][1]))
 
     for _ in range(args.warmup):
         step(False)
@@ -218,15 +348,24 @@ def main():
     else:
         n_total = n_local
 
-    trav_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
-    slab = args.slab_rows if args.slab_rows > 0 else n_local
-    launches = forest.n_chunks * -(-n_local // slab)
-    launch_ms = trav_ms / launches
-    # every launch streams its slab's rows once: total algorithmic bytes / total time
-    fvar = forest.variant if args.forest_variant < 0 else args.forest_variant
-    bpr = forest_bytes_per_row(fvar, forest.n_chunks)
-    achieved = bpr * n_local / (trav_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(fvar)
+    trav_ms = sum(a.elapsed_time(b) for a, b in trav) / max(len(trav), 1)
+    launches = forest.n_chunks
+    fvar = forest.variant
+    # §8(d): K3 = 90 B per transaction (15 features in, proba out), over the traversal time
+    achieved = ALG["K3"] * n_local / (trav_ms * 1e-3) / 1e9
+    pmc, pmc_src = pmc_table()
+
+    def pmc_bytes(kernels):
+        tot, seen = 0.0, True
+        for sub, cnt in kernels:
+            hits = [v for k, v in pmc.items() if sub in k]
+            if not hits:
+                seen = False
+                continue
+            tot += max(hits) * (launches if cnt == "chunks" else cnt)
+        return tot if seen and pmc else None
+
+    fk = [v for k, v in pmc.items() if "k_forest_rank" in k]
     out = {
         "metric": METRIC,
         "value": round(n_total * args.steps / dt, 1),
@@ -242,42 +381,68 @@ def main():
         "data": "synthetic: handbook-distribution generator (fdx.synth, seed 1234+rank), resident in HBM",
         "config": {"workload": f"configs[1]: {args.customers} customers / {args.terminals} terminals / "
                                f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
-                   "tx_per_gpu": n_local, "global_tx": n_total, "parallelism": f"customer-sharded x{world}",
+                   "tx_per_gpu": n_local, "global_tx": n_total,
+                   "parallelism": f"customer-sharded x{world}" + (" (RCCL all-to-all re-key)" if world > 1 else ""),
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)"},
-        "roofline": {"kernel": "k_forest_rank" if fvar >= 16 else "k_forest_chunk", "bound": "hbm", "achieved": round(achieved, 1),
+        "roofline": {"kernel": "k_forest_rank", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_unit": "bytes per launch",
-                     "algorithmic_bytes_per_launch": round(bpr / forest.n_chunks * n_local),
-                     "traffic_source": traffic_src, "avg_launch_ms": round(launch_ms, 4),
-                     "launches_per_step": launches,
-                     "traverse_ms": round(trav_ms, 3),
-                     "forest_variant": fvar,
-                     "bytes_per_row_per_launch": round(bpr / forest.n_chunks, 2)},
+                     "traffic": round(max(fk)) if fk else None, "traffic_unit": "HBM bytes per launch (PMC)",
+                     "algorithmic_bytes_per_launch": round(ALG["K3"] * n_local / launches),
+                     "algorithmic_bytes_per_tx": ALG["K3"], "avg_launch_ms": round(trav_ms / launches, 4),
+                     "launches_per_step": launches, "traverse_ms": round(trav_ms, 3), "forest_variant": fvar,
+                     "traffic_source": pmc_src},
     }
-    steps = walk_steps_per_row(arrays)
-    ach_steps = steps * n_local / (trav_ms * 1e-3)
-    out["roofline_lds"] = {"kernel": out["roofline"]["kernel"], "bound": "lds", "unit": "node steps/s",
+    steps_max = walk_steps_per_row(arrays)
+    ach_steps = steps_max * n_local / (trav_ms * 1e-3)
+    out["roofline_lds"] = {"kernel": "k_forest_rank", "bound": "lds", "unit": "node steps/s",
                            "achieved": float(f"{ach_steps:.4g}"), "peak": float(f"{LDS_PEAK_STEPS:.4g}"),
-                           "frac": round(ach_steps / LDS_PEAK_STEPS, 4), "node_steps_per_row_max": steps,
+                           "frac": round(ach_steps / LDS_PEAK_STEPS, 4), "node_steps_per_row_max": steps_max,
                            "note": "2 ds_read per step at 2 LDS cycles each; steps = sum of tree depths (upper "
                                    "bound: wave-wide early exit), so frac is an upper bound"}
+    if marks_all:
+        table = []
+        names = [s for s, _, _ in STAGES]
+        for name, unit, kernels in STAGES:
+            ms = []
+            for mk in marks_all:
+                idx = {nm: i for i, (nm, _) in enumerate(mk)}
+                i = idx[name]
+                ms.append(mk[i - 1][1].elapsed_time(mk[i][1]))
+            t_ms = sum(ms) / len(ms)
+            table.append({"stage": name, "unit": unit, "ms": round(t_ms, 4),
+                          "kernels": [k for k, _ in kernels], "pmc_bytes": pmc_bytes(kernels)})
+        # §8(d) units: K1-cust = layout + walk, K3 = assemble + traverse
+        units = {}
+        for row in table:
+            u = units.setdefault(row["unit"] + ("" if row["unit"] != "K2" else ":" + row["stage"]),
+                                 {"ms": 0.0, "stages": [], "pmc": 0.0, "pmc_ok": True})
+            u["ms"] += row["ms"]
+            u["stages"].append(row["stage"])
+            if row["pmc_bytes"] is None:
+                u["pmc_ok"] = False
+            else:
+                u["pmc"] += row["pmc_bytes"]
+        krows = []
+        for key, u in units.items():
+            unit = key.split(":")[0]
+            alg = ALG[unit] * n_local
+            gbs = alg / (u["ms"] * 1e-3) / 1e9
+            krows.append({"unit": unit, "stages": u["stages"], "alg_bytes_per_tx": ALG[unit],
+                          "ms": round(u["ms"], 4), "achieved_GBs": round(gbs, 1),
+                          "frac": round(gbs / HBM_PEAK_GBS, 4),
+                          "pmc_traffic_bytes": round(u["pmc"]) if u["pmc_ok"] and pmc else None,
+                          "traffic_over_alg": round(u["pmc"] / alg, 2) if u["pmc_ok"] and pmc else None})
+        step_ms = sum(r["ms"] for r in table)
+        e2e = ALG["end-to-end"] * n_local / (step_ms * 1e-3) / 1e9
+        out["kernels"] = {"per_stage": table, "per_unit": krows, "stage_sum_ms": round(step_ms, 3),
+                          "end_to_end": {"alg_bytes_per_tx": ALG["end-to-end"], "achieved_GBs": round(e2e, 1),
+                                         "frac": round(e2e / HBM_PEAK_GBS, 4)},
+                          "note": "ms = HIP events around each stage on its stream, mean over the timed steps; "
+                                  "alg bytes = SURVEY.md §8(d) per tx x tx; pmc = rocprofv3 FETCH/WRITE per "
+                                  "dispatch x dispatches (profiles/pmc_kernels.json)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, args.cpu_sample_customers)
-    if args.sweep_slab and rank == 0:
-        res = {}
-        for sr in [int(x) for x in args.sweep_slab.split(",")]:
-            forest.set_slab_rows(sr)
-            ops.forest_traverse(forest, n_local, ws, proba)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(3):
-                ops.forest_traverse(forest, n_local, ws, proba)
-            b.record()
-            torch.cuda.synchronize()
-            res[sr] = round(a.elapsed_time(b) / 3, 3)
-        forest.set_slab_rows(args.slab_rows)
-        print(json.dumps({"slab_sweep_traverse_ms": res}), file=sys.stderr)
-    if args.sweep_variant and rank == 0:
+        out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, check_X, check_proba, args.cpu_score_rows)
+    if args.sweep_variant and rank == 0 and world == 1 and not args.sharded:
         # each variant: one full untimed pipeline pass (the prepared row format depends on
         # the layout), bit-equality of proba against the default, then 3 timed traversals
         res = {}
@@ -298,48 +463,10 @@ def main():
             res[v] = {"ms": round(a.elapsed_time(b) / 3, 3), "chunks": forest.n_chunks, "bit_equal": same}
         forest.set_variant(args.forest_variant if args.forest_variant >= 0 else default_variant)
         print(json.dumps({"variant_sweep_traverse": res}), file=sys.stderr)
-    if args.breakdown and rank == 0:
-        print(json.dumps(stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba)),
-              file=sys.stderr)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1 or args.sharded:
         dist.destroy_process_group()
-
-
-def stage_breakdown(pipe, forest, ts, cust, term, amt, fr, args, ws, proba):
-    import torch
-
-    from fdx import ops
-
-    marks = []
-
-    def mark(name):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        marks.append((name, e))
-
-    n = ts.numel()
-    mark("start")
-    cperm, cseg, _ = ops.rekey(cust, args.customers)
-    mark("rekey_customer")
-    lay = ops.customer_layout(cseg, cperm, ts, amt, 3, windows_days=(1, 7, 30))
-    mark("customer_layout")
-    inb, isum = ops.customer_windows_walk(lay, cseg)
-    mark("customer_windows")
-    tperm, tseg, _ = ops.rekey(term, args.terminals)
-    mark("rekey_terminal")
-    trec = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm)
-    mark("terminal_windows")
-    wsb = pipe._forest_ws(lay.n_slots, ws, ts.device)
-    ops.forest_prepare_grouped(forest, 0, lay.its, lay.iamt, inb, isum, lay.irow, None, trec, wsb, n=lay.n_slots,
-                               val_is_sum=True)
-    mark("assemble_scale_z32")
-    ops.forest_traverse_perm(forest, lay.n_slots, wsb, proba, lay.irow)
-    mark("forest_traverse")
-    torch.cuda.synchronize()
-    return {"breakdown_ms": {marks[i][0]: round(marks[i - 1][1].elapsed_time(marks[i][1]), 4)
-                             for i in range(1, len(marks))}, "n": n, "scoring_slots": lay.n_slots}
 
 
 if __name__ == "__main__":

@@ -224,6 +224,11 @@ int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, in
 #define FDX_KEY_SUB 2 /* out = key - param  (shard-local customer id)           */
 int fdx_key_map(const int32_t *keys_d, int64_t n, int32_t op, int32_t param, int32_t *out_d,
                 void *stream);
+/* *count_d = #{i : keys_d[i] < lo or keys_d[i] >= hi} (stream-ordered; count_d is zeroed by
+ * the call).  fdx_rekey requires keys in [0, n_keys): a shard's customer ids outside its
+ * range would be mis-grouped, so the callers check with this before trusting the segments. */
+int fdx_count_out_of_range(const int32_t *keys_d, int64_t n, int32_t lo, int32_t hi, int32_t *count_d,
+                           void *stream);
 int fdx_exchange_pack(const int64_t *ts_d, const int32_t *term_d, const uint8_t *fraud_d,
                       const int32_t *perm_d, int64_t n, int64_t *rec_d, void *stream);
 int fdx_exchange_unpack(const int64_t *rec_d, int64_t m, int32_t world, int64_t *ts_d,
@@ -431,6 +436,9 @@ int fdx_stream_update(fdx_stream s, const int64_t *ts_d, const int32_t *cust_d, 
                       int32_t term_col0, int32_t *cust_nb_d, double *cust_sum_d, int64_t *term_rec_d,
                       void *stream);
 int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream);
+/* Non-blocking form: enqueues the copy of the status bits to flags_pinned_h (pinned host
+ * memory, valid once the stream reaches this point); does not clear them. */
+int fdx_stream_status_async(fdx_stream s, int32_t *flags_pinned_h, void *stream);
 int fdx_stream_destroy(fdx_stream s);
 
 /* f-4 delay-aware split and Card-Precision@k (shared_functions.py:133-188, :352-411).

@@ -91,7 +91,7 @@ def load_namespace(include_training: bool = False) -> dict:
     for table in (GENERATOR_DEFS, FEATURE_DEFS):
         for fname, nb in table.items():
             exec(compile(_find_def(nb, fname), f"<ref:{nb}:{fname}>", "exec"), ns)
-    for fname in ("read_from_files", "scaleData"):
+    for fname in ("read_from_files", "scaleData", "get_train_test_set"):
         exec(compile(_shared_function_src(fname), f"<ref:shared_functions.py:{fname}>", "exec"), ns)
     if include_training:
         for fname, nb in TRAINING_DEFS.items():

@@ -463,6 +463,21 @@ __global__ void k_key_map(const int32_t *__restrict__ in, int64_t n, int32_t op,
     }
 }
 
+// count of keys outside [lo, hi): per-wave ballot count, one atomic per wave
+__global__ void __launch_bounds__(256) k_count_out_of_range(const int32_t *__restrict__ keys, int64_t n, int32_t lo,
+                                                            int32_t hi, int32_t *__restrict__ count) {
+    int32_t bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k = keys[i];
+        bad += (k < lo || k >= hi) ? 1 : 0;
+    }
+    const uint64_t any = __ballot(bad != 0);
+    if (any == 0) return;
+#pragma unroll
+    for (int d = kWave / 2; d >= 1; d >>= 1) bad += __shfl_xor(bad, d, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(count, bad);
+}
+
 // rec[j] = {ts[r], term[r] << 32 | fraud[r] << 31 | r}, r = perm[j] (destination-grouped)
 __global__ void k_exchange_pack(const int64_t *__restrict__ ts, const int32_t *__restrict__ term,
                                 const uint8_t *__restrict__ fraud, const int32_t *__restrict__ perm,
@@ -554,6 +569,18 @@ extern "C" int fdx_key_map(const int32_t *keys_d, int64_t n, int32_t op, int32_t
     hipLaunchKernelGGL(k_key_map, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), keys_d, n, op,
                        param, out_d);
     FDX_LAUNCHED("k_key_map");
+    return FDX_OK;
+}
+
+extern "C" int fdx_count_out_of_range(const int32_t *keys_d, int64_t n, int32_t lo, int32_t hi, int32_t *count_d,
+                                      void *stream) {
+    FDX_REQUIRE(n >= 0 && count_d, "bad argument");
+    hipStream_t st = as_stream(stream);
+    FDX_HIP(hipMemsetAsync(count_d, 0, 4, st));
+    if (n == 0) return FDX_OK;
+    FDX_REQUIRE(keys_d, "null keys");
+    hipLaunchKernelGGL(k_count_out_of_range, dim3(stream_grid(n, 256)), dim3(256), 0, st, keys_d, n, lo, hi, count_d);
+    FDX_LAUNCHED("k_count_out_of_range");
     return FDX_OK;
 }
 

@@ -489,3 +489,9 @@ extern "C" int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream) {
     if (*flags_h) FDX_HIP(hipMemsetAsync(s->status_d, 0, 4, st));
     return FDX_OK;
 }
+
+extern "C" int fdx_stream_status_async(fdx_stream s, int32_t *flags_pinned_h, void *stream) {
+    FDX_REQUIRE(s && flags_pinned_h, "null pointer");
+    FDX_HIP(hipMemcpyAsync(flags_pinned_h, s->status_d, 4, hipMemcpyDeviceToHost, as_stream(stream)));
+    return FDX_OK;
+}

@@ -69,6 +69,7 @@ SIGNATURES = {
     "fdx_stream_memory": (ctypes.c_int, [P, P]),
     "fdx_stream_update": (ctypes.c_int, [P, P, P, P, P, P, c_i64, P, c_i64, c_i32, P, P, P, P]),
     "fdx_stream_status": (ctypes.c_int, [P, P, P]),
+    "fdx_stream_status_async": (ctypes.c_int, [P, P, P]),
     "fdx_stream_destroy": (ctypes.c_int, [P]),
     "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,
                                             c_sz, P, P]),
@@ -84,6 +85,7 @@ SIGNATURES = {
     "fdx_gather": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),
     "fdx_scatter": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),
     "fdx_key_map": (ctypes.c_int, [P, c_i64, c_i32, c_i32, P, P]),
+    "fdx_count_out_of_range": (ctypes.c_int, [P, c_i64, c_i32, c_i32, P, P]),
     "fdx_exchange_pack": (ctypes.c_int, [P, P, P, P, c_i64, P, P]),
     "fdx_exchange_unpack": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P]),
     "fdx_reply_assemble": (ctypes.c_int, [P, P, c_i64, c_i32, P, c_i64, c_i32, P]),

@@ -116,25 +116,61 @@ def exchange_terminal_features(K, ts, term, fraud, world, n_terminals_total, win
     return exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days, delay_days, group)
 
 
+def customer_shards(tx_per_customer, world: int):
+    """Contiguous CUSTOMER_ID ranges, one per rank, balanced by transaction count (SURVEY.md
+    §8(e)): rank k owns [base_k, base_k + count_k) with base_0 = 0 and the cut points at the
+    customers whose cumulative tx count first reaches k/world of the total.  Any remainder
+    (uneven customer or tx totals) lands on the ranks it falls to -- every customer is owned
+    exactly once.  -> list of (customer_base, n_customers_local)."""
+    import numpy as np
+
+    c = np.asarray(tx_per_customer, dtype=np.int64)
+    n_cust = len(c)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    cum = np.cumsum(c)
+    total = int(cum[-1]) if n_cust else 0
+    cuts = [0]
+    for k in range(1, world):
+        if total:  # smallest j with rows(customers [0, j)) >= ceil(k * total / world)
+            j = int(np.searchsorted(cum, -(-total * k // world), side="left")) + 1
+        else:
+            j = n_cust * k // world
+        cuts.append(min(max(j, cuts[-1]), n_cust))
+    cuts.append(n_cust)
+    return [(cuts[k], cuts[k + 1] - cuts[k]) for k in range(world)]
+
+
 class ShardedPipeline:
-    """FraudPipeline over `world` GPUs (this process = `rank`)."""
+    """FraudPipeline over `world` GPUs (this process = `rank`).  The rank owns the customers
+    [customer_base, customer_base + n_customers_local) -- pass each rank's range explicitly
+    (customer_shards balances them by tx count); its rows are exactly those customers'."""
 
     def __init__(self, pipe, world: int, rank: int, n_terminals_total: int, customer_base: int | None = None,
-                 group=None):
+                 group=None, n_customers_local: int | None = None):
         self.pipe, self.world, self.rank = pipe, world, rank
         self.n_terminals_total = n_terminals_total
         self.customer_base = customer_base
+        self.n_customers_local = n_customers_local
         self.group = group
 
-    def featurize(self, ts, customer, terminal, amount, fraud, n_customers_local: int):
+    def _range(self, n_customers_local=None):
+        n = self.n_customers_local if n_customers_local is None else int(n_customers_local)
+        if n is None:
+            raise _lib.FdxError("ShardedPipeline needs this rank's n_customers_local")
+        base = self.rank * n if self.customer_base is None else int(self.customer_base)
+        return base, n
+
+    def featurize(self, ts, customer, terminal, amount, fraud, n_customers_local: int | None = None):
         """customer: global ids of this rank's customers, dense in
         [customer_base, customer_base + n_customers_local)."""
         p = self.pipe
         W = len(p.windows_days)
         we, ni = ops.time_flags(ts, p.flags_mode)
-        base = self.rank * n_customers_local if self.customer_base is None else self.customer_base
+        base, n_local = self._range(n_customers_local)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
-        cperm, cseg, _ = ops.rekey(cust, n_customers_local)
+        rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")
+        cperm, cseg, _ = ops.rekey(cust, n_local)
         cnb, cavg = ops.customer_windows(ops.gather(ts, cperm), ops.gather(amount, cperm), cseg, p.windows_days)
         n = ts.numel()
         ld = 16 if p.n_features <= 16 else p.n_features
@@ -146,16 +182,16 @@ class ShardedPipeline:
                                                      self.n_terminals_total, p.windows_days, p.delay_days,
                                                      self.group)
         GpuKernels.reply_assemble(back, send_perm, W, X, 3 + 2 * W)
+        rc.check()
         return X[:, : p.n_features]
 
-    def run(self, ts, customer, terminal, amount, fraud, n_customers_total, proba, ws, events=None):
+    def run(self, ts, customer, terminal, amount, fraud, proba, ws, events=None, n_customers_local: int | None = None):
         """featurize + score this rank's rows: the single-GPU scoring path (interleaved
         customer layout, FraudPipeline.run_fused) for the customer half; the terminal half
         comes back from the owners as packed count records in send order."""
         p = self.pipe
         W = len(p.windows_days)
-        n_local = n_customers_total // self.world
-        base = self.rank * n_local if self.customer_base is None else self.customer_base
+        base, n_local = self._range(n_customers_local)
         # The terminal exchange (RCCL all-to-all there and back + the owner-side windows)
         # runs on a side stream, overlapped with the customer half on the main stream; the
         # two meet at the scoring-row assembly.
@@ -167,9 +203,11 @@ class ShardedPipeline:
         with torch.cuda.stream(side):
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
+        rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
         cperm, cseg, _ = ops.rekey(cust, n_local)
         lay = ops.customer_layout(cseg, cperm, ts, amount, W, None, p._slots_hint,
                                   p.windows_days)  # (host sync on main)
+        rc.check()
         p._slots_hint = lay.its.numel()
         with torch.cuda.stream(side):
             back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,

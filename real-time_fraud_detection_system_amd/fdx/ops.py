@@ -89,6 +89,33 @@ def key_map(keys: torch.Tensor, op: int, param: int, stream=None) -> torch.Tenso
     return out
 
 
+def count_out_of_range(keys: torch.Tensor, lo: int, hi: int, stream=None) -> torch.Tensor:
+    """-> int32 device scalar: #keys outside [lo, hi) (asynchronous; read it after a sync)."""
+    _dev(keys, torch.int32, "keys")
+    out = torch.empty(1, dtype=torch.int32, device=keys.device)
+    check(_lib.load().fdx_count_out_of_range(_ptr(keys), keys.numel(), int(lo), int(hi), _ptr(out), _s(stream)),
+          "fdx_count_out_of_range")
+    return out
+
+
+class KeyRangeCheck:
+    """Enqueue a key-range count now, read it after the caller's next host synchronisation
+    (no extra stall): the count is copied into pinned host memory on the same stream."""
+
+    def __init__(self, keys: torch.Tensor, n_keys: int, what: str = "keys", stream=None):
+        self.what, self.n_keys = what, int(n_keys)
+        self._host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        self._host.copy_(count_out_of_range(keys, 0, n_keys, stream), non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record(stream or torch.cuda.current_stream())
+
+    def check(self) -> None:
+        self._ev.synchronize()
+        bad = int(self._host.item())
+        if bad:
+            raise FdxError(f"{bad} {self.what} outside [0, {self.n_keys}): the grouping would be wrong")
+
+
 def argsort_i64(keys: torch.Tensor, stream=None) -> torch.Tensor:
     _dev(keys, torch.int64, "keys")
     n = keys.numel()
@@ -474,11 +501,12 @@ def forest_arrays_from_sklearn(model) -> dict:
     ests = getattr(model, "estimators_", None)
     if ests is None:
         ests = [model]
-    left, right, feat, thr, ml, val, off = [], [], [], [], [], [], [0]
+    left, right, feat, thr, ml, val, val0, off = [], [], [], [], [], [], [], [0]
     for e in ests:
         t = e.tree_
         if t.n_outputs != 1 or int(np.max(t.n_classes)) != 2:
             raise _lib.FdxUnsupported("only single-output binary classifiers are supported")
+        val0.append(np.ascontiguousarray(t.value[:, 0, 0], dtype=np.float64))
         left.append(t.children_left.astype(np.int64))
         right.append(t.children_right.astype(np.int64))
         feat.append(t.feature.astype(np.int64))
@@ -488,4 +516,4 @@ def forest_arrays_from_sklearn(model) -> dict:
         off.append(off[-1] + t.node_count)
     return dict(left=np.concatenate(left), right=np.concatenate(right), feature=np.concatenate(feat),
                 threshold=np.concatenate(thr), missing_left=np.concatenate(ml), value1=np.concatenate(val),
-                node_offsets=np.asarray(off, np.int64))
+                value0=np.concatenate(val0), node_offsets=np.asarray(off, np.int64))

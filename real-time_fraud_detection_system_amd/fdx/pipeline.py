@@ -103,33 +103,47 @@ class FraudPipeline:
         return f, self.score(f.X, stream=stream)
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
-                  proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, on_traverse=None):
+                  proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, mark=None,
+                  validate: bool = True):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
         slot, written there by the terminal kernel); the last forest launch writes proba back
-        in input row order."""
+        in input row order.  mark(stage) is called after each stage is enqueued (bench.py
+        records a HIP event there); validate: the customer / terminal ids must lie in
+        [0, n_customers) / [0, n_terminals) (counted on the device, read at the layout's
+        host sync -- no extra stall)."""
         W = len(self.windows_days)
+        mk = mark or (lambda _name: None)
+        if validate:
+            rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", stream),
+                  ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", stream))
         cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
+        mk("rekey_customer")
         lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint, self.windows_days)
+        mk("customer_layout")
+        if validate:
+            for c in rc:
+                c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
         inb, isum = ops.customer_windows_walk(lay, cseg, stream)
+        mk("customer_walk")
         tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
+        mk("rekey_terminal")
         # count records in input row order (the kernel reads ts/fraud through tperm).  Measured
         # (r01): writing them at their scoring slots instead (terminal_windows_packed_dest +
         # invert_slots, sequential reads in the row assembly) costs the terminal kernel one
         # more random read per row than it saves the assembly: 3.23 ms vs 2.93 ms.
         trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days, rows=tperm,
                                            stream=stream)
+        mk("terminal_windows")
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
                                    ws, stream, n=lay.n_slots, val_is_sum=True)
-        if on_traverse:
-            on_traverse(0)
+        mk("assemble_rows")
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, stream)
-        if on_traverse:
-            on_traverse(1)
+        mk("forest_traverse")
         return proba
 
     def _forest_ws(self, n_rows, ws, device):

@@ -9,8 +9,11 @@ Reference contract:
 
 Training (StandardScaler.fit, classifier.fit) stays in scikit-learn: it is offline and out
 of scope.  The transform and predict_proba -- the hot path -- run on the
-GPU through libfdx.so.  Tree models supported: DecisionTreeClassifier and
-RandomForestClassifier (binary, single output); other classifiers raise FdxUnsupported.
+GPU through libfdx.so.  Tree models on the GPU: DecisionTreeClassifier and
+RandomForestClassifier (binary, single output).  The reference's model zoo
+(model_training.ipynb:2209-2214) also holds LogisticRegression and XGBClassifier: those are
+not tree ensembles this path accelerates, so fit_model_and_get_predictions and the UDF call
+their own predict_proba, exactly as the reference does (the scaling still runs on the GPU).
 """
 from __future__ import annotations
 
@@ -82,6 +85,7 @@ class GpuForest:
         nf = int(getattr(model, "n_features_in_"))
         mean, scale = _scaler_params(scaler) if scaler is not None else (None, None)
         self.forest = ops.Forest(arrays, nf, mean, scale)
+        self._arrays, self._scaler, self._forest0 = arrays, (mean, scale), None
         self.device = dev
         self.n_features = nf
 
@@ -90,8 +94,16 @@ class GpuForest:
         return self.forest.predict(Xd, want_leaves=want_leaves)
 
     def predict_proba(self, X) -> np.ndarray:
+        """[n, 2] like sklearn.  Column 1 is the class-1 forest; column 0 is NOT 1 - p (that can
+        differ from sklearn in the last bit): sklearn sums tree_.value[:, 0, 0] in tree order,
+        so a second device forest over the class-0 leaf values does the same additions."""
         p = self._run(X).cpu().numpy()
-        return np.stack([1.0 - p, p], axis=1)
+        if getattr(self, "_forest0", None) is None:
+            a0 = dict(self._arrays, value1=self._arrays["value0"])
+            self._forest0 = ops.Forest(a0, self.n_features, *self._scaler)
+        Xd = torch.from_numpy(_as_f64_matrix(X)).to(self.device)
+        p0 = self._forest0.predict(Xd).cpu().numpy()
+        return np.stack([p0, p], axis=1)
 
     def predict_proba1(self, X) -> np.ndarray:
         return self._run(X).cpu().numpy()
@@ -108,19 +120,37 @@ def _is_supported_tree_model(clf) -> bool:
     return isinstance(clf, (sklearn.tree.DecisionTreeClassifier, sklearn.ensemble.RandomForestClassifier))
 
 
+class _OwnPredictor:
+    """A classifier outside the GPU tree path (LogisticRegression, XGBClassifier, ...): its own
+    predict_proba, as the reference calls it (model_training.ipynb:506)."""
+
+    def __init__(self, model, scaler=None):
+        self.model, self.scaler = model, scaler
+
+    def predict_proba1(self, X) -> np.ndarray:
+        if self.scaler is not None:  # scaling is on the hot path: GPU transform, then the model
+            X = pd.DataFrame(gpu_transform(self.scaler, X), columns=list(X.columns), index=X.index) \
+                if isinstance(X, pd.DataFrame) else gpu_transform(self.scaler, X)
+        return np.asarray(self.model.predict_proba(X))[:, 1]
+
+
+def predictor(model, scaler=None):
+    """GpuForest for sklearn tree classifiers, the model's own predict_proba otherwise."""
+    return GpuForest(model, scaler) if _is_supported_tree_model(model) else _OwnPredictor(model, scaler)
+
+
 def fit_model_and_get_predictions(classifier, train_df, test_df, input_features,
                                   output_feature="TX_FRAUD", scale=True):
-    """model_training.ipynb:491-520.  fit stays in sklearn; predict_proba runs on the GPU."""
-    if not _is_supported_tree_model(classifier):
-        raise _lib.FdxUnsupported(f"{type(classifier).__name__}: only DecisionTreeClassifier / "
-                                  "RandomForestClassifier are on the GPU path")
+    """model_training.ipynb:491-520.  fit stays in sklearn; predict_proba runs on the GPU for
+    tree classifiers and through the classifier's own predict_proba for the rest of the
+    notebook's model zoo (LR / XGB, model_training.ipynb:2209-2214)."""
     if scale:
         (train_df, test_df, _scaler) = scaleData(train_df, test_df, input_features)
     start_time = time.time()
     classifier.fit(train_df[input_features], train_df[output_feature])
     training_execution_time = time.time() - start_time
 
-    g = GpuForest(classifier)
+    g = predictor(classifier)
     start_time = time.time()
     predictions_test = g.predict_proba1(test_df[input_features])
     prediction_execution_time = time.time() - start_time
@@ -137,7 +167,7 @@ def make_scale_and_predict_udf(model, scaler, feature_columns: Optional[Sequence
     reference: ``scale_and_predict_udf = pandas_udf("double")(make_scale_and_predict_udf(
     model, loaded_scaler))``.  NULL features (LEFT JOIN misses) arrive as NaN and follow
     sklearn's missing-value routing."""
-    g = GpuForest(model, scaler)
+    g = predictor(model, scaler)
     cols_names = list(feature_columns or INPUT_FEATURES)
 
     def scale_and_predict_udf(*cols: pd.Series) -> pd.Series:

@@ -105,6 +105,29 @@ class StreamState:
         if f.value:
             raise FdxUnsupported("stream state: " + "; ".join(m for b, m in _STATUS.items() if f.value & b))
 
+    def watch(self, stream=None):
+        """Enqueue a non-blocking copy of the status bits (pinned host memory + event); the
+        next poll() raises if the batch that preceded this call reported a problem."""
+        if getattr(self, "_pin", None) is None:
+            self._pin = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._ev = torch.cuda.Event()
+        check(_lib.load().fdx_stream_status_async(self._h, ctypes.c_void_p(self._pin.data_ptr()), ops._s(stream)),
+              "fdx_stream_status_async")
+        self._ev.record(stream or torch.cuda.current_stream())
+        self._watching = True
+
+    def poll(self, block: bool = False):
+        """Raise (and clear the bits) if the last watch() saw a problem.  Non-blocking unless
+        block: a copy still in flight is looked at by a later poll()."""
+        if not getattr(self, "_watching", False):
+            return
+        if not block and not self._ev.query():
+            return
+        self._ev.synchronize()
+        self._watching = False
+        if int(self._pin.item()):
+            self.check()  # synchronises, clears and raises with the decoded bits
+
 
 class StreamScorer:
     """Features + scaler + forest per micro-batch on one GPU (config 5 at N = 1)."""
@@ -131,11 +154,17 @@ class StreamScorer:
         self.proba = torch.empty(max_batch, dtype=torch.float64, device=dev)
 
     def score(self, ts, customer, amount, terminal, fraud):
-        """-> predict_proba[:, 1] of the batch (device view, valid until the next call)."""
+        """-> predict_proba[:, 1] of the batch (device view, valid until the next call).
+        Ring overflows, ids out of range and rows that go back in time are flagged by the
+        kernels; every batch enqueues a non-blocking copy of those bits and the next score()
+        (or finish()) raises FdxUnsupported for the batch that set them."""
+        self.state.poll()
         n = ts.numel()
         if not self.fused:
             X = self.state.update(ts, customer, amount, terminal, fraud, X=self.X[:n])
-            return self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+            out = self.forest.predict(X, ws=self.ws, out=self.proba[:n])
+            self.state.watch()
+            return out
         W = self.state.W
         cnb, csum = self.cnb[:W * n].view(W, n), self.csum[:W * n].view(W, n)
         trec = self.trec[:n * W].view(n, W)
@@ -143,7 +172,13 @@ class StreamScorer:
         # flags (from ts), averages = SUM / NB, risks = FRAUD / NB, scaling, threshold ranks
         ops.forest_prepare_grouped(self.forest, self.flags_mode, ts, amount, cnb, csum, None, None, trec, self.ws,
                                    n=n, val_is_sum=True)
-        return ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
+        out = ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
+        self.state.watch()
+        return out
+
+    def finish(self):
+        """Wait for the last batch's status bits and raise if it reported a problem."""
+        self.state.poll(block=True)
 
 
 def stream_terminal_exchange(K, records, ts, terminal, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
@@ -192,6 +227,7 @@ class ShardedStreamScorer:
     def score(self, ts, customer, amount, terminal, fraud):
         from . import distributed as D
 
+        self.state.poll()
         n = ts.numel()
         W = self.state.W
         K = D.GpuKernels
@@ -205,4 +241,9 @@ class ShardedStreamScorer:
         inv = ops.invert_perm(send_perm)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, ts, amount, cnb, csum, None, inv, back, self.ws,
                                    n=n, val_is_sum=True)
-        return ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
+        out = ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
+        self.state.watch()
+        return out
+
+    def finish(self):
+        self.state.poll(block=True)

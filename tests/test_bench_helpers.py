@@ -31,3 +31,22 @@ def test_walk_steps_of_the_bench_model():
     a = {k: z[k] for k in ("left", "right", "node_offsets")}
     assert b.walk_steps_per_row(a) == 2000  # 100 trees, every one reaches depth 20
     assert b.LDS_PEAK_STEPS == 256 * 2.4e9 / 4 * 64
+
+
+def test_sklearn_forest_rebuilt_from_arrays_matches_saved_output():
+    """The CPU baseline times scikit-learn itself on the bench model, rebuilt from its node
+    arrays (no pickle): the rebuilt forest must give sklearn's saved predict_proba bit for bit."""
+    import sklearn.preprocessing
+
+    b = _bench()
+    arrays, mean, scale, cx, cp = b.load_model(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    rf = b.sklearn_forest(arrays)
+    sc = sklearn.preprocessing.StandardScaler()
+    sc.mean_, sc.scale_, sc.var_, sc.n_features_in_, sc.n_samples_seen_ = mean, scale, scale * scale, 15, 1
+    rf.set_params(n_jobs=1)
+    np.testing.assert_array_equal(rf.predict_proba(sc.transform(cx[:512]))[:, 1], cp[:512])
+
+
+def test_host_info_fields():
+    info = _bench().host_info()
+    assert info["nproc"] >= 1 and info["affinity_cpus"] >= 1 and info["joblib_cpus"] >= 1

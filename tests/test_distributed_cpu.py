@@ -227,3 +227,23 @@ def test_stream_terminal_exchange_matches_single_process():
         for k, w in enumerate((1, 7, 30)):
             np.testing.assert_array_equal(nb[:, k], f[f"TERMINAL_ID_NB_TX_{w}DAY_WINDOW"][idx])
             np.testing.assert_array_equal(risk[:, k], f[f"TERMINAL_ID_RISK_{w}DAY_WINDOW"][idx])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8])
+def test_customer_shards_cover_and_balance(world):
+    """Contiguous customer ranges, balanced by tx count, every customer owned once -- also
+    when the customer count does not divide by world (the round-1 n // world split left the
+    remainder's ids outside every rank's range)."""
+    from fdx.distributed import customer_shards
+
+    rng = np.random.default_rng(world)
+    for n_cust in (1, 7, 1001, 50_003):
+        counts = rng.poisson(rng.uniform(0, 4, n_cust) * 183)
+        sh = customer_shards(counts, world)
+        assert len(sh) == world and sh[0][0] == 0
+        assert all(sh[k][0] + sh[k][1] == sh[k + 1][0] for k in range(world - 1))
+        assert sh[-1][0] + sh[-1][1] == n_cust and all(c >= 0 for _, c in sh)
+        if n_cust >= 1000:
+            rows = [int(counts[b:b + c].sum()) for b, c in sh]
+            ideal = counts.sum() / world
+            assert max(rows) - ideal <= counts.max() + 1, (rows, ideal)

@@ -1,0 +1,170 @@
+"""BASELINE.json configs at full size, on the GPU, through the C ABI.
+
+configs[1]  50k customers / 100k terminals / 183 days (~17.7M tx): the bench's fused scoring
+            path (FraudPipeline.run_fused) must give, on EVERY row, the probability of the
+            float64 path (featurize -> X -> Forest.predict), and the features of >= 100 sampled
+            customers and terminals (all their rows) must equal the C oracle bit for bit.
+configs[2]  RandomForest(100 trees, depth 20) predict_proba: the bench model's 4,096 held-out
+            rows against sklearn's saved output, then 10M rows resampled from them.
+multi-rank  the exchange kernels (pack / unpack / owner records / reply) with world = 4 and 8
+            record formats, the all-to-all simulated on the host: every rank's features must
+            equal the single-GPU featurize of the union (the gloo test swaps these kernels for
+            numpy stand-ins; here the HIP kernels run).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from fdx import _lib, ops, synth
+from fdx.pipeline import FraudPipeline
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CUST_COLS, TERM_COLS = oracle.CUSTOMER_COLS, oracle.TERMINAL_COLS
+
+
+def T(a, dt, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+
+
+def _model():
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    return arrays, z
+
+
+def _check_sampled_segments(d, X, n_sample=128, seed=0):
+    """Customer features of n_sample customers and terminal features of n_sample terminals,
+    all their rows, against the oracle run on exactly those rows."""
+    rng = np.random.default_rng(seed)
+    cust = rng.choice(np.unique(d["customer"]), n_sample, replace=False)
+    m = np.isin(d["customer"], cust)
+    f = oracle.featurize_arrays(d["ts"][m], d["customer"][m], d["terminal"][m], d["amount"][m], d["fraud"][m])
+    got = X[m]
+    np.testing.assert_array_equal(got[:, 1], f["TX_DURING_WEEKEND"])
+    np.testing.assert_array_equal(got[:, 2], f["TX_DURING_NIGHT"])
+    for j, c in enumerate(CUST_COLS):
+        np.testing.assert_array_equal(got[:, 3 + j], f[c], err_msg=c)
+    term = rng.choice(np.unique(d["terminal"]), n_sample, replace=False)
+    m = np.isin(d["terminal"], term)
+    f = oracle.featurize_arrays(d["ts"][m], d["customer"][m], d["terminal"][m], d["amount"][m], d["fraud"][m])
+    got = X[m]
+    for j, c in enumerate(TERM_COLS):
+        np.testing.assert_array_equal(got[:, 9 + j], f[c], err_msg=c)
+    return int(m.sum())
+
+
+def test_config2_full_size_fused_path_every_row(dev):
+    arrays, z = _model()
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    d = synth.generate(50_000, 100_000, 183, seed=1234)
+    n = len(d["ts"])
+    assert n > 17_000_000
+    args = (T(d["ts"], torch.int64, dev), T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev),
+            T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    pipe = FraudPipeline(forest=forest)
+    proba = torch.empty(n, dtype=torch.float64, device=dev)
+    ws = ops.workspace(forest.workspace_size(n * 11 // 10), dev)
+    pipe.run_fused(*args, 50_000, 100_000, proba, ws)
+    fused = proba.cpu().numpy()
+    feats = pipe.featurize(*args, 50_000, 100_000)
+    p64 = pipe.score(feats.X).cpu().numpy()
+    np.testing.assert_array_equal(fused, p64)
+    X = feats.X.cpu().numpy()
+    np.testing.assert_array_equal(X[:, 0], d["amount"])
+    rows = _check_sampled_segments(d, X)
+    assert rows > 10_000
+    # the sampled rows' probabilities against the oracle forest on the oracle's features
+    sel = np.random.default_rng(1).choice(n, 20_000, replace=False)
+    np.testing.assert_array_equal(p64[sel], oracle.forest_predict(X[sel], arrays, z["mean"], z["scale"]))
+
+
+def test_config3_rf100_d20_bench_model(dev):
+    arrays, z = _model()
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    cx, cp = z["check_X"], z["check_proba"]
+    np.testing.assert_array_equal(forest.predict(T(cx, torch.float64, dev)).cpu().numpy(), cp)
+    # 10M rows resampled (fixed seed) from the held-out rows, resident in HBM
+    idx = np.random.default_rng(7).integers(0, len(cx), 10_000_000)
+    Xd = T(cx, torch.float64, dev)[T(idx, torch.int64, dev)]
+    ws = ops.workspace(forest.workspace_size(len(idx)), dev)
+    got = forest.predict(Xd, ws=ws).cpu().numpy()
+    np.testing.assert_array_equal(got, cp[idx])
+
+
+def test_fused_path_rejects_ids_out_of_range(dev):
+    arrays, z = _model()
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    d = synth.generate(300, 500, 20, seed=4)
+    n = len(d["ts"])
+    cust = d["customer"].copy()
+    cust[n // 2] = 300                      # one id past n_customers
+    args = (T(d["ts"], torch.int64, dev), T(cust, torch.int32, dev), T(d["terminal"], torch.int32, dev),
+            T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    pipe = FraudPipeline(forest=forest)
+    proba = torch.empty(n, dtype=torch.float64, device=dev)
+    with pytest.raises(_lib.FdxError, match="customer ids"):
+        pipe.run_fused(*args, 300, 500, proba)
+
+
+# ----------------------------------------------------------------- multi-rank dataflow
+@pytest.mark.parametrize("world", [4, 8])
+def test_exchange_kernels_world_gt1_host_simulated_all_to_all(dev, world):
+    """Ranks r = 0..world-1 own customers [r*C, (r+1)*C); every step of fdx.distributed's
+    exchange runs its HIP kernel; only the two all-to-alls are done on the host."""
+    from fdx.distributed import GpuKernels as K
+
+    C, n_terms = 150, 400
+    shards = [synth.generate(C, n_terms, 70, r=25, seed=40 + r, customer_offset=C * r) for r in range(world)]
+    for r, s in enumerate(shards):
+        s["gid"] = s["tid"] + (r << 32)
+    whole = {k: np.concatenate([s[k] for s in shards])
+             for k in ("ts", "customer", "terminal", "amount", "fraud", "gid")}
+    o = np.argsort(whole["ts"], kind="stable")
+    whole = {k: v[o] for k, v in whole.items()}
+    pipe = FraudPipeline()
+    ref = pipe.featurize(*(T(whole[k], dt, dev) for k, dt in (("ts", torch.int64), ("customer", torch.int32),
+                                                             ("terminal", torch.int32), ("amount", torch.float64),
+                                                             ("fraud", torch.uint8))),
+                         C * world, n_terms).X.cpu().numpy()
+    ref_row = {int(g): i for i, g in enumerate(whole["gid"])}
+    # phase 1 on every rank: owner keys, re-key by owner, pack
+    sent = []
+    for r, s in enumerate(shards):
+        ts, term, fr = T(s["ts"], torch.int64, dev), T(s["terminal"], torch.int32, dev), T(s["fraud"], torch.uint8, dev)
+        owner = K.owner_keys(term, world)
+        perm, seg = K.rekey(owner, world)
+        rec = K.exchange_pack(ts, term, fr, perm).cpu().numpy()
+        p = perm.cpu().numpy()
+        np.testing.assert_array_equal(rec[:, 0], s["ts"][p])
+        np.testing.assert_array_equal(rec[:, 1] >> 32, s["terminal"][p])
+        np.testing.assert_array_equal((rec[:, 1] >> 31) & 1, s["fraud"][p])
+        np.testing.assert_array_equal(rec[:, 1] & 0x7FFFFFFF, p)
+        sent.append((rec, seg.cpu().numpy(), p))
+    # host all-to-all: owner o receives source ranks' blocks in rank order
+    replies = {}
+    W = 3
+    for o_ in range(world):
+        blocks = [sent[r][0][sent[r][1][o_]:sent[r][1][o_ + 1]] for r in range(world)]
+        recv = np.concatenate(blocks)
+        rts, rterm, rfr = K.exchange_unpack(T(recv, torch.int64, dev), world)
+        np.testing.assert_array_equal(rterm.cpu().numpy(), (recv[:, 1] >> 32) // world)
+        perm, gseg = K.rekey(rterm, (n_terms + world - 1) // world)
+        rec = K.terminal_records(rts, rfr, perm, gseg, 7, (1, 7, 30)).cpu().numpy()
+        assert rec.shape == (len(recv), W)
+        off = 0
+        for r in range(world):
+            replies.setdefault(r, {})[o_] = rec[off:off + len(blocks[r])]
+            off += len(blocks[r])
+    # host all-to-all back, then the reply assembly on each source rank
+    for r, s in enumerate(shards):
+        back = np.concatenate([replies[r][o_] for o_ in range(world)])
+        X = torch.zeros((len(s["ts"]), 16), dtype=torch.float64, device=dev)
+        K.reply_assemble(T(back, torch.int64, dev), T(sent[r][2], torch.int32, dev), W, X, 3 + 2 * W)
+        got = X.cpu().numpy()[:, 9:15]
+        rows = [ref_row[int(g)] for g in s["gid"]]
+        np.testing.assert_array_equal(got, ref[rows][:, 9:15])

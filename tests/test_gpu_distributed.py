@@ -35,8 +35,8 @@ def test_sharded_pipeline_world1_matches_single(dev):
                 T(d["amount"], torch.float64), T(d["fraud"], torch.uint8))
         pipe = FraudPipeline()
         ref = pipe.featurize(*args, 3000, 5000).X.cpu().numpy()
-        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=5000)
-        got = sp.featurize(*args, 3000).cpu().numpy()
+        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=5000, customer_base=0, n_customers_local=3000)
+        got = sp.featurize(*args).cpu().numpy()
         np.testing.assert_array_equal(got, ref)
         # exchange kernels with world > 1 semantics (owner = t % 4, local id = t / 4)
         own = ops.key_map(args[2], 0, 4).cpu().numpy()
@@ -68,9 +68,9 @@ def test_fused_scoring_paths_agree(dev, golden):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
-        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=4000)
+        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=4000, customer_base=0, n_customers_local=2000)
         p2 = torch.zeros(n, dtype=torch.float64, device=dev)
-        sp.run(*args, 2000, p2, ws)
+        sp.run(*args, p2, ws)
         np.testing.assert_array_equal(p2.cpu().numpy(), p_ref.cpu().numpy())
     finally:
         dist.destroy_process_group()

@@ -141,3 +141,40 @@ def test_spark_udf_body(golden):
     assert isinstance(got, pd.Series) and got.dtype == np.float64
     np.testing.assert_array_equal(got.values, exp)
     _ = oracle
+
+
+def test_model_zoo_non_tree_classifier_uses_own_predict_proba(golden):
+    """model_training.ipynb:2209-2223 loops over LR, DT, RF, XGB: the drop-in must not break
+    on LogisticRegression (its own predict_proba on the GPU-scaled frame)."""
+    import sklearn.linear_model
+    import sklearn.preprocessing
+
+    z = golden("tiny_a.npz")
+    df = pd.DataFrame({c: z[c] for c in fdx.INPUT_FEATURES[1:]})
+    df.insert(0, "TX_AMOUNT", z["TX_AMOUNT"])
+    df["TX_FRAUD"] = z["TX_FRAUD"]
+    train, test = df.iloc[: len(df) * 2 // 3].copy(), df.iloc[len(df) * 2 // 3:].copy()
+    res = fdx.fit_model_and_get_predictions(sklearn.linear_model.LogisticRegression(max_iter=200), train.copy(),
+                                            test.copy(), fdx.INPUT_FEATURES)
+    tr, te = train.copy(), test.copy()
+    sc = sklearn.preprocessing.StandardScaler().fit(tr[fdx.INPUT_FEATURES])
+    tr[fdx.INPUT_FEATURES] = sc.transform(tr[fdx.INPUT_FEATURES])
+    te[fdx.INPUT_FEATURES] = sc.transform(te[fdx.INPUT_FEATURES])
+    lr = sklearn.linear_model.LogisticRegression(max_iter=200).fit(tr[fdx.INPUT_FEATURES], tr["TX_FRAUD"])
+    np.testing.assert_array_equal(res["predictions_test"], lr.predict_proba(te[fdx.INPUT_FEATURES])[:, 1])
+    # the UDF body with a non-tree model: GPU scaling, then the model's own predict_proba
+    udf = fdx.make_scale_and_predict_udf(lr, sc)
+    cols = [pd.Series(test[c].values) for c in fdx.INPUT_FEATURES]
+    np.testing.assert_array_equal(udf(*cols).values, lr.predict_proba(sc.transform(test[fdx.INPUT_FEATURES]))[:, 1])
+
+
+def test_predict_proba_both_columns_bit_exact(golden):
+    """GpuForest.predict_proba: column 0 is sklearn's tree-order sum of value[:, 0, 0], not 1 - p."""
+    import sklearn.ensemble
+
+    z = golden("tiny_a.npz")
+    X = np.column_stack([z["TX_AMOUNT"]] + [z[c] for c in fdx.INPUT_FEATURES[1:]])
+    rf = sklearn.ensemble.RandomForestClassifier(n_estimators=7, max_depth=9, random_state=0, n_jobs=1)
+    rf.fit(X[:6000], z["TX_FRAUD"][:6000])
+    got = fdx.GpuForest(rf).predict_proba(X[6000:])
+    np.testing.assert_array_equal(got, rf.predict_proba(X[6000:].astype(np.float32)))

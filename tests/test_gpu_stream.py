@@ -215,3 +215,18 @@ def test_sharded_stream_world1_equals_single(dev, golden):
         sh.state.check()
     finally:
         dist.destroy_process_group()
+
+
+def test_stream_scorer_raises_without_explicit_check(dev, golden):
+    """StreamScorer.score watches the status bits itself: a ring overflow in one batch makes
+    the next score() (or finish()) raise, with no state.check() by the caller."""
+    forest = _forest(golden)
+    sc = StreamScorer(forest, 4, 4, customer_ring=4, terminal_ring=4, max_batch=64)
+    base = 1_717_200_000_000_000_000
+    ts = base + np.arange(10, dtype=np.int64) * 3_600 * 10**9   # 10 rows of one key: ring of 4 overflows
+    z = np.zeros(10, np.int32)
+    args = (T(ts, torch.int64, dev), T(z, torch.int32, dev), T(np.ones(10), torch.float64, dev),
+            T(z, torch.int32, dev), T(np.zeros(10), torch.uint8, dev))
+    sc.score(*args)
+    with pytest.raises(_lib.FdxUnsupported, match="ring overflow"):
+        sc.finish()
