@@ -128,9 +128,8 @@ class _OwnPredictor:
         self.model, self.scaler = model, scaler
 
     def predict_proba1(self, X) -> np.ndarray:
-        if self.scaler is not None:  # scaling is on the hot path: GPU transform, then the model
-            X = pd.DataFrame(gpu_transform(self.scaler, X), columns=list(X.columns), index=X.index) \
-                if isinstance(X, pd.DataFrame) else gpu_transform(self.scaler, X)
+        if self.scaler is not None:  # fraud_detection.py:190-193: transform -> ndarray -> predict_proba
+            X = gpu_transform(self.scaler, X)
         return np.asarray(self.model.predict_proba(X))[:, 1]
 
 
