@@ -292,6 +292,23 @@ int fdx_forest_rank_layout_size(const fdx_forest_desc *desc, int64_t *n_nodes, i
 int fdx_forest_pack_rank(const fdx_forest_desc *desc, uint32_t *nodes_out, int32_t *orig_out,
                          double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out,
                          int32_t *depth_out, float *thr_out, int32_t *thr_off_out);
+/* Rank layout v2 (forests whose features have more than 32,767 distinct thresholds -- e.g. the
+ * reference's deployed RandomForestClassifier(random_state=0), model_training.ipynb:2212): 32
+ * u16 threshold-rank SLOTS, feature f spanning ceil(|U_f| / 32767) consecutive slots; slot s
+ * holds min(max(r_f - slot_base[s], 0), 32767).  Node (4 B): [30:16] k' | [15:11] slot |
+ * [10:0] right offset; leaf 0x7FFF0000; jump 0xFFFF0000 | offset.  version = 1 or 2 (1 = the
+ * fdx_forest_pack_rank layout; thr_off_out then has 17 meaningful entries of 33, slot tables 0).
+ * fdx_forest_create picks v1 when the forest fits it, else v2 when <= 16 features need <= 32
+ * slots, else the wide 8-byte layout.  v2 forests score through fdx_forest_predict /
+ * prepare + traverse (the fused scoring-pipeline prepares need v1). */
+int fdx_forest_rank_layout_size2(const fdx_forest_desc *desc, int32_t version, int64_t *n_nodes,
+                                 int32_t *n_thresholds, int32_t *n_slots);
+int fdx_forest_pack_rank2(const fdx_forest_desc *desc, int32_t version, uint32_t *nodes_out, int32_t *orig_out,
+                          double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out, int32_t *depth_out,
+                          float *thr_out, int32_t *thr_off_out /* [33] */, int32_t *slot_feat_out /* [32] */,
+                          int32_t *slot_base_out /* [32] */);
+/* *layout = 0 (wide 8-byte nodes), 1 (rank v1) or 2 (rank v2); *n_slots = rank slots. */
+int fdx_forest_layout(fdx_forest forest, int32_t *layout, int32_t *n_slots);
 int fdx_forest_destroy(fdx_forest forest);
 int fdx_forest_info(fdx_forest forest, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
                     int32_t *n_chunks);
@@ -324,7 +341,9 @@ int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
  * 10 = 768 x 1 x 2, 11 = 768 x 2 x 2, 12-15 = rows-resident tile kernels.  Rank layout
  * (4-byte nodes, u16 rank rows; see fdx_forest_pack_rank): 16 = 1024 x 1 x 4 (the default
  * when the forest fits the rank layout), 17 = 1024 x 1 x 2, 18 = 512 x 2 x 2,
- * 19 = 512 x 2 x 4, 20 = 1024 x 1 x 3, 21 = 768 x 1 x 4, 22 = 256 x 4 x 2, 23 = 1024 x 1 x 6.
+ * 19 = 512 x 2 x 4, 20 = 1024 x 1 x 3, 21 = 768 x 1 x 4, 22 = 256 x 4 x 2, 23 = 1024 x 1 x 6,
+ * ..., 41 = 1024 x 1 x 6 pipelined (the v1 default); rank layout v2: 44 = 1024 x 1 x 6 (default),
+ * 45 = 1024 x 1 x 4.
  * Variants > 0 need <= 16 features, 16+ need the rank layout (FDX_E_UNSUPPORTED otherwise).
  * Re-cuts the LDS chunks; results are identical for every variant.  The row format of a
  * prepared workspace depends on the layout: prepare again after switching layouts. */

@@ -63,11 +63,14 @@ struct fdx_forest_s {
     double *rlval_d = nullptr;
     uint8_t *rml_d = nullptr;
     float *rthr_d = nullptr;
-    int32_t rthr_off[16] = {}, rthr_cnt[16] = {};
+    int32_t rthr_off[32] = {}, rthr_cnt[32] = {};
     float *rseg_d = nullptr, *rsmp_d = nullptr;  // two-level rank search tables
     uint16_t *ritab_d = nullptr;                  // [16][kIntTab] ranks of small integer values
     uint16_t *rrat_d = nullptr;                   // [16][kRatN][kRatN] ranks of small ratios fr / nb
-    int32_t ruoff[16] = {}, rsoff[16] = {}, rscnt[16] = {}, rseg = 16, rnsmp = 0;
+    int32_t ruoff[32] = {}, rsoff[32] = {}, rscnt[32] = {}, rseg = 16, rnsmp = 0;
+    // rank layout v2 (32 threshold-rank slots, see build_rank_layout)
+    bool rank_v2 = false;
+    int32_t rn_slots = 0, rslot_feat[32] = {}, rslot_base[32] = {};
     int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
 };
 
@@ -109,13 +112,15 @@ constexpr int kRankXWords = 16 * kRankPlaneRows;  // 64 KiB of row planes
 
 struct RankTab {
     const float *u;  // concatenated U_f
-    int32_t off[16], cnt[16];
+    int32_t off[32], cnt[32];
     // two-level search tables (rank_row): U_f padded with +inf to whole segments of `seg`
     // floats at 16-float-aligned offsets (useg + uoff[f]), and the first float of every
     // segment (smp + soff[f], scnt[f] segments) -- staged into LDS by the prepare kernels
     const float *useg, *smp;
-    int32_t uoff[16], soff[16], scnt[16];
+    int32_t uoff[32], soff[32], scnt[32];
     int32_t seg, n_smp;
+    // rank layout v2: slot s holds min(max(rank(feature slot_feat[s]) - slot_base[s], 0), 32767)
+    int32_t n_slots, slot_feat[32], slot_base[32];
     // itab[f * kIntTab + c] = rank of the scaled integer c (c < kIntTab) in feature f: the
     // flags and window counts are small integers, so the prepare looks their ranks up
     const uint16_t *itab;
@@ -293,6 +298,64 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
         }
         if (nan) *nan_flag = 1;  // routes the traversal through the NaN-aware step
         store_row<FS, RANK>(z, r, v, nf, rt, s_smp);
+    }
+}
+
+// rank of v in feature f (lower_bound over U_f), two-level search as rank_row, one feature
+__device__ __forceinline__ uint32_t rank_one(float v, int f, const RankTab &rt, const float *s_smp) {
+    int32_t lo = rt.soff[f], n = rt.scnt[f];
+    if (n <= 0) return 0u;
+    while (n > 1) {
+        const int32_t h = n >> 1;
+        lo = (s_smp[lo + h] < v) ? lo + h : lo;
+        n -= h;
+    }
+    const int32_t c = lo - rt.soff[f] + (s_smp[lo] < v ? 1 : 0);
+    if (c <= 0) return 0u;
+    const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
+    uint32_t k = 0;
+    for (int q = 0; q < rt.seg / 4; ++q) {
+        const float4 w = sg[q];
+        k += (uint32_t)(w.x < v) + (uint32_t)(w.y < v) + (uint32_t)(w.z < v) + (uint32_t)(w.w < v);
+    }
+    return (uint32_t)(c - 1) * (uint32_t)rt.seg + k;
+}
+
+// Rank layout v2 rows: 32 u16 slots per row (64 B), slot s = the clamped rank of its
+// feature (build_rank_layout), 0xFFFF for a NaN feature; unused slots 0.
+__global__ void __launch_bounds__(256) k_prepare_v2(const double *__restrict__ X, int64_t n, int64_t rs, int64_t cs,
+                                                    int32_t nf, const double *__restrict__ mean,
+                                                    const double *__restrict__ scale, uint16_t *__restrict__ z,
+                                                    int32_t *__restrict__ nan_flag, RankTab rt) {
+    __shared__ float s_smp[kMaxRankSamples];
+    __shared__ __align__(16) uint16_t s_row[256][32];
+    stage_samples(s_smp, rt);
+    uint16_t *mine = s_row[threadIdx.x];
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = r0 + threadIdx.x;
+        if (r < n) {
+            bool any_nan = false;
+            for (int s = 0; s < 32; ++s) mine[s] = 0;
+            for (int f = 0; f < nf; ++f) {
+                double x = X[r * rs + (int64_t)f * cs];
+                if (mean) x = x - mean[f];
+                if (scale) x = x / scale[f];
+                const float v = (float)x;
+                const bool isn = v != v;
+                any_nan |= isn;
+                const uint32_t rk = isn ? 0u : rank_one(v, f, rt, s_smp);
+                for (int s = 0; s < rt.n_slots; ++s) {
+                    if (rt.slot_feat[s] != f) continue;
+                    const int64_t c = (int64_t)rk - rt.slot_base[s];
+                    mine[s] = isn ? (uint16_t)0xFFFFu : (uint16_t)(c < 0 ? 0 : (c > 32767 ? 32767 : c));
+                }
+            }
+            if (any_nan) *nan_flag = 1;
+            const uint4 *src = reinterpret_cast<const uint4 *>(mine);
+            uint4 *dst = reinterpret_cast<uint4 *>(z + r * 32);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = src[q];
+        }
     }
 }
 
@@ -714,7 +777,10 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 0, 1, 1, 1}, {1024, 1, 5, 0, 1, 0, 1}, {768, 1, 6, 0, 1, 0, 1}, {512, 2, 6, 0, 1, 0, 1},
     {512, 2, 4, 0, 1, 0, 1},
     // 41.. grouped waits (pipe = group width)
-    {1024, 1, 6, 0, 1, 0, 2}, {1024, 1, 6, 0, 1, 0, 3}, {1024, 1, 6, 0, 1, 0, 6}};
+    {1024, 1, 6, 0, 1, 0, 2}, {1024, 1, 6, 0, 1, 0, 3}, {1024, 1, 6, 0, 1, 0, 6},
+    // 44..: rank layout v2 (32 threshold-rank slots, u16 planes of 1,024 rows; p16 = 2)
+    {1024, 1, 6, 0, 1, 2, 2}, {1024, 1, 4, 0, 1, 2, 2}};
+constexpr int kDefaultRankV2Variant = 44;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -970,21 +1036,30 @@ __device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
 // is < 0 iff r <= k, and >= node & 0xFFFF >= right offset otherwise, so med3(d, 1, off)
 // steps exactly as in the 32-bit form (leaf: k = 0x7FFF vs sentinel 0x4000 -> d < 0, off 0;
 // jump: k = 0 -> d > 0); |d| < 2^31 because r, k <= 0x7FFF.
-template <bool NAN_AWARE, bool P16, int K>
+// Node / plane formats (template parameter P16): 0 = u32 planes, 4-bit feature, 12-bit right
+// offset (rank layout v1); 1 = the same nodes over u16 planes; 2 = rank layout v2: u16 planes
+// of 1,024 rows, a 5-bit SLOT field and an 11-bit right offset (see build_rank_layout).
+template <int P16>
+constexpr uint32_t kSlotMask = P16 == 2 ? 0xF800u : 0xF000u;
+template <int P16>
+constexpr uint32_t kOffMask = P16 == 2 ? 0x7FFu : 0xFFFu;
+
+template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        x[k] = P16 ? lds16(lds, (nd[k] & 0xF000u) | lane_base[k]) : lds32(lds, (nd[k] & 0xF000u) | lane_base[k]);
+        x[k] = P16 ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
+                   : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint32_t st;
         if (NAN_AWARE && x[k] == (P16 ? 0xFFFFu : 0xFFFFFFFFu)) {
-            st = mleft[(pa[k] - kRankNodeB) >> 2] != 0 ? 1u : (nd[k] & 0xFFFu);
+            st = mleft[(pa[k] - kRankNodeB) >> 2] != 0 ? 1u : (nd[k] & kOffMask<P16>);
         } else {
             const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
-            asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
+            asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
         }
         pa[k] += st << 2;
     }
@@ -992,7 +1067,7 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
     for (int k = 0; k < K; ++k) nd[k] = lds32(lds, pa[k]);
 }
 
-template <bool NAN_AWARE, bool P16, int K>
+template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft) {
     int d = 0;
@@ -1001,7 +1076,7 @@ __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane
         for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
         uint32_t moving = 0;  // leaves (and only leaves) have right offset 0
 #pragma unroll
-        for (int k = 0; k < K; ++k) moving |= nd[k] & 0xFFFu;
+        for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
         if (!__any(moving != 0)) return;
     }
     for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
@@ -1013,7 +1088,7 @@ __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane
 // with sched_barrier, so every chain has its next LDS read in flight while the others
 // compute (the default schedule clusters all K reads of a phase behind all K updates, and
 // a wave's outstanding reads drain to zero twice per step).
-template <bool P16>
+template <int P16>
 __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
     return P16 ? lds16(lds, addr) : lds32(lds, addr);
 }
@@ -1021,12 +1096,12 @@ __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
 // and its feature reads in forward order, so the first use in each group waits for the
 // group's last-issued read and one s_waitcnt covers the whole group (LDS reads of a wave
 // return in order): fewer issue slots per step.
-template <bool P16, int K, int PW>
+template <int P16, int K, int PW>
 __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                                uint32_t (&nd)[K], int depth) {
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = rank_x<P16>(lds, (nd[k] & 0xF000u) | lane_base[k]);
+    for (int k = 0; k < K; ++k) x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
     auto step = [&]() {
 #pragma unroll
         for (int g = 0; g < K; g += PW) {
@@ -1037,7 +1112,7 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
                     const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
                     uint32_t st;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
                     asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %0"
-                        : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & 0xFFFu));
+                        : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
                     nd[k] = lds32(lds, pa[k]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1045,7 +1120,7 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            x[k] = rank_x<P16>(lds, (nd[k] & 0xF000u) | lane_base[k]);
+            x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -1055,13 +1130,13 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
         for (int e = 0; e < kExitEvery; ++e) step();
         uint32_t moving = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) moving |= nd[k] & 0xFFFu;
+        for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
         if (!__any(moving != 0)) return;
     }
     for (; d < depth; ++d) step();
 }
 
-template <int R, int GG, bool P16, int PIPE>
+template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
                                            int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
@@ -1153,7 +1228,7 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-template <int BLOCK, int R, int G, bool P16, int PIPE>
+template <int BLOCK, int R, int G, int P16, int PIPE>
 __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
@@ -1162,7 +1237,9 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
     int32_t n_trees, int first, int last, const int32_t *__restrict__ chunk_t,
     const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n) {
-    constexpr int kPlaneRows = P16 ? 2 * kRankPlaneRows : kRankPlaneRows;  // both: 4 KiB per plane
+    // u32 planes: 1,024 rows x 16 slots; u16 planes: 2,048 rows x 16 slots; v2: 1,024 rows x 32 slots
+    constexpr int kPlaneRows = P16 == 1 ? 2 * kRankPlaneRows : kRankPlaneRows;
+    constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
     if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
         const int c = blockIdx.y;
         t0 = chunk_t[c];
@@ -1186,10 +1263,10 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     }
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {  // slot 15: the leaf / jump sentinel
-        if (P16)
+    for (int r = 0; r < R; ++r) {  // slot 15: the leaf / jump sentinel (v2 needs none)
+        if (P16 == 1)
             s_x16[15 * kPlaneRows + r * BLOCK + tid] = (uint16_t)(kRankSentinel >> 16);
-        else
+        else if (P16 == 0)
             s_x[15 * kRankPlaneRows + r * BLOCK + tid] = kRankSentinel;
     }
     __syncthreads();
@@ -1200,16 +1277,20 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * (P16 ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
-    uint4 q0[R], q1[R];
+    uint4 q0[R], q1[R], q2[R], q3[R];
     double pacc[R];
     auto fetch = [&](int64_t b) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t rw = b + r * BLOCK + tid;
             const bool okr = rw < r1;
-            const uint4 *src = reinterpret_cast<const uint4 *>(zr + (okr ? rw : r0) * 16);
+            const uint4 *src = reinterpret_cast<const uint4 *>(zr + (okr ? rw : r0) * kRowU16);
             q0[r] = src[0];
             q1[r] = src[1];
+            if (P16 == 2) {
+                q2[r] = src[2];
+                q3[r] = src[3];
+            }
             pacc[r] = (first || !okr) ? 0.0 : acc[rw];
         }
     };
@@ -1222,14 +1303,22 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
         for (int r = 0; r < R; ++r) {
             row[r] = base + r * BLOCK + tid;
             ok[r] = row[r] < r1;
-            const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
+            if constexpr (P16 == 2) {
+                const uint32_t w[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
+                                        q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
-            for (int f = 0; f < 15; ++f) {
-                const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                if (P16)
-                    s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
-                else
-                    s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+                for (int f = 0; f < 32; ++f)
+                    s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)((w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
+            } else {
+                const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
+#pragma unroll
+                for (int f = 0; f < 15; ++f) {
+                    const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
+                    if (P16)
+                        s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
+                    else
+                        s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+                }
             }
             a[r] = pacc[r];
         }
@@ -1408,21 +1497,41 @@ struct RankLayout {
     std::vector<uint8_t> ml;
     std::vector<int64_t> offsets;
     std::vector<float> thr;
-    int32_t thr_off[17] = {};
+    int32_t thr_off[33] = {};
+    // v2: threshold-rank slots (a feature with more than kSlotSpan thresholds spans several)
+    bool v2 = false;
+    int32_t n_slots = 0, slot_feat[32] = {}, slot_base[32] = {};
 };
 
 // Returns FDX_OK, or FDX_E_UNSUPPORTED (with the reason in fdx_last_error) when the forest
 // does not fit the layout (> 15 features, > 32767 distinct thresholds of one feature, a
 // tree larger than the LDS node budget).  `max_tree_nodes` = LDS node budget per chunk.
+//
+// v2 (rank layout v2, forests v1 cannot hold -- e.g. the reference's deployed
+// RandomForestClassifier(random_state=0): 100 unlimited-depth trees with up to 96k distinct
+// thresholds on one feature): 32 u16 SLOTS instead of 16 features.  Feature f with |U_f|
+// thresholds owns ceil(|U_f| / kSlotSpan) consecutive slots; slot j of f holds the clamped
+// rank  r_j = min(max(r - j*kSlotSpan, 0), kSlotSpan)  and a node testing U_f[k] tests slot
+// j = k / kSlotSpan with k' = k - j*kSlotSpan:  r <= k  <=>  r_j <= k'  (r below the slot's
+// range gives r_j = 0 <= k', above it r_j = kSlotSpan > k').  Node: [30:16] k' | [15:11]
+// slot | [10:0] right offset; leaf 0x7FFF0000 (k' = 0x7FFF >= every r_j: a fixed point of
+// the u16-plane step); jump 0xFFFF0000 | offset (k' = -1 in the step's 16-bit arithmetic:
+// always right).  No sentinel slot.
+constexpr int64_t kSlotSpan = 32767;
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
-                      RankLayout &L) {
-    if (d->n_features > 15) {
+                      RankLayout &L, bool v2 = false) {
+    if (!v2 && d->n_features > 15) {
         set_error("rank layout: %d features > 15", d->n_features);
         return FDX_E_UNSUPPORTED;
     }
+    const int nfeat = v2 ? 32 : 16;
+    const uint32_t kOff = v2 ? 0x7FFu : 0xFFFu;
+    const int64_t max_off = v2 ? 2047 : kRankMaxOffset;
+    const uint32_t leaf_word = v2 ? 0x7FFF0000u : kRankLeaf, jump_word = v2 ? 0xFFFF0000u : kRankJump;
+    L.v2 = v2;
     // U_f: sorted unique float32 thresholds per feature
-    std::vector<std::vector<float>> U(16);
+    std::vector<std::vector<float>> U(64);
     for (uint64_t nd : packed)
         if (nd >> 63) {
             const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
@@ -1431,18 +1540,33 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
             U[(hi >> 24) & 63].push_back(t);
         }
     L.thr.clear();
-    for (int f = 0; f < 16; ++f) {
+    int32_t slot_first[32] = {};
+    L.n_slots = 0;
+    for (int f = 0; f < nfeat; ++f) {
         auto &u = U[f];
         std::sort(u.begin(), u.end());
         u.erase(std::unique(u.begin(), u.end(), [](float a, float b) { return a == b; }), u.end());
-        if ((int64_t)u.size() > kRankMaxRank + 1) {
+        if (!v2 && (int64_t)u.size() > kRankMaxRank + 1) {
             set_error("rank layout: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank + 1);
             return FDX_E_UNSUPPORTED;
         }
         L.thr_off[f] = (int32_t)L.thr.size();
         L.thr.insert(L.thr.end(), u.begin(), u.end());
+        if (v2 && f < d->n_features) {
+            const int ns = (int)std::max<int64_t>(1, ceil_div((int64_t)u.size(), kSlotSpan));
+            if (L.n_slots + ns > 32) {
+                set_error("rank layout v2: more than 32 threshold slots needed");
+                return FDX_E_UNSUPPORTED;
+            }
+            slot_first[f] = L.n_slots;
+            for (int j = 0; j < ns; ++j) {
+                L.slot_feat[L.n_slots] = f;
+                L.slot_base[L.n_slots] = (int32_t)(j * kSlotSpan);
+                ++L.n_slots;
+            }
+        }
     }
-    L.thr_off[16] = (int32_t)L.thr.size();
+    L.thr_off[nfeat] = (int32_t)L.thr.size();
     L.nodes.clear(); L.orig.clear(); L.lval.clear(); L.ml.clear(); L.root.clear(); L.depth.clear();
     L.offsets.assign(1, 0);
     struct Pend { int64_t owner; };
@@ -1453,8 +1577,8 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         L.nodes.push_back(node); L.orig.push_back(o); L.lval.push_back(v); L.ml.push_back(m);
     };
     auto set_off = [&](int64_t pos, int64_t off) {
-        if (off < 1 || off > kRankMaxOffset) ok = false;
-        L.nodes[(size_t)pos] = (L.nodes[(size_t)pos] & ~0xFFFu) | (uint32_t)(off & 0xFFF);
+        if (off < 1 || off > max_off) ok = false;
+        L.nodes[(size_t)pos] = (L.nodes[(size_t)pos] & ~kOff) | (uint32_t)(off & kOff);
     };
     // pre-order emission; after every leaf, pending right pointers that are about to run out
     // of range are forwarded through a jump node placed right there (the slot after a leaf
@@ -1465,11 +1589,11 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         if (!(nd >> 63)) {
             double v;
             memcpy(&v, &nd, 8);
-            push(kRankLeaf, worig[(size_t)w], v, 0);
+            push(leaf_word, worig[(size_t)w], v, 0);
             for (auto &p : pend)
-                if ((int64_t)L.nodes.size() - p.owner + margin > kRankMaxOffset) {
+                if ((int64_t)L.nodes.size() - p.owner + margin > max_off) {
                     const int64_t j = (int64_t)L.nodes.size();
-                    push(kRankJump, -1, 0.0, 0);
+                    push(jump_word, -1, 0.0, 0);
                     set_off(p.owner, j - p.owner);
                     p.owner = j;
                 }
@@ -1481,7 +1605,14 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         memcpy(&t, &lo, 4);
         const auto &u = U[f];
         const int64_t k = std::lower_bound(u.begin(), u.end(), t) - u.begin();
-        push(((uint32_t)k << 16) | ((uint32_t)f << 12), worig[(size_t)w], 0.0, (uint8_t)((hi >> 30) & 1));
+        uint32_t word;
+        if (v2) {
+            const int64_t j = k / kSlotSpan;
+            word = ((uint32_t)(k - j * kSlotSpan) << 16) | ((uint32_t)(slot_first[f] + j) << 11);
+        } else {
+            word = ((uint32_t)k << 16) | ((uint32_t)f << 12);
+        }
+        push(word, worig[(size_t)w], 0.0, (uint8_t)((hi >> 30) & 1));
         pend.push_back({pos});
         const size_t pi = pend.size() - 1;
         emit(w + 1);
@@ -1492,7 +1623,7 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
     for (int32_t tr = 0; tr < d->n_trees; ++tr) {
         const int64_t tb = (int64_t)L.nodes.size();
         margin = 2 * wdepth[(size_t)tr] + 16;
-        if (margin > kRankMaxOffset / 2) {
+        if (margin > max_off / 2) {
             set_error("rank layout: tree %d is too deep (%d)", tr, wdepth[(size_t)tr]);
             return FDX_E_UNSUPPORTED;
         }
@@ -1512,12 +1643,13 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         int32_t dm = 0;
         for (int64_t p = tb; p < te; ++p) {
             const uint32_t nd = L.nodes[(size_t)p];
-            const int64_t off = nd & 0xFFF, s = st[(size_t)(p - tb)];
+            const int64_t off = nd & kOff, s = st[(size_t)(p - tb)];
             if (off == 0) {
                 dm = std::max<int32_t>(dm, (int32_t)s);
                 continue;
             }
-            if (((nd >> 12) & 15) != 15) st[(size_t)(p + 1 - tb)] = (int32_t)s + 1;
+            const bool jump = v2 ? (nd >> 16) == 0xFFFFu : ((nd >> 12) & 15) == 15;
+            if (!jump) st[(size_t)(p + 1 - tb)] = (int32_t)s + 1;
             st[(size_t)(p + off - tb)] = (int32_t)s + 1;
         }
         L.root.push_back((int32_t)tb);
@@ -1597,6 +1729,11 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
         set_error("variant %d needs the rank layout, which this forest does not fit", variant);
         return FDX_E_UNSUPPORTED;
     }
+    if (kVariants[variant].rank && (kVariants[variant].p16 == 2) != F->rank_v2) {
+        set_error("variant %d is for rank layout v%d; this forest uses v%d", variant,
+                  kVariants[variant].p16 == 2 ? 2 : 1, F->rank_v2 ? 2 : 1);
+        return FDX_E_UNSUPPORTED;
+    }
     const int prev = F->variant;
     F->variant = variant;
     build_chunks(F);
@@ -1628,12 +1765,60 @@ extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, in
     return FDX_OK;
 }
 
-static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL) {
+static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL, int version = 1) {
     std::vector<uint64_t> packed;
     std::vector<int32_t> orig, root, depth;
     int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
-    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL);
+    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2);
+}
+
+extern "C" int fdx_forest_rank_layout_size2(const fdx_forest_desc *d, int32_t version, int64_t *n_nodes,
+                                            int32_t *n_thresholds, int32_t *n_slots) {
+    FDX_REQUIRE(n_nodes && n_thresholds && n_slots, "null output");
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
+    RankLayout RL;
+    int rc = rank_layout_host(d, RL, version);
+    if (rc) return rc;
+    *n_nodes = (int64_t)RL.nodes.size();
+    *n_thresholds = (int32_t)RL.thr.size();
+    *n_slots = version == 2 ? RL.n_slots : 16;
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, uint32_t *nodes_out,
+                                     int32_t *orig_out, double *leaf_value_out, uint8_t *missing_left_out,
+                                     int32_t *root_out, int32_t *depth_out, float *thr_out, int32_t *thr_off_out,
+                                     int32_t *slot_feat_out, int32_t *slot_base_out) {
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
+    FDX_REQUIRE(nodes_out && orig_out && leaf_value_out && missing_left_out && root_out && depth_out && thr_off_out &&
+                    slot_feat_out && slot_base_out,
+                "null output");
+    RankLayout RL;
+    int rc = rank_layout_host(d, RL, version);
+    if (rc) return rc;
+    const size_t n = RL.nodes.size();
+    memcpy(nodes_out, RL.nodes.data(), 4 * n);
+    memcpy(orig_out, RL.orig.data(), 4 * n);
+    memcpy(leaf_value_out, RL.lval.data(), 8 * n);
+    memcpy(missing_left_out, RL.ml.data(), n);
+    memcpy(root_out, RL.root.data(), 4 * RL.root.size());
+    memcpy(depth_out, RL.depth.data(), 4 * RL.depth.size());
+    if (!RL.thr.empty()) {
+        FDX_REQUIRE(thr_out, "null output");
+        memcpy(thr_out, RL.thr.data(), 4 * RL.thr.size());
+    }
+    memcpy(thr_off_out, RL.thr_off, sizeof(RL.thr_off));
+    memcpy(slot_feat_out, RL.slot_feat, sizeof(RL.slot_feat));
+    memcpy(slot_base_out, RL.slot_base, sizeof(RL.slot_base));
+    return FDX_OK;
+}
+
+extern "C" int fdx_forest_layout(fdx_forest F, int32_t *layout, int32_t *n_slots) {
+    FDX_REQUIRE(F && layout && n_slots, "null pointer");
+    *layout = !F->rank_ok ? 0 : (F->rank_v2 ? 2 : 1);
+    *n_slots = F->rank_v2 ? F->rn_slots : (F->rank_ok ? 16 : 0);
+    return FDX_OK;
 }
 
 extern "C" int fdx_forest_rank_layout_size(const fdx_forest_desc *d, int64_t *n_nodes, int32_t *n_thresholds) {
@@ -1665,7 +1850,7 @@ extern "C" int fdx_forest_pack_rank(const fdx_forest_desc *d, uint32_t *nodes_ou
         FDX_REQUIRE(thr_out, "null output");
         memcpy(thr_out, RL.thr.data(), 4 * RL.thr.size());
     }
-    memcpy(thr_off_out, RL.thr_off, sizeof(RL.thr_off));
+    memcpy(thr_off_out, RL.thr_off, 17 * sizeof(int32_t));
     return FDX_OK;
 }
 
@@ -1686,15 +1871,23 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->node_offsets.assign(d->node_offsets, d->node_offsets + d->n_trees + 1);
     RankLayout RL;
     F->rank_ok = build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL) == FDX_OK;
+    if (!F->rank_ok && F->zstride == 16 && build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, true) == FDX_OK)
+        F->rank_ok = F->rank_v2 = true;  // v2: more thresholds per feature than v1's 15-bit ranks hold
     set_error("");
     // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
-    F->variant = F->rank_ok ? kDefaultRankVariant : (F->zstride == 16 ? 1 : 0);
+    F->variant = F->rank_ok ? (F->rank_v2 ? kDefaultRankV2Variant : kDefaultRankVariant) : (F->zstride == 16 ? 1 : 0);
+    const int nfs = F->rank_v2 ? 32 : 16;
     if (F->rank_ok) {
         F->rank_offsets = RL.offsets;
         F->rank_nodes = (int64_t)RL.nodes.size();
-        for (int f = 0; f < 16; ++f) {
+        for (int f = 0; f < nfs; ++f) {
             F->rthr_off[f] = RL.thr_off[f];
             F->rthr_cnt[f] = RL.thr_off[f + 1] - RL.thr_off[f];
+        }
+        F->rn_slots = RL.n_slots;
+        for (int j = 0; j < 32; ++j) {
+            F->rslot_feat[j] = RL.slot_feat[j];
+            F->rslot_base[j] = RL.slot_base[j];
         }
     }
     build_chunks(F);
@@ -1732,11 +1925,11 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         int seg = 16;
         for (;; seg *= 2) {
             int64_t m = 0;
-            for (int f = 0; f < 16; ++f) m += ceil_div(F->rthr_cnt[f], seg);
+            for (int f = 0; f < nfs; ++f) m += ceil_div(F->rthr_cnt[f], seg);
             if (m <= kMaxRankSamples) break;
         }
         F->rseg = seg;
-        for (int f = 0; f < 16; ++f) {
+        for (int f = 0; f < nfs; ++f) {
             const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, seg);
             F->ruoff[f] = (int32_t)useg.size();
             F->rsoff[f] = (int32_t)smp.size();
@@ -1754,7 +1947,7 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         // lower_bound the device search computes (bit-identical arithmetic on the host)
         itab.assign((size_t)16 * kIntTab, 0);
         rat.assign((size_t)16 * kRatN * kRatN, 0);
-        for (int f = 0; f < 16 && f < d->n_features; ++f) {
+        for (int f = 0; f < 16 && f < d->n_features && !F->rank_v2; ++f) {  // (v1 scoring pipeline only)
             const float *u0 = RL.thr.data() + RL.thr_off[f], *u1 = RL.thr.data() + RL.thr_off[f + 1];
             for (int c = 0; c < kIntTab; ++c) {
                 double x = (double)c;
@@ -1890,13 +2083,16 @@ static RankTab rank_tab(const fdx_forest_s *F) {
     rt.u = F->rthr_d;
     rt.useg = F->rseg_d;
     rt.smp = F->rsmp_d;
-    for (int f = 0; f < 16; ++f) {
+    for (int f = 0; f < 32; ++f) {
         rt.off[f] = F->rthr_off[f];
         rt.cnt[f] = F->rthr_cnt[f];
         rt.uoff[f] = F->ruoff[f];
         rt.soff[f] = F->rsoff[f];
         rt.scnt[f] = F->rscnt[f];
+        rt.slot_feat[f] = F->rslot_feat[f];
+        rt.slot_base[f] = F->rslot_base[f];
     }
+    rt.n_slots = F->rn_slots;
     rt.seg = F->rseg;
     rt.n_smp = F->rnsmp;
     rt.itab = F->ritab_d;
@@ -1947,6 +2143,12 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
+    if (rank_mode(F) && F->rank_v2) {
+        hipLaunchKernelGGL(k_prepare_v2, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride, F->n_features,
+                           F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
+        FDX_LAUNCHED("k_prepare_v2");
+        return FDX_OK;
+    }
     FDX_PREP(k_prepare, dim3(grid), st, X_d, n, row_stride, col_stride, F->n_features, F->mean_d, F->scale_d,
              (void *)z, flag);
     FDX_LAUNCHED("k_prepare");
@@ -2019,6 +2221,8 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                     case 41: FDX_LAUNCH_RANK(1024, 1, 6, false, 2); break;
                     case 42: FDX_LAUNCH_RANK(1024, 1, 6, false, 3); break;
                     case 43: FDX_LAUNCH_RANK(1024, 1, 6, false, 6); break;
+                    case 44: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
+                    case 45: FDX_LAUNCH_RANK(1024, 1, 4, 2, 2); break;
                     default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK
@@ -2129,6 +2333,7 @@ extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_wi
                                            const int32_t *term_nb_d, const double *term_risk_d, void *ws,
                                            size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
                 3 + 4 * n_windows);
@@ -2156,6 +2361,7 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
                                         int32_t n_windows, int32_t col0, void *ws, size_t ws_bytes,
                                         void *stream) {
     FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(col0 >= 0 && col0 + 2 * n_windows <= F->n_features, "columns out of range");
     if (n == 0) return FDX_OK;
@@ -2185,6 +2391,7 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                                           const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                           const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(flags_mode == FDX_FLAGS_NOTEBOOK || flags_mode == FDX_FLAGS_SPARK, "bad flags mode");
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,

@@ -94,6 +94,9 @@ SIGNATURES = {
     "fdx_forest_pack": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P]),
     "fdx_forest_rank_layout_size": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P]),
     "fdx_forest_pack_rank": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P, P, P, P, P, P]),
+    "fdx_forest_rank_layout_size2": (ctypes.c_int, [ctypes.POINTER(ForestDesc), c_i32, P, P, P]),
+    "fdx_forest_pack_rank2": (ctypes.c_int, [ctypes.POINTER(ForestDesc), c_i32, P, P, P, P, P, P, P, P, P, P]),
+    "fdx_forest_layout": (ctypes.c_int, [P, P, P]),
     "fdx_forest_destroy": (ctypes.c_int, [P]),
     "fdx_forest_info": (ctypes.c_int, [P, P, P, P, P]),
     "fdx_forest_workspace_size": (c_sz, [P, c_i64]),

@@ -54,14 +54,23 @@ def _scaler_params(scaler):
 
 
 def gpu_transform(scaler, X) -> np.ndarray:
-    """StandardScaler.transform on the GPU (float64, bit-identical)."""
+    """StandardScaler.transform on the GPU (float64, bit-identical).  The result has the
+    memory order sklearn's transform would give (for a multi-dtype DataFrame pandas hands its
+    values over column-major, and sklearn keeps that order), so that a BLAS consumer
+    downstream (LogisticRegression's X @ coef) sums in the same order as on the reference's
+    output (fraud_detection.py:190-193)."""
     dev = ops.require_gpu()
     Xh = _as_f64_matrix(X)
     mean, scale = _scaler_params(scaler)
     Xd = torch.from_numpy(Xh).to(dev)
     m = None if mean is None else torch.from_numpy(np.asarray(mean, np.float64)).to(dev)
     s = None if scale is None else torch.from_numpy(np.asarray(scale, np.float64)).to(dev)
-    return ops.standard_scale(Xd, m, s).cpu().numpy()
+    out = ops.standard_scale(Xd, m, s).cpu().numpy()
+    if isinstance(X, pd.DataFrame):
+        ref = X.to_numpy()
+        if ref.ndim == 2 and ref.flags.f_contiguous and not ref.flags.c_contiguous:
+            return np.asfortranarray(out)
+    return out
 
 
 def scaleData(train, test, features):

@@ -168,3 +168,30 @@ def test_exchange_kernels_world_gt1_host_simulated_all_to_all(dev, world):
         got = X.cpu().numpy()[:, 9:15]
         rows = [ref_row[int(g)] for g in s["gid"]]
         np.testing.assert_array_equal(got, ref[rows][:, 9:15])
+
+
+def test_deployed_model_rank_layout_v2(dev):
+    """The reference's deployed RandomForestClassifier(random_state=0) -- 100 unlimited-depth
+    trees, 1.68M nodes, up to 96k distinct thresholds on one feature (model_training.ipynb:2212,
+    served at fraud_detection.py:81-82, :190-193) -- on the GPU through rank layout v2: the
+    66,452-row test set of the notebook's split bit for bit against sklearn, both columns, then
+    1M rows resampled from it (the all-chunks-at-once path for small batches and the
+    chunk-sequential path for large ones)."""
+    import ctypes
+
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf_deployed.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    lay, ns = ctypes.c_int32(), ctypes.c_int32()
+    _lib.load().fdx_forest_layout(forest._h, ctypes.byref(lay), ctypes.byref(ns))
+    assert lay.value == 2 and 16 <= ns.value <= 32
+    X = z["test_X"]
+    assert len(X) == 66_452
+    np.testing.assert_array_equal(forest.predict(T(X, torch.float64, dev)).cpu().numpy(), z["test_proba1"])
+    f0 = ops.Forest(dict(arrays, value1=z["value0"]), 15, z["mean"], z["scale"])
+    np.testing.assert_array_equal(f0.predict(T(X, torch.float64, dev)).cpu().numpy(), z["test_proba0"])
+    idx = np.random.default_rng(3).integers(0, len(X), 1_000_000)
+    Xd = T(X, torch.float64, dev)[T(idx, torch.int64, dev)]
+    got = forest.predict(Xd, ws=ops.workspace(forest.workspace_size(len(idx)), dev)).cpu().numpy()
+    np.testing.assert_array_equal(got, z["test_proba1"][idx])

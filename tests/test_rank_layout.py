@@ -162,3 +162,111 @@ def test_rank_layout_ineligible_forest_falls_back():
     rng = np.random.default_rng(2)
     a = random_forest(rng, 2, 5, n_feat=20)
     assert pack_rank(a, n_features=20) is None
+
+
+def pack_rank2(a, n_features=15, version=2):
+    from fdx import _lib
+
+    L = _lib.load()
+    d, keep = _desc(a, n_features)
+    nn, nthr, ns = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+    rc = L.fdx_forest_rank_layout_size2(ctypes.byref(d), version, ctypes.byref(nn), ctypes.byref(nthr), ctypes.byref(ns))
+    if rc != 0:
+        return None
+    n, nt = nn.value, d.n_trees
+    out = dict(nodes=np.zeros(n, np.uint32), orig=np.zeros(n, np.int32), lval=np.zeros(n), ml=np.zeros(n, np.uint8),
+               root=np.zeros(nt, np.int32), depth=np.zeros(nt, np.int32), thr=np.zeros(max(nthr.value, 1), np.float32),
+               thr_off=np.zeros(33, np.int32), slot_feat=np.zeros(32, np.int32), slot_base=np.zeros(32, np.int32))
+    rc = L.fdx_forest_pack_rank2(ctypes.byref(d), version, *[out[k].ctypes.data for k in
+                                                             ("nodes", "orig", "lval", "ml", "root", "depth", "thr",
+                                                              "thr_off", "slot_feat", "slot_base")])
+    assert rc == 0, L.fdx_last_error()
+    out["n_slots"] = ns.value
+    return out
+
+
+def walk_rank_v2(R, z32):
+    """numpy model of k_forest_rank<.., P16 = 2>: slot s holds the clamped rank
+    min(max(r_f - base_s, 0), 32767) of its feature (0xFFFF for NaN), LDS node S = node ^
+    0xFFFF0000, d = int32((x << 16) + S), step = med3(d, 1, node & 0x7FF), slot = node[15:11]."""
+    n = z32.shape[0]
+    xs = np.zeros((n, 32), np.int64)
+    for s in range(R["n_slots"]):
+        f = R["slot_feat"][s]
+        u = R["thr"][R["thr_off"][f]:R["thr_off"][f + 1]]
+        r = np.searchsorted(u, z32[:, f], side="left").astype(np.int64)
+        xs[:, s] = np.clip(r - R["slot_base"][s], 0, 32767)
+        xs[np.isnan(z32[:, f]), s] = 0xFFFF
+    nodes = R["nodes"].astype(np.int64)
+    acc = np.zeros(n)
+    rows = np.arange(n)
+    nt = len(R["root"])
+    leaves = np.zeros((n, nt), np.int32)
+    for t in range(nt):
+        p = np.full(n, R["root"][t], np.int64)
+        for _ in range(int(R["depth"][t])):
+            nd = nodes[p]
+            x = xs[rows, (nd >> 11) & 31]
+            S = nd ^ 0xFFFF0000
+            d = ((x << 16) + S) & 0xFFFFFFFF
+            d = np.where(d >= 2**31, d - 2**32, d)
+            off = nd & 0x7FF
+            st = np.median(np.stack([d, np.ones_like(d), off]), axis=0).astype(np.int64)
+            st = np.where(x == 0xFFFF, np.where(R["ml"][p] != 0, 1, off), st)
+            p = p + st
+        assert ((nodes[p] & 0x7FF) == 0).all(), "walk did not end on leaves within depth"
+        acc = acc + R["lval"][p]
+        leaves[:, t] = R["orig"][p]
+    return acc / nt, leaves
+
+
+def test_rank_layout_v2_small_forests_match_v1(golden):
+    """v2 (slot field, 11-bit offsets, no sentinel) gives sklearn's leaves on the golden forests."""
+    for name in ("forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"):
+        z = golden(name)
+        R = pack_rank2(z)
+        assert R is not None and R["n_slots"] == 15
+        proba, leaves = walk_rank_v2(R, _z32(z["X"], z["mean"], z["scale"]))
+        np.testing.assert_array_equal(leaves, z["leaves"])
+        np.testing.assert_array_equal(proba, z["proba"])
+
+
+def test_rank_layout_v2_jump_nodes_and_many_thresholds():
+    """Deep random trees with more than 32,767 distinct thresholds on feature 0 (two slots)
+    and far right subtrees (jumps past the 11-bit offset), NaN rows included: v1 cannot hold
+    them, v2 reproduces the oracle."""
+    rng = np.random.default_rng(5)
+    a = random_forest(rng, 10, 13, p_leaf=0.01)
+    internal = a["left"] >= 0
+    a["feature"][internal] = 0
+    a["threshold"][internal] = rng.normal(size=int(internal.sum()))
+    assert len(np.unique(a["threshold"][internal].astype(np.float32))) > 32767
+    assert pack_rank(a) is None
+    R = pack_rank2(a)
+    n0 = len(np.unique(a["threshold"][internal].astype(np.float32)))
+    assert R is not None and R["n_slots"] == -(-n0 // 32767) + 14 and R["n_slots"] >= 16
+    assert int((R["orig"] == -1).sum()) > 0
+    X = rng.normal(size=(3000, 15))
+    X[rng.random(X.shape) < 0.05] = np.nan
+    op, ol = oracle.forest_predict(X, a, want_leaves=True)
+    proba, leaves = walk_rank_v2(R, X.astype(np.float32))
+    np.testing.assert_array_equal(leaves, ol)
+    np.testing.assert_array_equal(proba, op)
+
+
+def test_rank_layout_v2_deployed_model():
+    """The reference's deployed RandomForestClassifier(random_state=0) (100 unlimited-depth trees,
+    bench_assets/rf_deployed.npz, model_training.ipynb:2212): v1 rejects it (features with up to
+    96k thresholds), v2 reproduces sklearn's predict_proba of the served pipeline
+    (scaler.transform then the forest, fraud_detection.py:190-193) bit for bit."""
+    import os
+
+    from conftest import ROOT
+
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf_deployed.npz"))
+    assert pack_rank(z) is None
+    R = pack_rank2(z)
+    assert R is not None and R["n_slots"] <= 32
+    sel = np.arange(0, len(z["test_X"]), 16)
+    proba, _ = walk_rank_v2(R, _z32(z["test_X"][sel], z["mean"], z["scale"]))
+    np.testing.assert_array_equal(proba, z["test_proba1"][sel])
