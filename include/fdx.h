@@ -483,6 +483,40 @@ int fdx_card_precision_top_k(const int32_t *day_d, const int32_t *cust_d, const 
                              int32_t n_days, int32_t top_k, int32_t remove_detected, int32_t *nb_compromised_h,
                              double *cp_h, void *workspace_d, size_t workspace_bytes, void *stream);
 
+/* f-3 synthetic transactions with the handbook generator's distributions, on the GPU
+ * (fraud_detection_model/data_generator.ipynb :113-140 customers, :285-303 terminals, :420-437
+ * terminals within radius, :786-834 daily Poisson transactions, :1339-1371 time sort, :1732-1782
+ * add_frauds).  Profiles, the terminal sampler's band-sorted arrays and the compromised lists
+ * come from the host (fdx.synth.generate_device); every random draw is Philox4x32-10 keyed by
+ * `seed` with counter (customer, day, slot, purpose) -- the distributions of the reference,
+ * not its Python RNG stream.  Two phases: fdx_synth_plan (one host sync) returns the row count
+ * n_tx; fdx_synth_fill writes the time-ordered rows (ts ns, customer + customer_offset,
+ * terminal, amount, fraud; scenario_d / day_d optional).  comp_term_d: n_comp_term
+ * (terminal id, first day) int32 pairs sorted by terminal (compromised for 28 days);
+ * comp_cust_d: (customer, first day) pairs sorted by customer (14 days, 1/3 of the rows x5). */
+typedef struct {
+    int64_t n_customers, n_terminals;
+    int32_t n_days;
+    double radius;
+    uint64_t seed;
+    const double *cx_d, *cy_d, *mean_amount_d, *mean_nb_d; /* [n_customers] */
+    const double *tx_sorted_d, *ty_sorted_d;               /* [n_terminals], sorted by (band of r, x) */
+    const int32_t *t_order_d;                              /* sorted position -> terminal id */
+    const int32_t *range_lo_d, *range_hi_d;                /* [n_customers][3] runs of the 3 bands */
+    const int32_t *comp_term_d;
+    int32_t n_comp_term;
+    const int32_t *comp_cust_d;
+    int32_t n_comp_cust;
+    int64_t start_ns;
+    int32_t customer_offset;
+} fdx_synth_desc;
+size_t fdx_synth_workspace_size(const fdx_synth_desc *desc, int64_t n_tx);
+int fdx_synth_plan(const fdx_synth_desc *desc, void *workspace_d, size_t workspace_bytes, int64_t *n_tx_h,
+                   void *stream);
+int fdx_synth_fill(const fdx_synth_desc *desc, int64_t n_tx, void *workspace_d, size_t workspace_bytes, int64_t *ts_d,
+                   int32_t *customer_d, int32_t *terminal_d, double *amount_d, uint8_t *fraud_d, uint8_t *scenario_d,
+                   int32_t *day_d, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,17 @@ class ForestDesc(ctypes.Structure):
     ]
 
 
+class SynthDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_customers", c_i64), ("n_terminals", c_i64), ("n_days", c_i32), ("radius", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("cx", P), ("cy", P), ("mean_amount", P), ("mean_nb", P), ("tx_sorted", P), ("ty_sorted", P),
+        ("t_order", P), ("range_lo", P), ("range_hi", P),
+        ("comp_term", P), ("n_comp_term", c_i32), ("comp_cust", P), ("n_comp_cust", c_i32),
+        ("start_ns", c_i64), ("customer_offset", c_i32),
+    ]
+
+
 # name -> (restype, argtypes); exactly the symbols declared in include/fdx.h
 SIGNATURES = {
     "fdx_last_error": (ctypes.c_char_p, []),
@@ -98,6 +109,9 @@ SIGNATURES = {
     "fdx_forest_pack_rank2": (ctypes.c_int, [ctypes.POINTER(ForestDesc), c_i32, P, P, P, P, P, P, P, P, P, P]),
     "fdx_forest_layout": (ctypes.c_int, [P, P, P]),
     "fdx_forest_destroy": (ctypes.c_int, [P]),
+    "fdx_synth_workspace_size": (c_sz, [ctypes.POINTER(SynthDesc), c_i64]),
+    "fdx_synth_plan": (ctypes.c_int, [ctypes.POINTER(SynthDesc), P, c_sz, P, P]),
+    "fdx_synth_fill": (ctypes.c_int, [ctypes.POINTER(SynthDesc), c_i64, P, c_sz, P, P, P, P, P, P, P, P]),
     "fdx_forest_info": (ctypes.c_int, [P, P, P, P, P]),
     "fdx_forest_workspace_size": (c_sz, [P, c_i64]),
     "fdx_forest_workspace_size_max": (ctypes.c_size_t, [P, c_i64]),

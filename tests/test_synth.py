@@ -30,3 +30,17 @@ def test_generate_shape_and_order():
     assert (np.diff(d["ts"]) >= 0).all()
     assert d["customer"].max() < 300 and d["terminal"].max() < 600
     assert set(np.unique(d["fraud"])) <= {0, 1}
+
+
+def test_numpy_generator_matches_reference_statistics_config1():
+    """fdx.synth at BASELINE config 1 (5k customers / 10k terminals / 183 days) against the
+    reference generator's own output: 1,754,155 tx, 14,681 frauds (973 / 9,076 / 4,632 by
+    scenario), amount and time-of-day moments, per-customer volume quantiles."""
+    import synth_stats
+    from fdx import synth
+
+    for seed in (0, 1):
+        d = synth.generate(5000, 10000, 183, seed=seed)
+        secs = (d["ts"] - synth.START_NS) // synth.NS
+        synth_stats.assert_close(synth_stats.stats(d["day"], secs, d["customer"], d["terminal"], d["amount"],
+                                                   d["fraud"], d["scenario"]))
