@@ -43,11 +43,11 @@ ALG = {"K2": 30, "K1-cust": 58, "K1-term": 49, "K3": 90, "end-to-end": 107}
 # bench stages (marks of FraudPipeline.run_fused) -> §8(d) unit and the kernels they launch
 # (substring of the rocprofv3 kernel name, dispatches per step; "chunks" = forest chunks)
 STAGES = [
-    ("rekey_customer", "K2", [("k_radix_hist<unsigned int, 8>", 2), ("k_radix_scatter<unsigned int, 8>", 2)]),
-    ("customer_layout", "K1-cust", [("k_interleave<true>", 1)]),
+    ("rekey_customer", "K2", [("k_radix_hist<unsigned int, 8>", 2), ("k_radix_scatter<unsigned int, 8, 2>", 2)]),
+    ("customer_layout", "K1-cust", [("k_interleave<true, true>", 1)]),
     ("customer_walk", "K1-cust", [("k_customer_walk", 1)]),
-    ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 2), ("k_radix_scatter<unsigned int, 9>", 2)]),
-    ("terminal_windows", "K1-term", [("k_terminal<false>", 1)]),
+    ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 2), ("k_radix_scatter<unsigned int, 9, 1>", 2)]),
+    ("terminal_windows", "K1-term", [("k_terminal_g<false>", 1)]),
     ("assemble_rows", "K3", [("k_zfill_grouped_w3", 1)]),
     ("forest_traverse", "K3", [("k_forest_rank", "chunks")]),
 ]

@@ -96,6 +96,14 @@ int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_seg, const in
                                int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
                                double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
                                int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes, void *stream);
+/* fdx_customer_layout_starts over GROUPED ts / amount (fdx_rekey_payload outputs: row j of
+ * the grouping is gts_d[j], gamount_d[j]) -- the layout then reads every segment as a
+ * sequential stream instead of gathering through cperm_d (which still gives irow_d). */
+int fdx_customer_layout_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                       const int64_t *gts_d, const double *gamount_d, const int64_t *window_ns,
+                                       int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
+                                       double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
+                                       int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes, void *stream);
 /* The sequential half of fdx_customer_windows_interleaved over the starts of
  * fdx_customer_layout_starts: nb_d / sum_d as there ([W][n_slots] by slot; n_windows >= 3,
  * i.e. <= 21 segments per wave). */
@@ -174,6 +182,19 @@ int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *
                                          const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
                                          void *stream);
 
+/* The terminal windows over GROUPED inputs (the scoring pipeline's form): gts_d[q] = ts of
+ * grouped position q (fdx_rekey_payload output); fraud of q = gfraud_d[q], or bit 31 of
+ * rows_d[q] when gfraud_d is NULL (fdx_rekey_payload's packed flag); rows_d[q] & 0x7FFFFFFF =
+ * the row whose record is written (NULL: q).  Output: count records rec_d[row][n_windows] (as
+ * fdx_terminal_windows_packed) or, when rec_d is NULL, nb_d / risk_d [w*n + q].  runs != 0:
+ * segments are concatenations of time-sorted runs (multi-GPU owner side).  scratch_d: int32[n]
+ * (prefix fraud counts of segments longer than the kernel's LDS stage, 1,024 rows; such
+ * segments cost O(L log L)). */
+int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                                 const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                 const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
+                                 double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream);
+
 /* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
  * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /
  * groupby('TERMINAL_ID') (feature_transformation.ipynb:1092-1093, :2435-2436).
@@ -185,6 +206,17 @@ size_t fdx_rekey_workspace_size(int64_t n, int32_t key_bits);
 int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, int32_t *perm_d,
               int32_t *sorted_keys_d, int64_t *seg_off_d, void *workspace_d, size_t workspace_bytes,
               void *stream);
+
+/* fdx_rekey that also carries up to two 8-byte payload streams through the radix passes
+ * (pay0_d / pay1_d in input row order -> pay0_out_d / pay1_out_d in grouped order), so that the
+ * window kernels read the grouped table sequentially.  flag_d (optional, uint8 per row):
+ * perm_d[j] = row | (flag_d[row] != 0) << 31 (e.g. TX_FRAUD packed beside the row index).
+ * Workspace: fdx_rekey_payload_workspace_size(n, key_bits, number of payload streams). */
+size_t fdx_rekey_payload_workspace_size(int64_t n, int32_t key_bits, int32_t n_payload);
+int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
+                      const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
+                      uint64_t *pay0_out_d, uint64_t *pay1_out_d, void *workspace_d, size_t workspace_bytes,
+                      void *stream);
 
 /* Stable argsort of int64 keys (e.g. TX_DATETIME ns): perm_d[j] = input row at sorted
  * position j, ties keep input order.  Used when a caller's frame is not in time order

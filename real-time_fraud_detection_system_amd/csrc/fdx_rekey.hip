@@ -145,12 +145,20 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
     for (int d = threadIdx.x; d < kBins; d += kBlock) hist[(int64_t)d * n_tiles + blockIdx.x] = s_h[d];
 }
 
-// Stable scatter of one tile.  vals_in == nullptr means "the value is the row index".
-template <typename K, int BITS>
+// Stable scatter of one tile.  vals_in == nullptr means "the value is the row index" (with
+// bit 31 = flag_in[row] != 0 when flag_in is given: fdx_rekey_payload's packed flag).
+// PW > 0: PW 8-byte payload streams ride along -- the element placed at tile position p came
+// from tile-local index s_src[p], so its payload is read from pay_in[base + s_src[p]] (a
+// random read inside the tile's own 4,096-row window: L2-resident, each line fetched from HBM
+// once) and written next to its key (the same coalesced runs).  The grouped payload then reads
+// sequentially downstream, where gathering it through the permutation took a random HBM line
+// per 8-byte element (round-1 PMC: 3-6x the algorithmic bytes).
+template <typename K, int BITS, int PW>
 __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
     int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
-    uint32_t *__restrict__ vals_out) {
+    uint32_t *__restrict__ vals_out, const uint8_t *__restrict__ flag_in, const uint64_t *__restrict__ p0_in,
+    const uint64_t *__restrict__ p1_in, uint64_t *__restrict__ p0_out, uint64_t *__restrict__ p1_out) {
     constexpr int kBins = 1 << BITS, kPer = kBins / kBlock;
     static_assert(kBins % kBlock == 0, "digit bins must be a multiple of the block");
     __shared__ uint32_t s_run[kBins];                  // digit counts of earlier rounds
@@ -158,6 +166,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     __shared__ uint32_t s_start[kBins];                // tile-local digit starts
     __shared__ K s_key[kTile];
     __shared__ uint32_t s_val[kTile];
+    __shared__ uint16_t s_src[PW ? kTile : 1];
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -176,7 +185,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         const int64_t i = base + (int64_t)r * kBlock + tid;
         const bool valid = i < n;
         key[r] = valid ? keys_in[i] : (K)0;
-        val[r] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+        val[r] = valid ? (vals_in ? vals_in[i] : ((uint32_t)i | (flag_in && flag_in[i] ? 0x80000000u : 0u))) : 0u;
         const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
         // peers: lanes of this wave holding the same digit (wave multisplit by ballots)
         uint64_t peers = __ballot(valid);
@@ -232,6 +241,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
             const uint32_t p = s_start[d] + rank[r];
             s_key[p] = key[r];
             s_val[p] = val[r];
+            if (PW) s_src[p] = (uint16_t)(r * kBlock + tid);
         }
     }
     __syncthreads();
@@ -242,6 +252,11 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
         keys_out[dst] = k;
         vals_out[dst] = s_val[p];
+        if constexpr (PW > 0) {
+            const int64_t src = base + s_src[p];
+            p0_out[dst] = p0_in[src];
+            if constexpr (PW > 1) p1_out[dst] = p1_in[src];
+        }
     }
 }
 
@@ -302,10 +317,11 @@ template <typename K>
 struct SortWs {
     K *k0, *k1;
     uint32_t *v0, *v1, *hist, *part;
+    uint64_t *q[2][2];  // payload ping-pong buffers [stream][parity] (PW streams)
 };
 
 template <typename K>
-size_t sort_ws(int64_t n, SortWs<K> *w, char *base) {
+size_t sort_ws(int64_t n, SortWs<K> *w, char *base, int pw = 0) {
     const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kTile));
     const int64_t hm = tiles * kMaxBins;
     size_t off = 0;
@@ -321,16 +337,29 @@ size_t sort_ws(int64_t n, SortWs<K> *w, char *base) {
     t.v1 = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * n));
     t.hist = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * hm));
     t.part = reinterpret_cast<uint32_t *>(take(sizeof(uint32_t) * (scan_partials_count(hm) + 1)));
+    for (int q = 0; q < 2; ++q)
+        for (int par = 0; par < 2; ++par)
+            t.q[q][par] = q < pw ? reinterpret_cast<uint64_t *>(take(sizeof(uint64_t) * n)) : nullptr;
     if (w) *w = t;
     return off;
 }
 
 // Stable LSD radix sort of (key, row index) pairs over the low `bits` bits of (key ^ flip).
-// vals_out receives the input row index of each sorted position; keys_out (optional) the
-// sorted keys.  Returns the buffer that holds the sorted keys.
+// vals_out receives the input row index of each sorted position (| flag << 31 with flag_in);
+// keys_out (optional) the sorted keys; pay_out[q] (PW streams) the payload in sorted order.
+// Returns the buffer that holds the sorted keys.
+template <typename K, int BITS, int PW>
+void launch_scatter(const K *kin, const uint32_t *vin, int64_t n, int shift, K flip, int64_t tiles,
+                    const uint32_t *hist, K *kout, uint32_t *vout, const uint8_t *flag_in, const uint64_t *const (&pin)[2],
+                    uint64_t *const (&pout)[2], hipStream_t st) {
+    hipLaunchKernelGGL((k_radix_scatter<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n, shift,
+                       flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
+}
+
 template <typename K>
 int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t *vals_out,
-               const SortWs<K> &w, hipStream_t st, const K **sorted) {
+               const SortWs<K> &w, hipStream_t st, const K **sorted, int pw = 0, const uint8_t *flag_in = nullptr,
+               const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr) {
     const int64_t tiles = ceil_div(n, kTile);
     // 9-bit digits when they need fewer passes than 8-bit ones (17- and 18-bit keys: 2, not 3)
     static const bool only8 = getenv("FDX_RADIX_8BIT") != nullptr;  // A/B switch
@@ -338,9 +367,16 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
     const int passes = (bits + dbits - 1) / dbits;
     const K *kin = keys;
     const uint32_t *vin = nullptr;  // identity on the first pass
+    const uint64_t *pin[2] = {pw > 0 ? pay_in[0] : nullptr, pw > 1 ? pay_in[1] : nullptr};
     if (passes == 0) {
+        if (flag_in) {
+            set_error("a packed flag needs at least one radix pass");
+            return FDX_E_INVALID;
+        }
         hipLaunchKernelGGL(k_iota, dim3(stream_grid(n, 256)), dim3(256), 0, st, vals_out, n);
         FDX_LAUNCHED("k_iota");
+        for (int q = 0; q < pw; ++q)
+            FDX_HIP(hipMemcpyAsync(pay_out[q], pay_in[q], sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
         *sorted = keys;
         return FDX_OK;
     }
@@ -350,6 +386,8 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         K *kout = (p & 1) ? w.k1 : w.k0;
         if (last && keys_out) kout = keys_out;
         uint32_t *vout = last ? vals_out : ((p & 1) ? w.v1 : w.v0);
+        uint64_t *pout[2] = {nullptr, nullptr};
+        for (int q = 0; q < pw; ++q) pout[q] = last ? pay_out[q] : w.q[q][p & 1];
         if (dbits == 9)
             hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
                                tiles, w.hist);
@@ -359,15 +397,19 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         FDX_LAUNCHED("k_radix_hist");
         int rc = exclusive_scan(w.hist, tiles * ((int64_t)1 << dbits), w.part, st);
         if (rc) return rc;
-        if (dbits == 9)
-            hipLaunchKernelGGL((k_radix_scatter<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
-                               shift, flip, tiles, w.hist, kout, vout);
-        else
-            hipLaunchKernelGGL((k_radix_scatter<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin,
-                               n, shift, flip, tiles, w.hist, kout, vout);
+        const uint8_t *fl = p == 0 ? flag_in : nullptr;
+#define FDX_SCATTER(B, PWV) \
+    launch_scatter<K, B, PWV>(kin, vin, n, shift, flip, tiles, w.hist, kout, vout, fl, pin, pout, st)
+        if (dbits == 9) {
+            if (pw == 2) FDX_SCATTER(9, 2); else if (pw == 1) FDX_SCATTER(9, 1); else FDX_SCATTER(9, 0);
+        } else {
+            if (pw == 2) FDX_SCATTER(kRadixBits, 2); else if (pw == 1) FDX_SCATTER(kRadixBits, 1); else FDX_SCATTER(kRadixBits, 0);
+        }
+#undef FDX_SCATTER
         FDX_LAUNCHED("k_radix_scatter");
         kin = kout;
         vin = vout;
+        for (int q = 0; q < pw; ++q) pin[q] = pout[q];
     }
     *sorted = kin;
     return FDX_OK;
@@ -412,6 +454,49 @@ extern "C" int fdx_rekey(const int32_t *keys_d, int64_t n, int32_t key_bits, int
                            reinterpret_cast<uint32_t *>(sorted_keys_d), n);
         FDX_LAUNCHED("k_copy_u32");
     }
+    if (seg_off_d) {
+        hipLaunchKernelGGL(k_seg_offsets, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, sorted, n, n_keys,
+                           seg_off_d);
+        FDX_LAUNCHED("k_seg_offsets");
+    }
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_rekey_payload_workspace_size(int64_t n, int32_t key_bits, int32_t n_payload) {
+    (void)key_bits;
+    if (n < 0) n = 0;
+    return sort_ws<uint32_t>(n, nullptr, nullptr, n_payload < 0 ? 0 : (n_payload > 2 ? 2 : n_payload));
+}
+
+extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                                 const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
+                                 int64_t *seg_off_d, uint64_t *pay0_out_d, uint64_t *pay1_out_d, void *workspace_d,
+                                 size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(key_bits >= 1 && key_bits <= 31, "key_bits must be in [1, 31]");
+    FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
+    FDX_REQUIRE((pay0_d == nullptr) == (pay0_out_d == nullptr) && (pay1_d == nullptr) == (pay1_out_d == nullptr) &&
+                    (pay1_d == nullptr || pay0_d != nullptr),
+                "payload inputs and outputs go together (stream 1 needs stream 0)");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        if (seg_off_d) FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
+        return FDX_OK;
+    }
+    FDX_REQUIRE(keys_d && perm_d, "null keys/perm");
+    const int pw = pay1_d ? 2 : (pay0_d ? 1 : 0);
+    SortWs<uint32_t> w;
+    size_t need = sort_ws<uint32_t>(n, &w, reinterpret_cast<char *>(workspace_d), pw);
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("rekey workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    const uint64_t *pin[2] = {pay0_d, pay1_d};
+    uint64_t *pout[2] = {pay0_out_d, pay1_out_d};
+    const uint32_t *sorted = nullptr;
+    int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, nullptr,
+                                  reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted, pw, flag_d, pin, pout);
+    if (rc) return rc;
     if (seg_off_d) {
         hipLaunchKernelGGL(k_seg_offsets, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, sorted, n, n_keys,
                            seg_off_d);

@@ -192,8 +192,11 @@ __global__ void k_group_slots(const int64_t *__restrict__ seg_off, const int32_t
 // from the just-written slots (L2) into LDS, binary searches in LDS -- written
 // segment-contiguous: starts[w * n_slots + goff[g] + l * Lg + t] (Lg = the group's longest
 // segment), so both this writer and k_customer_walk's per-lane reads are contiguous.
+// GROUPED: ts / amount are already in grouped order (fdx_rekey_payload carried them through
+// the re-key): slot (t, l) reads ts[seg_off[s] + t] -- each segment a sequential stream --
+// instead of ts[cperm[...]], a random HBM line per 8-byte element.
 constexpr int kStartLds = 1024;  // segment rows staged per wave for the start searches
-template <bool STARTS>
+template <bool STARTS, bool GROUPED = false>
 __global__ void __launch_bounds__(256) k_interleave(
     const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder, const int32_t *__restrict__ cperm,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, const int64_t *__restrict__ ts,
@@ -215,8 +218,8 @@ __global__ void __launch_bounds__(256) k_interleave(
             const int64_t slot = base + t * S + l;
             if (t < L) {
                 const int32_t r = cperm[b + t];
-                its[slot] = ts[r];
-                iamt[slot] = amount[r];
+                its[slot] = ts[GROUPED ? b + t : r];
+                iamt[slot] = amount[GROUPED ? b + t : r];
                 irow[slot] = r;
             } else {
                 its[slot] = 0;
@@ -855,6 +858,144 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
     }
 }
 
+// Terminal windows over GROUPED inputs (fdx_rekey_payload carried ts -- and the fraud bit in
+// bit 31 of the perm -- through the re-key): every read is sequential within a segment.
+//   gts[q]    ts of grouped position q; segments time-sorted, or (RUNS) concatenations of
+//             time-sorted runs (the multi-GPU owner side: one run per source rank)
+//   fraud(q)  gfraud ? gfraud[q] : rows[q] >> 31
+//   rows[q]   destination row of q's record (bits 30..0; NULL: q itself)
+// Output: count records rec_out[row] (W words NB | FRAUD << 32), or nb_out/risk_out[w*n + q].
+// Segments of <= kTermLdsRows rows are staged in LDS (closed form of k_terminal).  Longer
+// ones -- a hot terminal, or one terminal's rows from every rank on its owner -- use global
+// memory: the segment's wave first writes the inclusive prefix fraud count of every position
+// to scratch[q], then each row binary-searches its window bounds in gts (per run) and reads
+// two prefix counts: O(L log L) per segment (round 1 counted them directly, O(L^2)).
+template <bool RUNS>
+__global__ void __launch_bounds__(kTermBlock) k_terminal_g(
+    const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
+    const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
+    int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
+    int32_t *__restrict__ scratch) {
+    __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
+    __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
+    __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
+    const int64_t nwaves = (int64_t)gridDim.x * kTermWaves;
+    int64_t *lts = s_ts[wv];
+    int32_t *lf = s_f[wv];
+    int32_t *lr = s_runs[RUNS ? wv : 0];
+    auto fraud_of = [&](int64_t q) -> int { return gfraud ? (gfraud[q] != 0) : (int)((uint32_t)rows[q] >> 31); };
+    auto dest_of = [&](int64_t q) -> int64_t { return rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q; };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int64_t seg = gwave; seg < n_seg; seg += nwaves) {
+        const int64_t b = seg_off[seg], e = seg_off[seg + 1];
+        const int64_t L = e - b;
+        if (L <= 0) continue;
+        const bool in_lds = L <= kTermLdsRows;
+        // stage ts (LDS) and the inclusive prefix fraud counts (LDS: lf[j + 1]; global: scratch[b + j])
+        int carry = 0;
+        if (in_lds && lane == 0) lf[0] = 0;
+        for (int64_t c = 0; c < L; c += kWave) {
+            const int64_t j = c + lane;
+            int f = 0;
+            if (j < L) {
+                f = fraud_of(b + j);
+                if (in_lds) lts[j] = gts[b + j];
+            }
+            const int inc = wave_incl_scan(f, lane) + carry;
+            if (j < L) {
+                if (in_lds) lf[j + 1] = inc;
+                else scratch[b + j] = inc;
+            }
+            carry = __shfl(inc, kWave - 1, kWave);
+        }
+        // this wave's scratch writes before its reads below; an agent-scope fence also drops
+        // L1 lines another wave of this CU may hold for a neighbouring segment's scratch
+        if (!in_lds) __threadfence();
+        wave_sync();
+        // timestamps and prefix counts F(j) = # fraud rows in [0, j) of the segment
+        auto T = [&](int64_t j) -> int64_t { return in_lds ? lts[j] : __builtin_nontemporal_load(gts + b + j); };
+        auto F = [&](int64_t j) -> int32_t {
+            return in_lds ? lf[j] : (j == 0 ? 0 : __builtin_nontemporal_load(scratch + b + j - 1));
+        };
+        auto ub = [&](int64_t lo, int64_t hi, int64_t x) -> int64_t {  // first j in [lo, hi) with T(j) > x
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (T(mid) <= x) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        int nruns = 1;
+        if (RUNS) {  // run starts: wherever ts descends
+            if (lane == 0) lr[0] = 0;
+            int nr = 1;
+            for (int64_t c = 0; c < L; c += kWave) {
+                const int64_t j = c + lane;
+                const bool dsc = j > 0 && j < L && T(j) < T(j - 1);
+                const uint64_t m = __ballot(dsc);
+                const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
+                if (dsc && at < kMaxRuns) lr[at] = (int32_t)j;
+                nr += __popcll(m);
+            }
+            if (lane == 0 && nr <= kMaxRuns) lr[nr] = (int32_t)L;
+            nruns = nr;
+            wave_sync();
+        }
+        for (int64_t i = lane; i < L; i += kWave) {
+            const int64_t t = T(i);
+            const int64_t row = dest_of(b + i);
+            int32_t nbh = 0, frh = 0;
+            if (!RUNS || nruns == 1) {
+                const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
+                nbh = (int32_t)hi;
+                frh = F(hi);
+                for (int w = 0; w < n_win; ++w) {
+                    const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), frh - F(lo));
+                }
+            } else if (nruns <= kMaxRuns) {
+                for (int r = 0; r < nruns; ++r) {
+                    const int64_t h = ub(lr[r], lr[r + 1], t - delay);
+                    nbh += (int32_t)(h - lr[r]);
+                    frh += F(h) - F(lr[r]);
+                }
+                for (int w = 0; w < n_win; ++w) {
+                    int32_t nbl = 0, frl = 0;
+                    for (int r = 0; r < nruns; ++r) {
+                        const int64_t lo = ub(lr[r], lr[r + 1], t - delay - win.w[w]);
+                        nbl += (int32_t)(lo - lr[r]);
+                        frl += F(lo) - F(lr[r]);
+                    }
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl, frh - frl);
+                }
+            } else {  // more than kMaxRuns unsorted runs: count directly (correct for any order)
+                int32_t nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
+                for (int64_t j = 0; j < L; ++j) {
+                    const int64_t tj = T(j);
+                    if (tj > t - delay) continue;
+                    const int fj = F(j + 1) - F(j);
+                    ++nbh;
+                    frh += fj;
+                    for (int w = 0; w < n_win; ++w)
+                        if (tj <= t - delay - win.w[w]) {
+                            ++nbl[w];
+                            frl[w] += fj;
+                        }
+                }
+                for (int w = 0; w < n_win; ++w)
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl[w], frh - frl[w]);
+            }
+        }
+        wave_sync();
+    }
+}
+
 // X[r][0..2] = amount, weekend, night (rows already in output order)
 __global__ void __launch_bounds__(256) k_assemble_time(const double *__restrict__ amount,
                                                        const uint8_t *__restrict__ weekend,
@@ -1025,6 +1166,30 @@ extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, cons
                            true, stream);
 }
 
+extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                                            const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                            const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
+                                            double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(delay_ns > 0, "delay must be > 0 ns");
+    FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(gts_d && seg_off_d && scratch_d, "null pointer");
+    FDX_REQUIRE(gfraud_d || rows_d, "fraud comes from gfraud_d or bit 31 of rows_d");
+    FDX_REQUIRE(rec_d || (nb_d && risk_d), "no output");
+    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
+    if (runs)
+        hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
+                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d);
+    else
+        hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
+                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d);
+    FDX_LAUNCHED("k_terminal_g");
+    return FDX_OK;
+}
+
 extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
                                      const uint8_t *weekend_d, const uint8_t *night_d,
                                      const int32_t *cust_perm_d, const int32_t *cust_nb_d,
@@ -1064,7 +1229,7 @@ static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_
                            const int64_t *ts_d, const double *amount_d, int32_t n_windows,
                            int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
                            int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
-                           size_t ws_bytes, void *stream, const WinArgs *wa, int32_t *starts_d) {
+                           size_t ws_bytes, void *stream, const WinArgs *wa, int32_t *starts_d, bool grouped = false) {
     FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64, "bad argument");
     FDX_REQUIRE(seg_off_d && cperm_d && ts_d && amount_d && sorder_d && goff_d && its_d && iamt_d && irow_d &&
                     n_slots_h && ws,
@@ -1100,7 +1265,11 @@ static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_
         set_error("interleaved layout needs %u slots > max_slots %lld", total, (long long)max_slots);
         return FDX_E_WORKSPACE;
     }
-    if (starts_d)
+    if (starts_d && grouped)
+        hipLaunchKernelGGL((k_interleave<true, true>), dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
+                           cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
+                           (int64_t)total);
+    else if (starts_d)
         hipLaunchKernelGGL(k_interleave<true>, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
                            cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
                            (int64_t)total);
@@ -1132,6 +1301,20 @@ extern "C" int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_se
     FDX_REQUIRE(starts_d, "null pointer");
     return customer_layout(seg_off_d, n_seg, cperm_d, ts_d, amount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
                            irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, &wa, starts_d);
+}
+
+extern "C" int fdx_customer_layout_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                                  const int64_t *gts_d, const double *gamount_d,
+                                                  const int64_t *window_ns, int32_t n_windows, int32_t *sorder_d,
+                                                  uint32_t *goff_d, int64_t *its_d, double *iamt_d, int32_t *irow_d,
+                                                  int32_t *starts_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                                                  size_t ws_bytes, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(starts_d, "null pointer");
+    return customer_layout(seg_off_d, n_seg, cperm_d, gts_d, gamount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
+                           irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, &wa, starts_d, true);
 }
 
 extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *seg_off_d, const int32_t *sorder_d,

@@ -65,6 +65,15 @@ class GpuKernels:
         return ops.terminal_windows_packed_unsorted(ts, fraud, seg, delay_days, windows_days, rows=rows)
 
     @staticmethod
+    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days):
+        """owner side: stable re-key of the receive buffer by local terminal id carrying ts
+        (and the fraud bit in the perm), then the records of segments made of per-rank
+        time-sorted runs, indexed by receive position"""
+        perm, seg, gts, _ = ops.rekey_payload(rterm, n_local_terms, rts, flag=rfraud)
+        return ops.terminal_windows_grouped(gts, seg, rows=perm, delay_days=delay_days, windows_days=windows_days,
+                                            runs=True)
+
+    @staticmethod
     def reply_assemble(reply, perm, W, X, col0):
         check(_lib.load().fdx_reply_assemble(ops._ptr(reply), ops._ptr(perm), perm.numel(), W, ops._ptr(X),
                                              X.stride(0), col0, ops._s()), "fdx_reply_assemble")
@@ -100,8 +109,7 @@ def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows
     n_local_terms = (n_terminals_total + world - 1) // world
     # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
     # the records kernel handles such segments itself (no global time sort of the receive buffer)
-    perm, gseg = K.rekey(rterm, n_local_terms)                  # grouped position -> receive index
-    reply = K.terminal_records(rts, rfr, perm, gseg, delay_days, windows_days)  # indexed by receive index
+    reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days)  # by receive index
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
     dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
     return back, send_perm
@@ -170,8 +178,8 @@ class ShardedPipeline:
         base, n_local = self._range(n_customers_local)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")
-        cperm, cseg, _ = ops.rekey(cust, n_local)
-        cnb, cavg = ops.customer_windows(ops.gather(ts, cperm), ops.gather(amount, cperm), cseg, p.windows_days)
+        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        cnb, cavg = ops.customer_windows(gts, gamt, cseg, p.windows_days)
         n = ts.numel()
         ld = 16 if p.n_features <= 16 else p.n_features
         X = torch.empty((n, ld), dtype=torch.float64, device=ts.device)
@@ -204,9 +212,9 @@ class ShardedPipeline:
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
-        cperm, cseg, _ = ops.rekey(cust, n_local)
-        lay = ops.customer_layout(cseg, cperm, ts, amount, W, None, p._slots_hint,
-                                  p.windows_days)  # (host sync on main)
+        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, p.windows_days,
+                                  grouped=True)  # (host sync on main)
         rc.check()
         p._slots_hint = lay.its.numel()
         with torch.cuda.stream(side):

@@ -80,6 +80,34 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
     return perm, seg, sk
 
 
+def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
+                  flag: torch.Tensor | None = None, stream=None):
+    """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
+    grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
+    -> (perm int32, seg_off int64[n_keys+1], pay0 grouped | None, pay1 grouped | None)."""
+    _dev(keys, torch.int32, "keys")
+    n = keys.numel()
+    dev = keys.device
+    for t, nm in ((pay0, "pay0"), (pay1, "pay1")):
+        if t is not None:
+            if t.device.type != "cuda" or t.element_size() != 8 or not t.is_contiguous() or t.numel() != n:
+                raise FdxError(f"{nm} must be a contiguous 8-byte GPU column of {n} rows")
+    if pay1 is not None and pay0 is None:
+        raise FdxError("pay1 needs pay0")
+    if flag is not None:
+        _dev(flag, torch.uint8, "flag")
+    kb = max(key_bits_for(n_keys), 1)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+    o0 = torch.empty_like(pay0) if pay0 is not None else None
+    o1 = torch.empty_like(pay1) if pay1 is not None else None
+    L = _lib.load()
+    ws = workspace(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), dev)
+    check(L.fdx_rekey_payload(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm), _ptr(seg),
+                              _ptr(o0), _ptr(o1), _ptr(ws), ws.numel(), _s(stream)), "fdx_rekey_payload")
+    return perm, seg, o0, o1
+
+
 def key_map(keys: torch.Tensor, op: int, param: int, stream=None) -> torch.Tensor:
     """MOD: key % param, DIV: key / param, SUB: key - param (int32, on the GPU)."""
     _dev(keys, torch.int32, "keys")
@@ -197,9 +225,10 @@ class CustomerLayout:
 
 
 def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, _slots_hint=None,
-                    windows_days=None) -> CustomerLayout:
+                    windows_days=None, grouped: bool = False) -> CustomerLayout:
     """windows_days: also compute the window starts in the layout kernel (for
-    customer_windows_walk)."""
+    customer_windows_walk).  grouped: ts_ns / amount are in grouped order (rekey_payload
+    outputs) and are read as sequential streams (needs windows_days)."""
     _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(amount, torch.float64, "amount")
     n_seg = seg_off.numel() - 1
@@ -225,7 +254,8 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
             if len(windows_days) != int(n_windows):
                 raise FdxError("windows_days must have n_windows entries")
             starts = torch.empty(int(n_windows) * max_slots, dtype=torch.int32, device=dev)
-            rc = L.fdx_customer_layout_starts(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount),
+            fn = L.fdx_customer_layout_starts_grouped if grouped else L.fdx_customer_layout_starts
+            rc = fn(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount),
                                               _win_ns(windows_days), int(n_windows), _ptr(sorder), _ptr(goff),
                                               _ptr(its), _ptr(iamt), _ptr(irow), _ptr(starts), max_slots,
                                               ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
@@ -287,6 +317,38 @@ def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1
                                                   _win_ns(windows_days), W, _ptr(rec), _s(stream)),
           "fdx_terminal_windows_packed")
     return rec
+
+
+def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
+                             runs: bool = False, records: bool = True, stream=None):
+    """Terminal windows over grouped inputs (rekey_payload(terminal, ts, flag=fraud) outputs):
+    gts = grouped ts; fraud from gfraud (grouped uint8) or bit 31 of rows; record of grouped
+    position q written at row rows[q] & 0x7FFFFFFF (rows None: at q).  records: count records
+    int64 [n, W]; else (nb int32 [W, n], risk float64 [W, n]) at grouped positions."""
+    _dev(gts, torch.int64, "gts"); _dev(seg_off, torch.int64, "seg_off")
+    if rows is not None:
+        _dev(rows, torch.int32, "rows")
+    if gfraud is not None:
+        _dev(gfraud, torch.uint8, "gfraud")
+    if rows is None and gfraud is None:
+        raise FdxError("fraud comes from gfraud or from bit 31 of rows")
+    n = gts.numel()
+    W = len(windows_days)
+    dev = gts.device
+    scratch = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    L = _lib.load()
+    args = (_ptr(gts), _ptr(gfraud), _ptr(rows), _ptr(seg_off), seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
+            _win_ns(windows_days), W, int(bool(runs)))
+    if records:
+        rec = torch.empty((n, W), dtype=torch.int64, device=dev)
+        check(L.fdx_terminal_windows_grouped(*args, None, None, _ptr(rec), _ptr(scratch), _s(stream)),
+              "fdx_terminal_windows_grouped")
+        return rec
+    nb = torch.empty((W, n), dtype=torch.int32, device=dev)
+    risk = torch.empty((W, n), dtype=torch.float64, device=dev)
+    check(L.fdx_terminal_windows_grouped(*args, _ptr(nb), _ptr(risk), None, _ptr(scratch), _s(stream)),
+          "fdx_terminal_windows_grouped")
+    return nb, risk
 
 
 def terminal_windows_packed_dest(ts_ns, fraud, seg_off, rows, dest, n_out: int, delay_days=7,

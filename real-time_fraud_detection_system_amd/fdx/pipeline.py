@@ -65,12 +65,13 @@ class FraudPipeline:
             return f
         n = ts_ns.numel()
         we, ni = ops.time_flags(ts_ns, self.flags_mode, stream)
-        cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
-        cnb, cavg = ops.customer_windows(ops.gather(ts_ns, cperm, stream), ops.gather(amount, cperm, stream),
-                                         cseg, self.windows_days, stream)
-        tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
-        tnb, trisk = ops.terminal_windows(ops.gather(ts_ns, tperm, stream), ops.gather(fraud, tperm, stream),
-                                          tseg, self.delay_days, self.windows_days, stream)
+        # the re-keys carry the columns the window kernels read (grouped, sequential)
+        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=stream)
+        cnb, cavg = ops.customer_windows(gts, gamt, cseg, self.windows_days, stream)
+        tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, stream=stream)
+        tnb, trisk = ops.terminal_windows_grouped(tgts, tseg, gfraud=ops.gather(fraud, tperm, stream),
+                                                  delay_days=self.delay_days, windows_days=self.windows_days,
+                                                  records=False, stream=stream)
         f = Features(we, ni, cperm, cseg, cnb, cavg, tperm, tseg, tnb, trisk)
         if assemble:
             f.X = self.assemble(f, amount, stream)
@@ -118,9 +119,11 @@ class FraudPipeline:
         if validate:
             rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", stream),
                   ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", stream))
-        cperm, cseg, _ = ops.rekey(customer, n_customers, stream)
+        # the customer re-key carries ts and amount into grouped order (sequential layout reads)
+        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=stream)
         mk("rekey_customer")
-        lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, stream, self._slots_hint, self.windows_days)
+        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, stream, self._slots_hint, self.windows_days,
+                                  grouped=True)
         mk("customer_layout")
         if validate:
             for c in rc:
@@ -129,14 +132,12 @@ class FraudPipeline:
         self.last_slots = lay.n_slots
         inb, isum = ops.customer_windows_walk(lay, cseg, stream)
         mk("customer_walk")
-        tperm, tseg, _ = ops.rekey(terminal, n_terminals, stream)
+        # the terminal re-key carries ts (and TX_FRAUD in bit 31 of the perm); the records come
+        # out in input row order, read by the row assembly through the layout's irow
+        tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=stream)
         mk("rekey_terminal")
-        # count records in input row order (the kernel reads ts/fraud through tperm).  Measured
-        # (r01): writing them at their scoring slots instead (terminal_windows_packed_dest +
-        # invert_slots, sequential reads in the row assembly) costs the terminal kernel one
-        # more random read per row than it saves the assembly: 3.23 ms vs 2.93 ms.
-        trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days, rows=tperm,
-                                           stream=stream)
+        trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                            windows_days=self.windows_days, stream=stream)
         mk("terminal_windows")
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,

@@ -71,6 +71,11 @@ class CpuKernels:
         return torch.from_numpy(rec)
 
     @staticmethod
+    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days):
+        perm, seg = CpuKernels.rekey(rterm, n_local_terms)
+        return CpuKernels.terminal_records(rts, rfraud, perm, seg, delay_days, windows_days)
+
+    @staticmethod
     def unpack_reply(back, W):
         b = back.numpy()
         nb = (b & 0xFFFFFFFF).astype(np.float64)

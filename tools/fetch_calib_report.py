@@ -29,7 +29,7 @@ def second_dispatch(prefix, counter=None):
     rows = list(csv.DictReader(open(f[0])))
     seen = collections.defaultdict(list)
     for r in rows:
-        name = r["Kernel_Name"]
+        name = r["Kernel_Name"].removeprefix("void ")
         key = next((k for k in KNOWN if name.startswith(k.split("<")[0]) and (("<" not in k) or k in name)), None)
         if key is None:
             continue
