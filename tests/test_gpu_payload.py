@@ -112,7 +112,11 @@ def test_customer_layout_grouped_equals_gathering_form(dev):
     assert a.n_slots == b.n_slots
     for k in ("its", "iamt", "irow"):
         assert torch.equal(getattr(a, k)[: a.n_slots], getattr(b, k)[: b.n_slots]), k
-    assert torch.equal(a.starts[: 3 * a.n_slots], b.starts[: 3 * b.n_slots])
+    # the window starts (only defined for real rows; padding entries are never written):
+    # compare what the walk computes from them
+    valid = (a.irow[: a.n_slots] >= 0).cpu().numpy()
+    for x, y in zip(ops.customer_windows_walk(a, cseg), ops.customer_windows_walk(b, cseg)):
+        np.testing.assert_array_equal(x.cpu().numpy()[:, valid], y.cpu().numpy()[:, valid])
 
 
 def test_fused_pipeline_hot_terminal_matches_oracle(dev, golden):
