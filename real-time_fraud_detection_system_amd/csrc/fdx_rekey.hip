@@ -147,10 +147,10 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
 
 // Stable scatter of one tile.  vals_in == nullptr means "the value is the row index" (with
 // bit 31 = flag_in[row] != 0 when flag_in is given: fdx_rekey_payload's packed flag).
-// PW > 0: PW 8-byte payload streams ride along -- the element placed at tile position p came
-// from tile-local index s_src[p], so its payload is read from pay_in[base + s_src[p]] (a
-// random read inside the tile's own 4,096-row window: L2-resident, each line fetched from HBM
-// once) and written next to its key (the same coalesced runs).  The grouped payload then reads
+// PW > 0: PW 8-byte payload streams ride along.  After the keys are out, each stream is
+// loaded coalesced in input order, re-ordered through LDS (reusing the key/value buffers as
+// 4,096 8-byte slots) with the same tile permutation, and written to the destinations the key
+// pass computed: the same coalesced runs as the keys.  The grouped payload then reads
 // sequentially downstream, where gathering it through the permutation took a random HBM line
 // per 8-byte element (round-1 PMC: 3-6x the algorithmic bytes).
 template <typename K, int BITS, int PW>
@@ -164,9 +164,11 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     __shared__ uint32_t s_run[kBins];                  // digit counts of earlier rounds
     __shared__ uint32_t s_wcnt[kWavesPerBlock][kBins]; // this round's per-wave counts
     __shared__ uint32_t s_start[kBins];                // tile-local digit starts
-    __shared__ K s_key[kTile];
-    __shared__ uint32_t s_val[kTile];
-    __shared__ uint16_t s_src[PW ? kTile : 1];
+    // keys | values; later re-used as 4,096 8-byte payload slots (>= 8 bytes per element)
+    constexpr int kKeyWords = (int)(sizeof(K) / 4);
+    __shared__ __align__(16) uint32_t s_kv[(kKeyWords + 1) * kTile];
+    K *s_key = reinterpret_cast<K *>(s_kv);
+    uint32_t *s_val = s_kv + kKeyWords * kTile;
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -233,29 +235,55 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         }
     }
     __syncthreads();
+    uint32_t pos[kItems];  // tile position of each of this thread's items (payload re-order)
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const int64_t i = base + (int64_t)r * kBlock + tid;
         if (i < n) {
             const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
             const uint32_t p = s_start[d] + rank[r];
+            pos[r] = p;
             s_key[p] = key[r];
             s_val[p] = val[r];
-            if (PW) s_src[p] = (uint16_t)(r * kBlock + tid);
         }
     }
     __syncthreads();
     const int64_t cnt = std::min<int64_t>(kTile, n - base);
-    for (int p = tid; p < cnt; p += kBlock) {
-        const K k = s_key[p];
-        const uint32_t d = digit_of<K, BITS>(k, shift, flip);
-        const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
-        keys_out[dst] = k;
-        vals_out[dst] = s_val[p];
-        if constexpr (PW > 0) {
-            const int64_t src = base + s_src[p];
-            p0_out[dst] = p0_in[src];
-            if constexpr (PW > 1) p1_out[dst] = p1_in[src];
+    int32_t dsts[kItems];  // destination of tile position tid + j * kBlock
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int p = tid + j * kBlock;
+        if (p < cnt) {
+            const K k = s_key[p];
+            const uint32_t d = digit_of<K, BITS>(k, shift, flip);
+            const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
+            dsts[j] = (int32_t)dst;
+            keys_out[dst] = k;
+            vals_out[dst] = s_val[p];
+        }
+    }
+    if constexpr (PW > 0) {
+        uint64_t *s_pay = reinterpret_cast<uint64_t *>(s_kv);
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+            const uint64_t *pin = q == 0 ? p0_in : p1_in;
+            uint64_t *pout = q == 0 ? p0_out : p1_out;
+            uint64_t v[kItems];
+#pragma unroll
+            for (int r = 0; r < kItems; ++r) {  // coalesced, input order
+                const int64_t i = base + (int64_t)r * kBlock + tid;
+                v[r] = i < n ? pin[i] : 0ull;
+            }
+            __syncthreads();  // the previous contents of the LDS slots are consumed
+#pragma unroll
+            for (int r = 0; r < kItems; ++r)
+                if (base + (int64_t)r * kBlock + tid < n) s_pay[pos[r]] = v[r];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const int p = tid + j * kBlock;
+                if (p < cnt) pout[dsts[j]] = s_pay[p];
+            }
         }
     }
 }

@@ -109,42 +109,56 @@ class FraudPipeline:
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
-        slot, written there by the terminal kernel); the last forest launch writes proba back
-        in input row order.  mark(stage) is called after each stage is enqueued (bench.py
-        records a HIP event there); validate: the customer / terminal ids must lie in
-        [0, n_customers) / [0, n_terminals) (counted on the device, read at the layout's
-        host sync -- no extra stall)."""
+        row, read through the layout's irow); the last forest launch writes proba back in
+        input row order.
+
+        Streams: the terminal half (re-key + windows) runs on a side stream, concurrently with
+        the customer half on the caller's stream -- the customer walk is a latency-bound
+        recurrence with one lane per (customer, window) that leaves most SIMDs idle; the two
+        meet at the row assembly.  mark(stage, stream) is called after each stage is enqueued
+        on its stream (bench.py records a HIP event there).  validate: the customer / terminal
+        ids must lie in [0, n_customers) / [0, n_terminals) (counted on the device, read at
+        the layout's host sync -- no extra stall)."""
         W = len(self.windows_days)
-        mk = mark or (lambda _name: None)
+        mk = mark or (lambda _name, _st: None)
+        main = stream or torch.cuda.current_stream()
+        if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
+            self._side = torch.cuda.Stream(device=ts_ns.device)
+        side = self._side
+        mk("start", main)
         if validate:
-            rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", stream),
-                  ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", stream))
-        # the customer re-key carries ts and amount into grouped order (sequential layout reads)
-        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=stream)
-        mk("rekey_customer")
-        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, stream, self._slots_hint, self.windows_days,
+            rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
+                  ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
+        side.wait_stream(main)
+        mk("start", side)
+        # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
+        # perm); the records come out in input row order, read by the row assembly through irow
+        tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+        mk("rekey_terminal", side)
+        trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                            windows_days=self.windows_days, stream=side)
+        mk("terminal_windows", side)
+        # customer half (caller's stream): the re-key carries ts and amount into grouped order
+        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
+        mk("rekey_customer", main)
+        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint, self.windows_days,
                                   grouped=True)
-        mk("customer_layout")
+        mk("customer_layout", main)
         if validate:
             for c in rc:
                 c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
-        inb, isum = ops.customer_windows_walk(lay, cseg, stream)
-        mk("customer_walk")
-        # the terminal re-key carries ts (and TX_FRAUD in bit 31 of the perm); the records come
-        # out in input row order, read by the row assembly through the layout's irow
-        tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=stream)
-        mk("rekey_terminal")
-        trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                            windows_days=self.windows_days, stream=stream)
-        mk("terminal_windows")
+        inb, isum = ops.customer_windows_walk(lay, cseg, main)
+        mk("customer_walk", main)
+        main.wait_stream(side)
+        trec.record_stream(main)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                   ws, stream, n=lay.n_slots, val_is_sum=True)
-        mk("assemble_rows")
-        ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, stream)
-        mk("forest_traverse")
+                                   ws, main, n=lay.n_slots, val_is_sum=True)
+        mk("assemble_rows", main)
+        ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
+        mk("forest_traverse", main)
         return proba
 
     def _forest_ws(self, n_rows, ws, device):
