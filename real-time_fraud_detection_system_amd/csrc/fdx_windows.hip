@@ -495,7 +495,8 @@ template <int S_MAX, int kRing>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
-    int32_t *__restrict__ nb_out, double *__restrict__ sum_out, const int32_t *__restrict__ starts) {
+    int32_t *__restrict__ nb_out, double *__restrict__ sum_out, const int32_t *__restrict__ starts,
+    int32_t lg_min = 0, int32_t lg_max = INT32_MAX) {
     static_assert((kRing & (kRing - 1)) == 0 && kRing % kChunk == 0, "power-of-two ring of whole chunks");
     constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;  // chunk elements per lane
     constexpr int kRingEl = kRing * S_MAX + kWave;             // + one miss slot per lane
@@ -504,6 +505,7 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     const int64_t g = blockIdx.x;
     const int64_t s0 = sorder[g * S];
     const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
+    if (Lg < lg_min || Lg >= lg_max) return;  // another launch's length class
     const int l = lane / n_win, wi = lane - l * n_win;
     const int64_t si = g * S + l;
     const bool active = l < S && si < n_seg;
@@ -1317,6 +1319,27 @@ extern "C" int fdx_customer_layout_starts_grouped(const int64_t *seg_off_d, int6
                            irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, &wa, starts_d, true);
 }
 
+// A side stream (per device, created once) for launches that fork from the caller's stream
+// and join back before the call returns: the caller still sees one stream-ordered call.
+struct ForkStream {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static int fork_stream(ForkStream **out) {
+    static ForkStream per_dev[64];
+    int dev = 0;
+    FDX_HIP(hipGetDevice(&dev));
+    FDX_REQUIRE(dev >= 0 && dev < 64, "device id out of range");
+    ForkStream &f = per_dev[dev];
+    if (!f.side) {
+        FDX_HIP(hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking));
+        FDX_HIP(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming));
+        FDX_HIP(hipEventCreateWithFlags(&f.join, hipEventDisableTiming));
+    }
+    *out = &f;
+    return FDX_OK;
+}
+
 extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *seg_off_d, const int32_t *sorder_d,
                                          const uint32_t *goff_d, int64_t n_seg, int64_t n_slots, int32_t n_windows,
                                          const int32_t *starts_d, int32_t *nb_d, double *sum_d, void *stream) {
@@ -1327,9 +1350,35 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     const int32_t S = kWave / n_windows;
     FDX_REQUIRE(S <= 21, "the walk kernel is built for <= 21 segments per wave (>= 3 windows)");
     const int64_t n_groups = ceil_div(n_seg, S);
-    hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, as_stream(stream), iamt_d,
-                       seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d);
+    hipStream_t st = as_stream(stream);
+    // Length classes: the groups of the longest segments (the busiest customers, whose
+    // longest window holds more rows than the 128-row ring minus a chunk, so nearly every
+    // removal would miss the ring and wait on a dependent global load) walk with a 256-row
+    // ring on a forked stream, concurrently with the rest on the 128-row ring (twice the
+    // blocks per CU).  FDX_CUSTOMER_WALK_SPLIT = the class boundary in rows (0 = one launch).
+    static const int split = [] {
+        const char *e = getenv("FDX_CUSTOMER_WALK_SPLIT");
+        return e ? atoi(e) : 480;
+    }();
+    if (split <= 0) {
+        hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d, seg_off_d,
+                           sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, 0, INT32_MAX);
+        FDX_LAUNCHED("k_customer_walk");
+        return FDX_OK;
+    }
+    ForkStream *f;
+    int rc = fork_stream(&f);
+    if (rc) return rc;
+    FDX_HIP(hipEventRecord(f->fork, st));
+    FDX_HIP(hipStreamWaitEvent(f->side, f->fork, 0));
+    hipLaunchKernelGGL((k_customer_walk<21, 256>), dim3((unsigned)n_groups), dim3(64), 0, f->side, iamt_d, seg_off_d,
+                       sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, split, INT32_MAX);
     FDX_LAUNCHED("k_customer_walk");
+    hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d, seg_off_d,
+                       sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, 0, split);
+    FDX_LAUNCHED("k_customer_walk");
+    FDX_HIP(hipEventRecord(f->join, f->side));
+    FDX_HIP(hipStreamWaitEvent(st, f->join, 0));
     return FDX_OK;
 }
 

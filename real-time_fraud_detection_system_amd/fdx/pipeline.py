@@ -130,14 +130,19 @@ class FraudPipeline:
             rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
                   ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
         side.wait_stream(main)
-        mk("start", side)
         # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
-        # perm); the records come out in input row order, read by the row assembly through irow
-        tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
-        mk("rekey_terminal", side)
-        trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                            windows_days=self.windows_days, stream=side)
-        mk("terminal_windows", side)
+        # perm); the records come out in input row order, read by the row assembly through irow.
+        # Allocated under the side stream's context, so that the caching allocator hands
+        # these buffers to nothing on the main stream while the side stream still uses them.
+        with torch.cuda.stream(side):
+            mk("start", side)
+            tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+            mk("rekey_terminal", side)
+            trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                windows_days=self.windows_days, stream=side)
+            mk("terminal_windows", side)
+        for t in (ts_ns, terminal, fraud):
+            t.record_stream(side)  # inputs in use on the side stream
         # customer half (caller's stream): the re-key carries ts and amount into grouped order
         cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
         mk("rekey_customer", main)
