@@ -1110,9 +1110,11 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
                 const int k = g + j;
                 if (k < K) {
                     const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
-                    uint32_t st;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
-                    asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %0"
-                        : "+v"(pa[k]), "=&v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
+                    uint32_t st, pn;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
+                    // (a separate output: a read-write operand made the compiler copy pa first)
+                    asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %4"
+                        : "=v"(pn), "=&v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>), "v"(pa[k]));
+                    pa[k] = pn;
                     nd[k] = lds32(lds, pa[k]);
                     __builtin_amdgcn_sched_barrier(0);
                 }

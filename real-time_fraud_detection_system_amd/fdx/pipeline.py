@@ -14,6 +14,7 @@ sorts them on the GPU.  All outputs are returned in input row order.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -36,6 +37,12 @@ class Features:
     term_nb: torch.Tensor        # int32 [W, n] grouped order
     term_risk: torch.Tensor      # float64 [W, n] grouped order
     X: Optional[torch.Tensor] = None  # float64 [n, ld] input_features in row order
+
+
+# A/B switches for measurements (bench / profiling runs); the defaults are the measured-best forms
+_OVERLAP = os.environ.get("FDX_OVERLAP", "1") != "0"            # terminal half on a side stream
+_CUST_PAYLOAD = os.environ.get("FDX_CUSTOMER_PAYLOAD", "1") != "0"  # re-key carries ts / amount
+_TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key carries ts + fraud bit
 
 
 class FraudPipeline:
@@ -129,6 +136,8 @@ class FraudPipeline:
         if validate:
             rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
                   ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
+        if not _OVERLAP:
+            side = main
         side.wait_stream(main)
         # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
         # perm); the records come out in input row order, read by the row assembly through irow.
@@ -136,18 +145,29 @@ class FraudPipeline:
         # these buffers to nothing on the main stream while the side stream still uses them.
         with torch.cuda.stream(side):
             mk("start", side)
-            tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
-            mk("rekey_terminal", side)
-            trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                windows_days=self.windows_days, stream=side)
+            if _TERM_PAYLOAD:
+                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+                mk("rekey_terminal", side)
+                trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                    windows_days=self.windows_days, stream=side)
+            else:  # round-1 form: plain re-key, the kernel gathers ts / fraud through the perm
+                tperm, tseg, _ = ops.rekey(terminal, n_terminals, side)
+                mk("rekey_terminal", side)
+                trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days,
+                                                   rows=tperm, stream=side)
             mk("terminal_windows", side)
         for t in (ts_ns, terminal, fraud):
             t.record_stream(side)  # inputs in use on the side stream
         # customer half (caller's stream): the re-key carries ts and amount into grouped order
-        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
-        mk("rekey_customer", main)
-        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint, self.windows_days,
-                                  grouped=True)
+        if _CUST_PAYLOAD:
+            cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
+            mk("rekey_customer", main)
+            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint, self.windows_days,
+                                      grouped=True)
+        else:  # round-1 form: plain re-key, the layout gathers ts / amount through the perm
+            cperm, cseg, _ = ops.rekey(customer, n_customers, main)
+            mk("rekey_customer", main)
+            lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, main, self._slots_hint, self.windows_days)
         mk("customer_layout", main)
         if validate:
             for c in rc:
