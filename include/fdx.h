@@ -339,7 +339,10 @@ int fdx_forest_pack_rank2(const fdx_forest_desc *desc, int32_t version, uint32_t
                           double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out, int32_t *depth_out,
                           float *thr_out, int32_t *thr_off_out /* [33] */, int32_t *slot_feat_out /* [32] */,
                           int32_t *slot_base_out /* [32] */);
-/* *layout = 0 (wide 8-byte nodes), 1 (rank v1) or 2 (rank v2); *n_slots = rank slots. */
+/* *layout = 0 (wide 8-byte nodes), 1 (rank v1), 2 (rank v2) or 3 (rank v2 with one slot per
+ * feature: v1 row format, compact 32 KiB row planes -- the default when the forest fits it);
+ * *n_slots = rank slots.  fdx_forest_set_variant rebuilds the rank layout in the other node
+ * format when the requested variant needs it. */
 int fdx_forest_layout(fdx_forest forest, int32_t *layout, int32_t *n_slots);
 int fdx_forest_destroy(fdx_forest forest);
 int fdx_forest_info(fdx_forest forest, int32_t *n_trees, int32_t *n_features, int64_t *n_nodes,
@@ -374,8 +377,9 @@ int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
  * (4-byte nodes, u16 rank rows; see fdx_forest_pack_rank): 16 = 1024 x 1 x 4 (the default
  * when the forest fits the rank layout), 17 = 1024 x 1 x 2, 18 = 512 x 2 x 2,
  * 19 = 512 x 2 x 4, 20 = 1024 x 1 x 3, 21 = 768 x 1 x 4, 22 = 256 x 4 x 2, 23 = 1024 x 1 x 6,
- * ..., 41 = 1024 x 1 x 6 pipelined (the v1 default); rank layout v2: 44 = 1024 x 1 x 6 (default),
- * 45 = 1024 x 1 x 4.
+ * ..., 41 = 1024 x 1 x 6 pipelined (v1); rank layout v2: 44 = 1024 x 1 x 6 (32 slots, the default
+ * of forests needing more than one slot for a feature), 45 = 1024 x 1 x 4; v2 over compact 16-slot
+ * planes: 46 = 1024 x 1 x 6 (the default when every feature fits one slot), 47 = 1024 x 1 x 8.
  * Variants > 0 need <= 16 features, 16+ need the rank layout (FDX_E_UNSUPPORTED otherwise).
  * Re-cuts the LDS chunks; results are identical for every variant.  The row format of a
  * prepared workspace depends on the layout: prepare again after switching layouts. */

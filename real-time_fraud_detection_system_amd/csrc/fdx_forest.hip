@@ -70,6 +70,12 @@ struct fdx_forest_s {
     int32_t ruoff[32] = {}, rsoff[32] = {}, rscnt[32] = {}, rseg = 16, rnsmp = 0;
     // rank layout v2 (32 threshold-rank slots, see build_rank_layout)
     bool rank_v2 = false;
+    bool rank_identity = false;  // v2 with slot s = feature s (<= 16 slots): v1 rank rows, compact planes
+    // host copies of the packed forest and scaler (set_variant rebuilds the rank layout in the
+    // other node format when a variant needs it)
+    std::vector<uint64_t> h_packed;
+    std::vector<int32_t> h_orig, h_depth;
+    std::vector<double> h_mean, h_scale;
     int32_t rn_slots = 0, rslot_feat[32] = {}, rslot_base[32] = {};
     int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
 };
@@ -779,8 +785,11 @@ constexpr Variant kVariants[] = {
     // 41.. grouped waits (pipe = group width)
     {1024, 1, 6, 0, 1, 0, 2}, {1024, 1, 6, 0, 1, 0, 3}, {1024, 1, 6, 0, 1, 0, 6},
     // 44..: rank layout v2 (32 threshold-rank slots, u16 planes of 1,024 rows; p16 = 2)
-    {1024, 1, 6, 0, 1, 2, 2}, {1024, 1, 4, 0, 1, 2, 2}};
+    {1024, 1, 6, 0, 1, 2, 2}, {1024, 1, 4, 0, 1, 2, 2},
+    // 46..: v2 nodes over 16 slots of 1,024 u16 rows (32 KiB of planes; slot = feature, v1 rows)
+    {1024, 1, 6, 0, 1, 3, 2}, {1024, 1, 8, 0, 1, 3, 2}};
 constexpr int kDefaultRankV2Variant = 44;
+constexpr int kDefaultRankCompactVariant = 46;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -1040,9 +1049,14 @@ __device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
 // offset (rank layout v1); 1 = the same nodes over u16 planes; 2 = rank layout v2: u16 planes
 // of 1,024 rows, a 5-bit SLOT field and an 11-bit right offset (see build_rank_layout).
 template <int P16>
-constexpr uint32_t kSlotMask = P16 == 2 ? 0xF800u : 0xF000u;
+constexpr uint32_t kSlotMask = P16 >= 2 ? 0xF800u : 0xF000u;
 template <int P16>
-constexpr uint32_t kOffMask = P16 == 2 ? 0x7FFu : 0xFFFu;
+constexpr uint32_t kOffMask = P16 >= 2 ? 0x7FFu : 0xFFFu;
+// 3 = the v2 node format over 16 u16 planes of 1,024 rows (32 KiB): forests whose every feature
+// fits one slot (slot = feature, the v1 row format); the node region starts at 32 KiB, so a
+// chunk holds a third more nodes than with 64 KiB of planes (fewer chunk launches per batch)
+template <int P16>
+constexpr uint32_t kNodeB = P16 == 3 ? 32768u : kRankNodeB;
 
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
@@ -1056,7 +1070,7 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
     for (int k = 0; k < K; ++k) {
         uint32_t st;
         if (NAN_AWARE && x[k] == (P16 ? 0xFFFFu : 0xFFFFFFFFu)) {
-            st = mleft[(pa[k] - kRankNodeB) >> 2] != 0 ? 1u : (nd[k] & kOffMask<P16>);
+            st = mleft[(pa[k] - kNodeB<P16>) >> 2] != 0 ? 1u : (nd[k] & kOffMask<P16>);
         } else {
             const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
             asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
@@ -1148,7 +1162,7 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
     int dmax = 0;
 #pragma unroll
     for (int g = 0; g < GG; ++g) {
-        const uint32_t p0 = kRankNodeB + (uint32_t)(root[t + g] - node_base) * 4u;
+        const uint32_t p0 = kNodeB<P16> + (uint32_t)(root[t + g] - node_base) * 4u;
         const uint32_t n0 = lds32(lds, p0);
         dmax = max(dmax, depth[t + g]);
 #pragma unroll
@@ -1168,9 +1182,10 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
 
 template <int K>
 __device__ __forceinline__ void rank_leaf_values(const uint32_t (&pa)[K], int64_t node_base,
-                                                 const double *__restrict__ lval, double (&v)[K]) {
+                                                 const double *__restrict__ lval, double (&v)[K],
+                                                 uint32_t nodeb = kRankNodeB) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = lval[node_base + ((pa[k] - kRankNodeB) >> 2)];
+    for (int k = 0; k < K; ++k) v[k] = lval[node_base + ((pa[k] - nodeb) >> 2)];
 }
 
 // a[r] += v[r*GG + g] in tree order
@@ -1186,7 +1201,8 @@ template <int R, int GG>
 __device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int64_t node_base, int t,
                                               const int64_t (&row)[R], const bool (&ok)[R],
                                               const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out,
-                                              const int32_t *__restrict__ orig, int32_t n_trees) {
+                                              const int32_t *__restrict__ orig, int32_t n_trees,
+                                              uint32_t nodeb = kRankNodeB) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!ok[r]) continue;
@@ -1194,7 +1210,7 @@ __device__ __forceinline__ void rank_leaf_ids(const uint32_t (&pa)[R * GG], int6
         if (dst < 0) continue;
 #pragma unroll
         for (int g = 0; g < GG; ++g)
-            leaf_out[dst * n_trees + t + g] = orig[node_base + ((pa[r * GG + g] - kRankNodeB) >> 2)];
+            leaf_out[dst * n_trees + t + g] = orig[node_base + ((pa[r * GG + g] - nodeb) >> 2)];
     }
 }
 
@@ -1242,6 +1258,8 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     // u32 planes: 1,024 rows x 16 slots; u16 planes: 2,048 rows x 16 slots; v2: 1,024 rows x 32 slots
     constexpr int kPlaneRows = P16 == 1 ? 2 * kRankPlaneRows : kRankPlaneRows;
     constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
+    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS
+    constexpr uint32_t kNB = kNodeB<P16>;
     if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
         const int c = blockIdx.y;
         t0 = chunk_t[c];
@@ -1254,14 +1272,14 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
-    constexpr int kNodeWords = (kLdsTotal - kRankXWords * 4) / 4;
-    __shared__ __align__(16) uint32_t s_mem[kRankXWords + kNodeWords];
+    constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
+    __shared__ __align__(16) uint32_t s_mem[kXW + kNodeWords];
     uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
     const int tid = threadIdx.x;
     {
         const uint32_t *nb = nodes + node_base;
-        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kRankXWords + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
     }
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
@@ -1314,7 +1332,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
             } else {
                 const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
 #pragma unroll
-                for (int f = 0; f < 15; ++f) {
+                for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
                     const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
                     if (P16)
                         s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
@@ -1332,10 +1350,10 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
             uint32_t pa[K];
             rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
             if (pending) rank_accumulate<R, G>(a, pv);
-            rank_leaf_values<K>(pa, node_base, lval, pv);
+            rank_leaf_values<K>(pa, node_base, lval, pv, kNB);
             if (tv) rank_tree_values<R, G>(pv, t, row, ok, tv, tv_n);
             pending = true;
-            if (leaf_out) rank_leaf_ids<R, G>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees);
+            if (leaf_out) rank_leaf_ids<R, G>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees, kNB);
         }
         const int nt = t1 - t;
 #define FDX_RANK_TAIL(NT)                                                                                  \
@@ -1346,10 +1364,10 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
             rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);           \
             if (pending) rank_accumulate<R, G>(a, pv);                                                     \
             pending = false;                                                                               \
-            rank_leaf_values<R * NT>(pt, node_base, lval, vt);                                             \
+            rank_leaf_values<R * NT>(pt, node_base, lval, vt, kNB);                                        \
             if (tv) rank_tree_values<R, NT>(vt, t, row, ok, tv, tv_n);                                     \
             rank_accumulate<R, NT>(a, vt);                                                                 \
-            if (leaf_out) rank_leaf_ids<R, NT>(pt, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees); \
+            if (leaf_out) rank_leaf_ids<R, NT>(pt, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees, kNB); \
         }                                                                                                  \
     }
         FDX_RANK_TAIL(1)
@@ -1669,9 +1687,11 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
 
 namespace fdx {
 namespace {
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
+constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
 
 bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
 
@@ -1681,7 +1701,8 @@ bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; 
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
     F->tile_ok = v.tile != 0;
-    const int64_t cap_nodes = v.rank ? kRankNodeCap : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
+    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
+                                     : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
     F->chunks.clear();
@@ -1731,9 +1752,18 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
         set_error("variant %d needs the rank layout, which this forest does not fit", variant);
         return FDX_E_UNSUPPORTED;
     }
-    if (kVariants[variant].rank && (kVariants[variant].p16 == 2) != F->rank_v2) {
-        set_error("variant %d is for rank layout v%d; this forest uses v%d", variant,
-                  kVariants[variant].p16 == 2 ? 2 : 1, F->rank_v2 ? 2 : 1);
+    if (kVariants[variant].rank && (kVariants[variant].p16 >= 2) != F->rank_v2) {
+        // the variant runs on the other node format: rebuild the rank layout in it
+        const bool want_v2 = kVariants[variant].p16 >= 2;
+        int rc = install_rank_layout(F, want_v2, nullptr);
+        if (rc) {
+            install_rank_layout(F, !want_v2, nullptr);  // restore the previous format
+            set_error("variant %d needs rank layout v%d, which this forest does not fit", variant, want_v2 ? 2 : 1);
+            return FDX_E_UNSUPPORTED;
+        }
+    }
+    if (kVariants[variant].rank && kVariants[variant].p16 == 3 && !F->rank_identity) {
+        set_error("variant %d needs one threshold slot per feature (<= 16 slots)", variant);
         return FDX_E_UNSUPPORTED;
     }
     const int prev = F->variant;
@@ -1818,7 +1848,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
 
 extern "C" int fdx_forest_layout(fdx_forest F, int32_t *layout, int32_t *n_slots) {
     FDX_REQUIRE(F && layout && n_slots, "null pointer");
-    *layout = !F->rank_ok ? 0 : (F->rank_v2 ? 2 : 1);
+    *layout = !F->rank_ok ? 0 : (F->rank_v2 ? (F->rank_identity ? 3 : 2) : 1);
     *n_slots = F->rank_v2 ? F->rn_slots : (F->rank_ok ? 16 : 0);
     return FDX_OK;
 }
@@ -1856,6 +1886,126 @@ extern "C" int fdx_forest_pack_rank(const fdx_forest_desc *d, uint32_t *nodes_ou
     return FDX_OK;
 }
 
+namespace fdx {
+namespace {
+void free_rank_buffers(fdx_forest_s *F) {
+    void **bufs[] = {(void **)&F->rnodes_d, (void **)&F->rorig_d, (void **)&F->rlval_d, (void **)&F->rml_d,
+                     (void **)&F->rroot_d, (void **)&F->rdepth_d, (void **)&F->rthr_d, (void **)&F->rseg_d,
+                     (void **)&F->ritab_d, (void **)&F->rrat_d, (void **)&F->rsmp_d};
+    for (void **b : bufs) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+}
+
+// Build the rank layout (v2 nodes when `v2`, else v1) from the host copy of the packed forest
+// and upload it with its search tables; synchronous (creation / set_variant, off the hot path).
+// On FDX_E_UNSUPPORTED the forest has no rank layout (rank_ok = false).
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
+    free_rank_buffers(F);
+    F->rank_ok = F->rank_v2 = F->rank_identity = false;
+    fdx_forest_desc d{};
+    d.n_trees = F->n_trees;
+    d.n_features = F->n_features;
+    d.node_offsets = F->node_offsets.data();
+    RankLayout RL;
+    if (v2 && F->zstride != 16) return FDX_E_UNSUPPORTED;
+    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2);
+    if (rc) return rc;
+    F->rank_ok = true;
+    F->rank_v2 = v2;
+    if (v2) {
+        bool ident = RL.n_slots <= 16 && RL.n_slots == F->n_features;
+        for (int j = 0; j < RL.n_slots && ident; ++j) ident = RL.slot_feat[j] == j && RL.slot_base[j] == 0;
+        F->rank_identity = ident;
+    }
+    const int nfs = v2 ? 32 : 16;
+    F->rank_offsets = RL.offsets;
+    F->rank_nodes = (int64_t)RL.nodes.size();
+    for (int f = 0; f < 32; ++f) {
+        F->rthr_off[f] = f < nfs ? RL.thr_off[f] : 0;
+        F->rthr_cnt[f] = f < nfs ? RL.thr_off[f + 1] - RL.thr_off[f] : 0;
+    }
+    F->rn_slots = RL.n_slots;
+    for (int j = 0; j < 32; ++j) {
+        F->rslot_feat[j] = RL.slot_feat[j];
+        F->rslot_base[j] = RL.slot_base[j];
+    }
+    // two-level search tables (RankTab): smallest segment with <= kMaxRankSamples samples
+    std::vector<float> useg, smp;
+    std::vector<uint16_t> itab, rat;
+    int seg = 16;
+    for (;; seg *= 2) {
+        int64_t m = 0;
+        for (int f = 0; f < nfs; ++f) m += ceil_div(F->rthr_cnt[f], seg);
+        if (m <= kMaxRankSamples) break;
+    }
+    F->rseg = seg;
+    for (int f = 0; f < nfs; ++f) {
+        const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, seg);
+        F->ruoff[f] = (int32_t)useg.size();
+        F->rsoff[f] = (int32_t)smp.size();
+        F->rscnt[f] = ns;
+        for (int32_t j = 0; j < ns * seg; ++j) useg.push_back(j < c ? RL.thr[(size_t)(RL.thr_off[f] + j)] : INFINITY);
+        for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
+    }
+    F->rnsmp = (int32_t)smp.size();
+    // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every
+    // searched feature unconditionally (a feature without thresholds points here)
+    for (int j = 0; j < 16; ++j) useg.push_back(INFINITY);
+    if (smp.empty()) smp.push_back(INFINITY);
+    // integer / ratio rank tables of the scoring pipeline's prepares (the v1 row format: one
+    // slot per feature): the same float64 scaling and float32 cast as zval(), then the
+    // lower_bound the device search computes (bit-identical arithmetic on the host)
+    itab.assign((size_t)16 * kIntTab, 0);
+    rat.assign((size_t)16 * kRatN * kRatN, 0);
+    for (int f = 0; f < 16 && f < F->n_features && (!v2 || F->rank_identity); ++f) {
+        const float *u0 = RL.thr.data() + RL.thr_off[f], *u1 = RL.thr.data() + RL.thr_off[f + 1];
+        const double *mean = F->h_mean.empty() ? nullptr : F->h_mean.data();
+        const double *scale = F->h_scale.empty() ? nullptr : F->h_scale.data();
+        for (int c = 0; c < kIntTab; ++c) {
+            double x = (double)c;
+            if (mean) x = x - mean[f];
+            if (scale) x = x / scale[f];
+            itab[(size_t)f * kIntTab + c] = (uint16_t)(std::lower_bound(u0, u1, (float)x) - u0);
+        }
+        for (int nb = 0; nb < kRatN; ++nb)  // term_risk(): nb > 0 ? fr / nb : 0.0
+            for (int fr = 0; fr < kRatN; ++fr) {
+                double x = nb > 0 ? (double)fr / (double)nb : 0.0;
+                if (mean) x = x - mean[f];
+                if (scale) x = x / scale[f];
+                rat[((size_t)f * kRatN + nb) * kRatN + fr] = (uint16_t)(std::lower_bound(u0, u1, (float)x) - u0);
+            }
+    }
+    const size_t rn = RL.nodes.size(), nt = (size_t)F->n_trees, nthr = std::max<size_t>(RL.thr.size(), 1);
+    FDX_HIP(hipMalloc(&F->rnodes_d, 4 * rn));
+    FDX_HIP(hipMalloc(&F->rorig_d, 4 * rn));
+    FDX_HIP(hipMalloc(&F->rlval_d, 8 * rn));
+    FDX_HIP(hipMalloc(&F->rml_d, rn));
+    FDX_HIP(hipMalloc(&F->rroot_d, 4 * nt));
+    FDX_HIP(hipMalloc(&F->rdepth_d, 4 * nt));
+    FDX_HIP(hipMalloc(&F->rthr_d, 4 * nthr));
+    FDX_HIP(hipMalloc(&F->rseg_d, 4 * useg.size()));
+    FDX_HIP(hipMalloc(&F->rsmp_d, 4 * smp.size()));
+    FDX_HIP(hipMalloc(&F->ritab_d, 2 * itab.size()));
+    FDX_HIP(hipMalloc(&F->rrat_d, 2 * rat.size()));
+    FDX_HIP(hipMemcpyAsync(F->rseg_d, useg.data(), 4 * useg.size(), hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rrat_d, rat.data(), 2 * rat.size(), hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rlval_d, RL.lval.data(), 8 * rn, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rml_d, RL.ml.data(), rn, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rroot_d, RL.root.data(), 4 * nt, hipMemcpyHostToDevice, st));
+    FDX_HIP(hipMemcpyAsync(F->rdepth_d, RL.depth.data(), 4 * nt, hipMemcpyHostToDevice, st));
+    if (!RL.thr.empty()) FDX_HIP(hipMemcpyAsync(F->rthr_d, RL.thr.data(), 4 * RL.thr.size(), hipMemcpyHostToDevice, st));
+    FDX_HIP(hipStreamSynchronize(st));  // the host vectors die at return
+    return FDX_OK;
+}
+}  // namespace
+}  // namespace fdx
+
 extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void *stream) {
     FDX_REQUIRE(d && out, "null pointer");
     *out = nullptr;
@@ -1871,28 +2021,11 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->zstride = d->n_features <= 16 ? 16 : 32;
     F->n_nodes = total;
     F->node_offsets.assign(d->node_offsets, d->node_offsets + d->n_trees + 1);
-    RankLayout RL;
-    F->rank_ok = build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL) == FDX_OK;
-    if (!F->rank_ok && F->zstride == 16 && build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, true) == FDX_OK)
-        F->rank_ok = F->rank_v2 = true;  // v2: more thresholds per feature than v1's 15-bit ranks hold
-    set_error("");
-    // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
-    F->variant = F->rank_ok ? (F->rank_v2 ? kDefaultRankV2Variant : kDefaultRankVariant) : (F->zstride == 16 ? 1 : 0);
-    const int nfs = F->rank_v2 ? 32 : 16;
-    if (F->rank_ok) {
-        F->rank_offsets = RL.offsets;
-        F->rank_nodes = (int64_t)RL.nodes.size();
-        for (int f = 0; f < nfs; ++f) {
-            F->rthr_off[f] = RL.thr_off[f];
-            F->rthr_cnt[f] = RL.thr_off[f + 1] - RL.thr_off[f];
-        }
-        F->rn_slots = RL.n_slots;
-        for (int j = 0; j < 32; ++j) {
-            F->rslot_feat[j] = RL.slot_feat[j];
-            F->rslot_base[j] = RL.slot_base[j];
-        }
-    }
-    build_chunks(F);
+    F->h_packed = packed;
+    F->h_orig = orig;
+    F->h_depth = depth;
+    if (d->scaler_mean) F->h_mean.assign(d->scaler_mean, d->scaler_mean + d->n_features);
+    if (d->scaler_scale) F->h_scale.assign(d->scaler_scale, d->scaler_scale + d->n_features);
     hipStream_t st = as_stream(stream);
     auto fail = [&](hipError_t e, const char *what) {
         set_error("%s failed: %s", what, hipGetErrorString(e));
@@ -1906,6 +2039,23 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
             return fail(e, "hipDeviceGetAttribute");
         if (ncu > 0) F->n_cu = ncu;
     }
+    // Rank layout choice: v2 nodes when the forest fits them (FDX_RANK_V1=1 forces v1 for A/B);
+    // a v2 forest whose every feature needs one slot keeps v1's row format (slot = feature) and
+    // runs on the compact 32 KiB planes; else v1; else the wide 8-byte layout.
+    static const bool force_v1 = getenv("FDX_RANK_V1") != nullptr;
+    rc = install_rank_layout(F, !force_v1, st);
+    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, force_v1, st);
+    if (rc == FDX_E_UNSUPPORTED) rc = FDX_OK;  // the wide layout serves it
+    if (rc) {
+        fdx_forest_destroy(F);
+        return rc;
+    }
+    set_error("");
+    // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
+    F->variant = !F->rank_ok ? (F->zstride == 16 ? 1 : 0)
+                             : (!F->rank_v2 ? kDefaultRankVariant
+                                            : (F->rank_identity ? kDefaultRankCompactVariant : kDefaultRankV2Variant));
+    build_chunks(F);
     if ((e = hipMalloc(&F->nodes_d, sizeof(uint64_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->root_d, sizeof(int32_t) * d->n_trees)) != hipSuccess) return fail(e, "hipMalloc");
@@ -1921,77 +2071,6 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
         return fail(e, "hipMemcpyAsync");
     if ((e = hipMemcpyAsync(F->root_d, root.data(), sizeof(int32_t) * d->n_trees, hipMemcpyHostToDevice, st)))
         return fail(e, "hipMemcpyAsync");
-    std::vector<float> useg, smp;
-    std::vector<uint16_t> itab, rat;
-    if (F->rank_ok) {  // two-level search tables (RankTab): smallest segment with <= kMaxRankSamples samples
-        int seg = 16;
-        for (;; seg *= 2) {
-            int64_t m = 0;
-            for (int f = 0; f < nfs; ++f) m += ceil_div(F->rthr_cnt[f], seg);
-            if (m <= kMaxRankSamples) break;
-        }
-        F->rseg = seg;
-        for (int f = 0; f < nfs; ++f) {
-            const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, seg);
-            F->ruoff[f] = (int32_t)useg.size();
-            F->rsoff[f] = (int32_t)smp.size();
-            F->rscnt[f] = ns;
-            for (int32_t j = 0; j < ns * seg; ++j)
-                useg.push_back(j < c ? RL.thr[(size_t)(RL.thr_off[f] + j)] : INFINITY);
-            for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
-        }
-        F->rnsmp = (int32_t)smp.size();
-        // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every
-        // searched feature unconditionally (a feature without thresholds points here)
-        for (int j = 0; j < 16; ++j) useg.push_back(INFINITY);
-        if (smp.empty()) smp.push_back(INFINITY);
-        // integer rank table: the same float64 scaling and float32 cast as zval(), then the
-        // lower_bound the device search computes (bit-identical arithmetic on the host)
-        itab.assign((size_t)16 * kIntTab, 0);
-        rat.assign((size_t)16 * kRatN * kRatN, 0);
-        for (int f = 0; f < 16 && f < d->n_features && !F->rank_v2; ++f) {  // (v1 scoring pipeline only)
-            const float *u0 = RL.thr.data() + RL.thr_off[f], *u1 = RL.thr.data() + RL.thr_off[f + 1];
-            for (int c = 0; c < kIntTab; ++c) {
-                double x = (double)c;
-                if (d->scaler_mean) x = x - d->scaler_mean[f];
-                if (d->scaler_scale) x = x / d->scaler_scale[f];
-                const float zf = (float)x;
-                itab[(size_t)f * kIntTab + c] = (uint16_t)(std::lower_bound(u0, u1, zf) - u0);
-            }
-            for (int nb = 0; nb < kRatN; ++nb)  // term_risk(): nb > 0 ? fr / nb : 0.0
-                for (int fr = 0; fr < kRatN; ++fr) {
-                    double x = nb > 0 ? (double)fr / (double)nb : 0.0;
-                    if (d->scaler_mean) x = x - d->scaler_mean[f];
-                    if (d->scaler_scale) x = x / d->scaler_scale[f];
-                    const float zf = (float)x;
-                    rat[((size_t)f * kRatN + nb) * kRatN + fr] = (uint16_t)(std::lower_bound(u0, u1, zf) - u0);
-                }
-        }
-    }
-    if (F->rank_ok) {
-        const size_t rn = RL.nodes.size(), nt = (size_t)d->n_trees, nthr = std::max<size_t>(RL.thr.size(), 1);
-        if ((e = hipMalloc(&F->rnodes_d, 4 * rn)) || (e = hipMalloc(&F->rorig_d, 4 * rn)) ||
-            (e = hipMalloc(&F->rlval_d, 8 * rn)) || (e = hipMalloc(&F->rml_d, rn)) ||
-            (e = hipMalloc(&F->rroot_d, 4 * nt)) || (e = hipMalloc(&F->rdepth_d, 4 * nt)) ||
-            (e = hipMalloc(&F->rthr_d, 4 * nthr)) || (e = hipMalloc(&F->rseg_d, 4 * useg.size())) ||
-            (e = hipMalloc(&F->rsmp_d, 4 * smp.size())) || (e = hipMalloc(&F->ritab_d, 2 * itab.size())) ||
-            (e = hipMalloc(&F->rrat_d, 2 * rat.size())))
-            return fail(e, "hipMalloc");
-        if ((e = hipMemcpyAsync(F->rseg_d, useg.data(), 4 * useg.size(), hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rrat_d, rat.data(), 2 * rat.size(), hipMemcpyHostToDevice, st)))
-            return fail(e, "hipMemcpyAsync");
-        if ((e = hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rlval_d, RL.lval.data(), 8 * rn, hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rml_d, RL.ml.data(), rn, hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rroot_d, RL.root.data(), 4 * nt, hipMemcpyHostToDevice, st)) ||
-            (e = hipMemcpyAsync(F->rdepth_d, RL.depth.data(), 4 * nt, hipMemcpyHostToDevice, st)) ||
-            (!RL.thr.empty() &&
-             (e = hipMemcpyAsync(F->rthr_d, RL.thr.data(), 4 * RL.thr.size(), hipMemcpyHostToDevice, st))))
-            return fail(e, "hipMemcpyAsync");
-    }
     if (d->scaler_mean) {
         if ((e = hipMalloc(&F->mean_d, sizeof(double) * d->n_features))) return fail(e, "hipMalloc");
         if ((e = hipMemcpyAsync(F->mean_d, d->scaler_mean, sizeof(double) * d->n_features,
@@ -2145,7 +2224,7 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
-    if (rank_mode(F) && F->rank_v2) {
+    if (rank_mode(F) && kVariants[F->variant].p16 == 2) {
         hipLaunchKernelGGL(k_prepare_v2, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride, F->n_features,
                            F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
         FDX_LAUNCHED("k_prepare_v2");
@@ -2225,6 +2304,8 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                     case 43: FDX_LAUNCH_RANK(1024, 1, 6, false, 6); break;
                     case 44: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                     case 45: FDX_LAUNCH_RANK(1024, 1, 4, 2, 2); break;
+                    case 46: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
+                    case 47: FDX_LAUNCH_RANK(1024, 1, 8, 3, 2); break;
                     default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK
@@ -2335,7 +2416,8 @@ extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_wi
                                            const int32_t *term_nb_d, const double *term_risk_d, void *ws,
                                            size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
+    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+                "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
                 3 + 4 * n_windows);
@@ -2363,7 +2445,8 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
                                         int32_t n_windows, int32_t col0, void *ws, size_t ws_bytes,
                                         void *stream) {
     FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
+    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+                "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(col0 >= 0 && col0 + 2 * n_windows <= F->n_features, "columns out of range");
     if (n == 0) return FDX_OK;
@@ -2393,7 +2476,8 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                                           const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                           const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(!(F->rank_v2 && rank_mode(F)), "the fused scoring rows need rank layout v1 (this forest: v2)");
+    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+                "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(flags_mode == FDX_FLAGS_NOTEBOOK || flags_mode == FDX_FLAGS_SPARK, "bad flags mode");
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,

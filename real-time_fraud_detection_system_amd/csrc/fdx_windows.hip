@@ -214,23 +214,43 @@ __global__ void __launch_bounds__(256) k_interleave(
         const int64_t s = si < n_seg ? sorder[si] : -1;
         const int64_t b = s >= 0 ? seg_off[s] : 0;
         const int64_t L = s >= 0 ? seg_off[s + 1] - b : 0;
-        for (int64_t t = tt; t < Lg; t += rows_per_iter) {
-            const int64_t slot = base + t * S + l;
-            if (t < L) {
-                const int32_t r = cperm[b + t];
-                its[slot] = ts[GROUPED ? b + t : r];
-                iamt[slot] = amount[GROUPED ? b + t : r];
-                irow[slot] = r;
-            } else {
-                its[slot] = 0;
-                iamt[slot] = 0.0;
-                irow[slot] = -1;
+        // 4 rows per trip, every load issued before the first store (the loop is memory-latency
+        // bound: one dependent load -> store round trip per row otherwise)
+        constexpr int U = 4;
+        for (int64_t t0 = tt; t0 < Lg; t0 += U * rows_per_iter) {
+            int64_t vts[U];
+            double vam[U];
+            int32_t vr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t t = t0 + (int64_t)u * rows_per_iter;
+                vr[u] = t < L ? cperm[b + t] : -1;
+                if (GROUPED) {
+                    vts[u] = t < L ? ts[b + t] : 0;
+                    vam[u] = t < L ? amount[b + t] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t t = t0 + (int64_t)u * rows_per_iter;
+                if (!GROUPED) {
+                    vts[u] = vr[u] >= 0 ? ts[vr[u]] : 0;
+                    vam[u] = vr[u] >= 0 ? amount[vr[u]] : 0.0;
+                }
+                if (t < Lg) {
+                    const int64_t slot = base + t * S + l;
+                    its[slot] = vts[u];
+                    iamt[slot] = vam[u];
+                    irow[slot] = vr[u];
+                }
             }
         }
     }
     if constexpr (STARTS) {
-        __threadfence_block();
-        __syncthreads();  // the block's slot writes are visible to the block (read back below)
+        if (!GROUPED) {  // the window starts read the timestamps back from the slots just written
+            __threadfence_block();
+            __syncthreads();
+        }
         const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
         int64_t *lts = s_ts[wv];
         for (int ls = wv; ls < S; ls += (int)(blockDim.x / kWave)) {
@@ -238,23 +258,27 @@ __global__ void __launch_bounds__(256) k_interleave(
             if (si >= n_seg) break;
             const int64_t sg = sorder[si];
             const int64_t L = seg_off[sg + 1] - seg_off[sg];
-            const int64_t *gts = its + base + ls;  // row t: gts[t * S]
+            // row t's ts: the grouped input (contiguous) or, gathering form, the slots just written
+            const int64_t *gts = GROUPED ? ts + seg_off[sg] : its + base + ls;
+            const int64_t gstride = GROUPED ? 1 : S;
             const bool in_lds = L <= kStartLds;
             if (in_lds)
-                for (int64_t t = lane; t < L; t += kWave) lts[t] = __builtin_nontemporal_load(gts + t * S);
+                for (int64_t t = lane; t < L; t += kWave) lts[t] = __builtin_nontemporal_load(gts + t * gstride);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int32_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound (starts rise)
             for (int64_t t = lane; t < L; t += kWave) {
-                const int64_t tv = in_lds ? lts[t] : __builtin_nontemporal_load(gts + t * S);
+                const int64_t tv = in_lds ? lts[t] : __builtin_nontemporal_load(gts + t * gstride);
                 for (int w = 0; w < n_win; ++w) {
                     const int64_t bound = tv - win.w[w];
-                    int64_t a = 0, e = t;  // first k in [0, t] with ts_k > bound (k = t qualifies)
+                    int64_t a = prev[w], e = t;  // first k in [prev, t] with ts_k > bound (k = t qualifies)
                     while (a < e) {
                         const int64_t m = (a + e) >> 1;
-                        const int64_t x = in_lds ? lts[m] : __builtin_nontemporal_load(gts + m * S);
+                        const int64_t x = in_lds ? lts[m] : __builtin_nontemporal_load(gts + m * gstride);
                         if (x > bound) e = m; else a = m + 1;
                     }
+                    prev[w] = (int32_t)a;
                     starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = (int32_t)a;
                 }
             }

@@ -9,11 +9,9 @@ run() {  # run <name> <env assignments...>
         > gpurun_out/${TAG}_ab_${name}.json 2>> gpurun_out/${TAG}_ab.err
     python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_ab_${name}.json')); print('${name}', d['ms_per_step'], [(r['stage'], r['ms']) for r in d['kernels']['per_stage']])"
 }
-run base FDX_OVERLAP=1
-run serial FDX_OVERLAP=0
-run serial_r1 FDX_OVERLAP=0 FDX_CUSTOMER_PAYLOAD=0 FDX_TERMINAL_PAYLOAD=0
-run serial_custr1 FDX_OVERLAP=0 FDX_CUSTOMER_PAYLOAD=0
-run overlap_custr1 FDX_CUSTOMER_PAYLOAD=0
-run overlap_r1 FDX_CUSTOMER_PAYLOAD=0 FDX_TERMINAL_PAYLOAD=0
-run nosplit FDX_CUSTOMER_WALK_SPLIT=0
+for spec in ${AB_RUNS:-base:FDX_OVERLAP=1}; do
+    name=${spec%%:*}
+    IFS=, read -ra kv <<< "${spec#*:}"
+    run "$name" "${kv[@]}"
+done
 echo ab done
