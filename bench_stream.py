@@ -9,7 +9,8 @@ micro-batches of --batch transactions (global) and each is timed end to end:
   host batch (pinned) -> HBM -> fdx_stream_update (2 launches) -> forest -> proba -> host.
 Also reported: the device-only time of the update + scoring (HIP events) and the rate.
 
-N GPUs (torch.distributed.run, one process per GPU): customers sharded by contiguous id
+N GPUs, one process per GPU (torch.distributed.run, or `--gpus N` alone: the script starts
+the N ranks itself, bench.spawn_ranks): customers sharded by contiguous id
 range, each micro-batch split by customer owner, terminals owned by id % N, one RCCL
 all-to-all there and back per batch (fdx.streaming.ShardedStreamScorer); the batch latency
 is the max over ranks.  Rank 0 prints one JSON line.
@@ -43,17 +44,22 @@ def parse():
 
 def main():
     args = parse()
+    from bench import load_model, spawn_ranks
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # one process per GPU, before this one touches the GPU
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    from bench import load_model
     from fdx import ops, synth
     from fdx.streaming import ShardedStreamScorer, StreamScorer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:

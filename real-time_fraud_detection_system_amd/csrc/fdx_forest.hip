@@ -2039,12 +2039,14 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
             return fail(e, "hipDeviceGetAttribute");
         if (ncu > 0) F->n_cu = ncu;
     }
-    // Rank layout choice: v2 nodes when the forest fits them (FDX_RANK_V1=1 forces v1 for A/B);
-    // a v2 forest whose every feature needs one slot keeps v1's row format (slot = feature) and
-    // runs on the compact 32 KiB planes; else v1; else the wide 8-byte layout.
-    static const bool force_v1 = getenv("FDX_RANK_V1") != nullptr;
-    rc = install_rank_layout(F, !force_v1, st);
-    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, force_v1, st);
+    // Rank layout choice: v1 when the forest fits it (measured fastest on MI355X for the bench
+    // model: 8.06 vs 8.68 ms for the compact v2 planes, profiles/r02_v6_ab_*.json); else v2 (more
+    // than 4,096 nodes under one threshold rank or ranks past 12 bits -- the deployed model);
+    // else the wide 8-byte layout.  FDX_RANK_V2=1 tries v2 first (A/B; a v2 forest whose every
+    // feature needs one slot keeps v1's row format and runs on the compact 32 KiB planes).
+    static const bool prefer_v2 = getenv("FDX_RANK_V2") != nullptr;
+    rc = install_rank_layout(F, prefer_v2, st);
+    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, !prefer_v2, st);
     if (rc == FDX_E_UNSUPPORTED) rc = FDX_OK;  // the wide layout serves it
     if (rc) {
         fdx_forest_destroy(F);

@@ -57,6 +57,7 @@ __device__ __forceinline__ double term_risk(int64_t w) {
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t round_up(size_t a, size_t m) { return (a + m - 1) / m * m; }
 
 // Grid for a grid-stride streaming kernel: enough blocks to fill 256 CUs several times,
 // capped so launch overhead and tail stay small (cdna_hip_programming.md Guideline 11).

@@ -648,16 +648,6 @@ constexpr int kTermBlock = 256;
 constexpr int kTermWaves = kTermBlock / kWave;
 constexpr int kTermLdsRows = 1024;  // rows of one segment staged per wave (12 KB)
 
-// number of entries of a[lo, hi) that are <= x (a sorted ascending); returns index
-template <typename P>
-__device__ __forceinline__ int64_t upper_bound(P a, int64_t lo, int64_t hi, int64_t x) {
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (a[mid] <= x) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
@@ -667,18 +657,8 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     return v;
 }
 
-// One wave per segment (grid-stride over segments).  Closed form of the reference's
-// rolling(delay+w) - rolling(delay) (bitwise-identical, tie-order independent because
-// every counted row is strictly older than the current one):
-//   hi   = #rows with t <= t_i - delay,  lo_w = #rows with t <= t_i - delay - w
-//   NB_w = hi - lo_w,  FRAUD_w = F[hi] - F[lo_w]  (F = prefix count of fraud rows)
-//   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
-// Segments up to kTermLdsRows rows are staged in LDS (timestamps + prefix counts) with
-// coalesced loads; longer ones are searched in global memory (L2) instead.
 // Output either column-major (nb_out/risk_out [W][n], grouped order) or, when rec_out !=
 // nullptr, one count record per row (W words NB | FRAUD << 32, see fdx.h) at rec_out[row].
-// With `rows` (the re-key perm), grouped position q reads ts/fraud of input row rows[q] and
-// its record goes to rec_out[rows[q]]: the gather and the scatter are fused into this kernel.
 __device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, int64_t *rec_out, int64_t n,
                                            int32_t n_win, int64_t q, int64_t row, int w, int32_t cnt,
                                            int32_t fr) {
@@ -690,199 +670,11 @@ __device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, in
     }
 }
 
-// timestamps of a segment read through the perm (global fallback for long segments)
-struct SegTs {
-    const int64_t *ts;
-    const int32_t *rows;
-    int64_t b;
-    __device__ __forceinline__ int64_t operator[](int64_t j) const { return rows ? ts[rows[b + j]] : ts[b + j]; }
-};
-
-__device__ __forceinline__ int64_t upper_bound_seg(const SegTs &a, int64_t lo, int64_t hi, int64_t x) {
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] <= x) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// RUNS: segments need not be in time order -- the multi-GPU owner side, where a terminal's
-// rows arrive as one time-sorted run per source rank.  The runs are found in the staged
-// segment (a run starts wherever ts descends) and every count of the closed form is summed
-// over the runs, each searched separately (a run is sorted; the prefix fraud counts of the
-// staged order serve each run): still exact and tie-order independent, no sort, records
-// written in place.  More than kMaxRuns runs, or segments longer than the LDS stage, are
-// counted directly (O(L^2), correct for any order).
+// Run starts (RUNS: wherever ts descends) kept per wave: kMaxRuns in s_runs for segments
+// staged in LDS; a long segment does not use the LDS stage, so its run list takes the stage's
+// timestamp words instead (kMaxRunsLong entries).
 constexpr int kMaxRuns = 64;
-template <bool RUNS>
-__global__ void __launch_bounds__(kTermBlock) k_terminal(
-    const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud, const int32_t *__restrict__ rows,
-    const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win,
-    int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
-    const int32_t *__restrict__ dest) {
-    __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
-    __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
-    __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
-    const int64_t nwaves = (int64_t)gridDim.x * kTermWaves;
-    int64_t *lts = s_ts[wv];
-    int32_t *lf = s_f[wv];
-
-    auto dest_of = [&](int64_t r) -> int64_t { return dest ? (int64_t)dest[r] : r; };
-    for (int64_t seg = gwave; seg < n_seg; seg += nwaves) {
-        const int64_t b = seg_off[seg], e = seg_off[seg + 1];
-        const int64_t L = e - b;
-        if (L <= 0) continue;
-        int nruns = 1;
-        if (L <= kTermLdsRows) {
-            int carry = 0;
-            if (lane == 0) lf[0] = 0;
-            if constexpr (RUNS) {
-                // stage + prefix (staging order), then the run starts: descents of ts
-                for (int64_t c = 0; c < L; c += kWave) {
-                    const int64_t j = c + lane;
-                    int f = 0;
-                    if (j < L) {
-                        const int64_t src = rows ? rows[b + j] : b + j;
-                        lts[j] = ts[src];
-                        f = fraud[src] != 0;
-                    }
-                    int inc = wave_incl_scan(f, lane) + carry;
-                    if (j < L) lf[j + 1] = inc;
-                    carry = __shfl(inc, kWave - 1, kWave);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                int32_t *lr = s_runs[wv];
-                int nr = 1;
-                if (lane == 0) lr[0] = 0;
-                for (int64_t c = 0; c < L; c += kWave) {
-                    const int64_t j = c + lane;
-                    const bool d = j > 0 && j < L && lts[j] < lts[j - 1];
-                    const uint64_t m = __ballot(d);
-                    const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
-                    if (d && at < kMaxRuns) lr[at] = (int32_t)j;
-                    nr += __popcll(m);
-                }
-                if (lane == 0 && nr <= kMaxRuns) lr[nr] = (int32_t)L;
-                nruns = nr;
-            } else {
-                for (int64_t c = 0; c < L; c += kWave) {
-                    const int64_t j = c + lane;
-                    int f = 0;
-                    if (j < L) {
-                        const int64_t src = rows ? rows[b + j] : b + j;
-                        lts[j] = ts[src];
-                        f = fraud[src] != 0;
-                    }
-                    int inc = wave_incl_scan(f, lane) + carry;
-                    if (j < L) lf[j + 1] = inc;
-                    carry = __shfl(inc, kWave - 1, kWave);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (RUNS && nruns > 1) {
-                const int32_t *lr = s_runs[RUNS ? wv : 0];
-                if (nruns <= kMaxRuns) {
-                    for (int64_t i = lane; i < L; i += kWave) {
-                        const int64_t t = lts[i];
-                        const int64_t row = dest_of(rows ? rows[b + i] : b + i);
-                        int32_t nbh = 0, frh = 0;
-                        for (int r = 0; r < nruns; ++r) {
-                            const int64_t h = upper_bound(lts, lr[r], lr[r + 1], t - delay);
-                            nbh += (int32_t)(h - lr[r]);
-                            frh += lf[h] - lf[lr[r]];
-                        }
-                        for (int w = 0; w < n_win; ++w) {
-                            int32_t nbl = 0, frl = 0;
-                            for (int r = 0; r < nruns; ++r) {
-                                const int64_t lo = upper_bound(lts, lr[r], lr[r + 1], t - delay - win.w[w]);
-                                nbl += (int32_t)(lo - lr[r]);
-                                frl += lf[lo] - lf[lr[r]];
-                            }
-                            term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl, frh - frl);
-                        }
-                    }
-                } else {
-                    for (int64_t i = lane; i < L; i += kWave) {  // too many runs: direct counts
-                        const int64_t t = lts[i];
-                        const int64_t row = dest_of(rows ? rows[b + i] : b + i);
-                        int32_t nbh = 0, frh = 0, nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
-                        for (int64_t j = 0; j < L; ++j) {
-                            const int64_t tj = lts[j];
-                            if (tj > t - delay) continue;
-                            const int fj = lf[j + 1] - lf[j];
-                            ++nbh;
-                            frh += fj;
-                            for (int w = 0; w < n_win; ++w)
-                                if (tj <= t - delay - win.w[w]) {
-                                    ++nbl[w];
-                                    frl[w] += fj;
-                                }
-                        }
-                        for (int w = 0; w < n_win; ++w)
-                            term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl[w], frh - frl[w]);
-                    }
-                }
-            } else {
-                for (int64_t i = lane; i < L; i += kWave) {
-                    const int64_t t = lts[i];
-                    const int64_t hi = upper_bound(lts, 0, i, t - delay);
-                    const int32_t fhi = lf[hi];
-                    const int64_t row = dest_of(rows ? rows[b + i] : b + i);  // coalesced re-read
-                    for (int w = 0; w < n_win; ++w) {
-                        const int64_t lo = upper_bound(lts, 0, hi, t - delay - win.w[w]);
-                        term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo),
-                                   fhi - lf[lo]);
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else if (RUNS) {  // long unsorted segment: direct counts over the segment
-            const SegTs gts{ts, rows, b};
-            for (int64_t i = lane; i < L; i += kWave) {
-                const int64_t t = gts[i];
-                const int64_t row = dest_of(rows ? rows[b + i] : b + i);
-                int32_t nb_hi = 0, fr_hi = 0, nb_lo[FDX_MAX_WINDOWS] = {}, fr_lo[FDX_MAX_WINDOWS] = {};
-                for (int64_t j = 0; j < L; ++j) {
-                    const int64_t tj = gts[j];
-                    if (tj > t - delay) continue;
-                    const int fj = fraud[rows ? rows[b + j] : b + j] != 0;
-                    ++nb_hi;
-                    fr_hi += fj;
-                    for (int w = 0; w < n_win; ++w)
-                        if (tj <= t - delay - win.w[w]) {
-                            ++nb_lo[w];
-                            fr_lo[w] += fj;
-                        }
-                }
-                for (int w = 0; w < n_win; ++w)
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nb_hi - nb_lo[w], fr_hi - fr_lo[w]);
-            }
-        } else {
-            const SegTs gts{ts, rows, b};
-            for (int64_t i = lane; i < L; i += kWave) {
-                const int64_t t = gts[i];
-                const int64_t hi = upper_bound_seg(gts, 0, i, t - delay);
-                const int64_t row = dest_of(rows ? rows[b + i] : b + i);
-                for (int w = 0; w < n_win; ++w) {
-                    const int64_t lo = upper_bound_seg(gts, 0, hi, t - delay - win.w[w]);
-                    int32_t fr = 0;
-                    for (int64_t j = lo; j < hi; ++j) fr += fraud[rows ? rows[b + j] : b + j] != 0;
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), fr);
-                }
-            }
-        }
-    }
-}
+constexpr int kMaxRunsLong = 2 * kTermLdsRows - 1;
 
 // Terminal windows over GROUPED inputs (fdx_rekey_payload carried ts -- and the fraud bit in
 // bit 31 of the perm -- through the re-key): every read is sequential within a segment.
@@ -891,11 +683,20 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal(
 //   fraud(q)  gfraud ? gfraud[q] : rows[q] >> 31
 //   rows[q]   destination row of q's record (bits 30..0; NULL: q itself)
 // Output: count records rec_out[row] (W words NB | FRAUD << 32), or nb_out/risk_out[w*n + q].
-// Segments of <= kTermLdsRows rows are staged in LDS (closed form of k_terminal).  Longer
-// ones -- a hot terminal, or one terminal's rows from every rank on its owner -- use global
-// memory: the segment's wave first writes the inclusive prefix fraud count of every position
-// to scratch[q], then each row binary-searches its window bounds in gts (per run) and reads
-// two prefix counts: O(L log L) per segment (round 1 counted them directly, O(L^2)).
+// One wave per segment (grid-stride over segments).  Closed form of the reference's
+// rolling(delay+w) - rolling(delay) (bitwise-identical, tie-order independent because every
+// counted row is strictly older than the current one):
+//   hi   = #rows with t <= t_i - delay,  lo_w = #rows with t <= t_i - delay - w
+//   NB_w = hi - lo_w,  FRAUD_w = F[hi] - F[lo_w]  (F = prefix count of fraud rows)
+//   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
+// RUNS: every count is summed over the segment's time-sorted runs, each searched separately.
+// Segments of <= kTermLdsRows rows are staged in LDS.  Longer ones -- a hot terminal, or one
+// terminal's rows from every rank on its owner -- use global memory: the segment's wave
+// first writes the inclusive prefix fraud count of every position to scratch[q], then each
+// row binary-searches its window bounds in gts (per run) and reads two prefix counts:
+// O(L log L) per segment.  Only a segment of more unsorted runs than its run list holds
+// (> 64 in LDS, > 2047 long -- never the owner side, which has one run per source rank)
+// is counted directly, O(L) per row.
 template <bool RUNS>
 __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
@@ -911,7 +712,6 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t nwaves = (int64_t)gridDim.x * kTermWaves;
     int64_t *lts = s_ts[wv];
     int32_t *lf = s_f[wv];
-    int32_t *lr = s_runs[RUNS ? wv : 0];
     auto fraud_of = [&](int64_t q) -> int { return gfraud ? (gfraud[q] != 0) : (int)((uint32_t)rows[q] >> 31); };
     auto dest_of = [&](int64_t q) -> int64_t { return rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q; };
     auto wave_sync = [] {
@@ -958,6 +758,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
             return lo;
         };
         int nruns = 1;
+        int32_t *lr = in_lds ? s_runs[RUNS ? wv : 0] : reinterpret_cast<int32_t *>(lts);
+        const int max_runs = in_lds ? kMaxRuns : kMaxRunsLong;
         if (RUNS) {  // run starts: wherever ts descends
             if (lane == 0) lr[0] = 0;
             int nr = 1;
@@ -966,10 +768,10 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                 const bool dsc = j > 0 && j < L && T(j) < T(j - 1);
                 const uint64_t m = __ballot(dsc);
                 const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
-                if (dsc && at < kMaxRuns) lr[at] = (int32_t)j;
+                if (dsc && at < max_runs) lr[at] = (int32_t)j;
                 nr += __popcll(m);
             }
-            if (lane == 0 && nr <= kMaxRuns) lr[nr] = (int32_t)L;
+            if (lane == 0 && nr <= max_runs) lr[nr] = (int32_t)L;
             nruns = nr;
             wave_sync();
         }
@@ -985,7 +787,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                     const int64_t lo = ub(0, hi, t - delay - win.w[w]);
                     term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), frh - F(lo));
                 }
-            } else if (nruns <= kMaxRuns) {
+            } else if (nruns <= max_runs) {
                 for (int r = 0; r < nruns; ++r) {
                     const int64_t h = ub(lr[r], lr[r + 1], t - delay);
                     nbh += (int32_t)(h - lr[r]);
@@ -1000,7 +802,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                     }
                     term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl, frh - frl);
                 }
-            } else {  // more than kMaxRuns unsorted runs: count directly (correct for any order)
+            } else {  // more unsorted runs than the run list holds: count directly (any order)
                 int32_t nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
                 for (int64_t j = 0; j < L; ++j) {
                     const int64_t tj = T(j);
@@ -1104,6 +906,62 @@ extern "C" int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount
     return FDX_OK;
 }
 
+// The input-order entry points (round 1's interface: ts / fraud in input order, segments
+// through the re-key perm) run the grouped kernel: a gather puts ts / fraud / destination in
+// grouped order first (stream-ordered temporaries), so every terminal kernel is k_terminal_g.
+__global__ void k_term_gather(const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud,
+                              const int32_t *__restrict__ rows, const int32_t *__restrict__ dest, int64_t n,
+                              int64_t *__restrict__ gts, uint8_t *__restrict__ gfr, int32_t *__restrict__ grow) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t src = rows ? rows[q] : q;
+        gts[q] = ts[src];
+        gfr[q] = fraud[src];
+        grow[q] = dest ? dest[src] : (int32_t)src;
+    }
+}
+
+static int terminal_input_order(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
+                                const int32_t *dest_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                int64_t delay_ns, const WinArgs &wa, int32_t n_windows, bool runs, int32_t *nb_d,
+                                double *risk_d, int64_t *rec_d, hipStream_t st) {
+    const bool gather = row_d || dest_d;
+    const size_t b_ts = gather ? round_up((size_t)n * 8, 256) : 0;
+    const size_t b_fr = gather ? round_up((size_t)n, 256) : 0;
+    const size_t b_row = gather ? round_up((size_t)n * 4, 256) : 0;
+    const size_t bytes = b_ts + b_fr + b_row + round_up((size_t)n * 4, 256);
+    char *tmp = nullptr;
+    hipError_t e = hipMallocAsync((void **)&tmp, bytes, st);
+    if (e != hipSuccess) {
+        set_error("hipMallocAsync(%zu) failed: %s", bytes, hipGetErrorString(e));
+        return FDX_E_HIP;
+    }
+    const int64_t *gts = ts_ns_d;
+    const uint8_t *gfr = fraud_d;
+    const int32_t *grow = nullptr;
+    if (gather) {
+        hipLaunchKernelGGL(k_term_gather, dim3(stream_grid(n, 256)), dim3(256), 0, st, ts_ns_d, fraud_d, row_d,
+                           dest_d, n, (int64_t *)tmp, (uint8_t *)(tmp + b_ts), (int32_t *)(tmp + b_ts + b_fr));
+        gts = (const int64_t *)tmp;
+        gfr = (const uint8_t *)(tmp + b_ts);
+        grow = (const int32_t *)(tmp + b_ts + b_fr);
+    }
+    int32_t *scratch = (int32_t *)(tmp + b_ts + b_fr + b_row);
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
+    if (runs)
+        hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
+                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch);
+    else
+        hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
+                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch);
+    e = hipGetLastError();
+    (void)hipFreeAsync(tmp, st);
+    if (e != hipSuccess) {
+        set_error("k_terminal_g launch failed: %s", hipGetErrorString(e));
+        return FDX_E_HIP;
+    }
+    return FDX_OK;
+}
+
 extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d,
                                     const int64_t *seg_off_d, int64_t n_seg, int64_t n,
                                     int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
@@ -1115,12 +973,8 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
     if (n_seg == 0 || n == 0) return FDX_OK;
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
-    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d,
-                       fraud_d, (const int32_t *)nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d,
-                       risk_d, (int64_t *)nullptr, (const int32_t *)nullptr);
-    FDX_LAUNCHED("k_terminal");
-    return FDX_OK;
+    return terminal_input_order(ts_ns_d, fraud_d, nullptr, nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows,
+                                false, nb_d, risk_d, nullptr, as_stream(stream));
 }
 
 static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
@@ -1134,17 +988,8 @@ static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const
     FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
     if (n_seg == 0 || n == 0) return FDX_OK;
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && rec_d, "null pointer");
-    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    if (sort)
-        hipLaunchKernelGGL(k_terminal<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
-                           row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
-                           rec_d, dest_d);
-    else
-        hipLaunchKernelGGL(k_terminal<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), ts_ns_d, fraud_d,
-                           row_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, (int32_t *)nullptr, (double *)nullptr,
-                           rec_d, dest_d);
-    FDX_LAUNCHED("k_terminal");
-    return FDX_OK;
+    return terminal_input_order(ts_ns_d, fraud_d, row_d, dest_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, sort,
+                                nullptr, nullptr, rec_d, as_stream(stream));
 }
 
 extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,

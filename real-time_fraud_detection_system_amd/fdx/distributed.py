@@ -6,11 +6,12 @@ the flags and the customer windows need no communication.  The terminal windows 
 rows of a terminal on one rank: owner(t) = t % world.  Per step
 
   owner keys -> stable re-key by owner -> pack {ts, term|fraud|row} (16 B/row)
-  -> all_to_all_single (splits exchanged first, 8 B per peer)
+  -> row exchange (splits exchanged first by all_to_all_single, 8 B per peer; the rows by
+     batched point-to-point chunks, alltoallv)
   -> owner: unpack, re-key by local terminal id (segments = per-rank time-sorted runs,
      sorted inside the records kernel), terminal windows as count records (W words/row:
      NB | FRAUD << 32) written straight to receive positions
-  -> all_to_all_single back (splits mirrored) -> scatter into the local feature matrix
+  -> the same exchange back (splits mirrored) -> scatter into the local feature matrix
   -> scale + forest locally.
 
 Ring collectives are the wrong primitive on xGMI's point-to-point links; the all-to-all
@@ -79,6 +80,46 @@ class GpuKernels:
                                              X.stride(0), col0, ops._s()), "fdx_reply_assemble")
 
 
+# Largest message of one point-to-point transfer.  RCCL 2.26 (the torch-ROCm wheel's) copies
+# only the first half of an all_to_all_single message above 1 GiB (measured on MI355X, world
+# 1: every size from 1.1 to 3 GB loses exactly its second half; <= 1 GiB and chunked calls are
+# exact -- DESIGN.md §5), and a config-4 rank's exchange is 1.4 GB.  So the row exchange is
+# written as batched isend/irecv in chunks of at most this many bytes: both ends of a pair
+# derive the same chunking from the same count, so no rank needs another's sizes.
+P2P_CHUNK_BYTES = 256 << 20
+
+
+def alltoallv(out, inp, out_splits, in_splits, group=None):
+    """all_to_all_single(out, inp, out_splits, in_splits) over rows of 2-D tensors: this
+    rank's own block is a device copy, every other peer's block goes as point-to-point
+    chunks of <= P2P_CHUNK_BYTES (one batched group call)."""
+    world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    row_bytes = max(inp[:1].numel() * inp.element_size(), out[:1].numel() * out.element_size(), 1)
+    chunk = max(P2P_CHUNK_BYTES // row_bytes, 1)
+    io = [0]
+    for c in in_splits:
+        io.append(io[-1] + int(c))
+    oo = [0]
+    for c in out_splits:
+        oo.append(oo[-1] + int(c))
+    ops = []
+    for p in range(world):
+        if p == me:
+            if io[p + 1] > io[p]:
+                out[oo[p]:oo[p + 1]].copy_(inp[io[p]:io[p + 1]])
+            continue
+        peer = p if group is None else dist.get_global_rank(group, p)
+        for a in range(io[p], io[p + 1], chunk):
+            ops.append(dist.P2POp(dist.isend, inp[a:min(a + chunk, io[p + 1])], peer, group))
+        for a in range(oo[p], oo[p + 1], chunk):
+            ops.append(dist.P2POp(dist.irecv, out[a:min(a + chunk, oo[p + 1])], peer, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out
+
+
 def exchange_begin(K, term, world, group=None):
     """Phase 1 (enqueue only, no host sync): owner keys, re-key by owner, split exchange."""
     owner = K.owner_keys(term, world)
@@ -99,19 +140,19 @@ def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows
     sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
     rec = K.exchange_pack(ts, term, fraud, send_perm)
     recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
-    dist.all_to_all_single(recv, rec, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    alltoallv(recv, rec, rc, sc, group)
     rts, rterm, rfr = K.exchange_unpack(recv, world)
     if records is not None:
         reply = records(rts, rterm, rfr)
         back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
-        dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
+        alltoallv(back, reply, sc, rc, group)
         return back, send_perm
     n_local_terms = (n_terminals_total + world - 1) // world
     # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
     # the records kernel handles such segments itself (no global time sort of the receive buffer)
     reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days)  # by receive index
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
-    dist.all_to_all_single(back, reply, output_split_sizes=sc, input_split_sizes=rc, group=group)
+    alltoallv(back, reply, sc, rc, group)
     return back, send_perm
 
 

@@ -93,10 +93,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, shards, n_terms, q):
+def _worker(rank, world, port, shards, n_terms, q, chunk_bytes=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fdx import distributed
     from fdx.distributed import exchange_terminal_features
+
+    if chunk_bytes is not None:  # many point-to-point chunks per peer
+        distributed.P2P_CHUNK_BYTES = chunk_bytes
 
     d = shards[rank]
     back, send_perm = exchange_terminal_features(
@@ -111,8 +115,8 @@ def _worker(rank, world, port, shards, n_terms, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_terminal_exchange_matches_single_process(world):
+@pytest.mark.parametrize("world,chunk_bytes", [(2, None), (3, None), (3, 16 * 37)])
+def test_terminal_exchange_matches_single_process(world, chunk_bytes):
     from fdx import synth
 
     n_terms = 150
@@ -121,7 +125,8 @@ def test_terminal_exchange_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, n_terms, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, n_terms, q, chunk_bytes))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -197,3 +197,56 @@ def test_deployed_model_rank_layout_v2(dev):
     Xd = T(X, torch.float64, dev)[T(idx, torch.int64, dev)]
     got = forest.predict(Xd, ws=ops.workspace(forest.workspace_size(len(idx)), dev)).cpu().numpy()
     np.testing.assert_array_equal(got, z["test_proba1"][idx])
+
+
+def test_config4_one_rank_shard(dev):
+    """configs[3] (1M customers / 2M terminals / 365 days, 8 GPUs) as ONE rank sees it: rank
+    3 of 8 owns customers [375000, 500000) and all their rows (~90M tx; the terminal ids range
+    over all 2M).  The sharded path (world 1 process group: its re-key exchange, owner-side
+    records and reply assembly run through RCCL to self) must give the probabilities of the
+    single-GPU fused path on the re-based ids on every row, and the sampled customers' and
+    terminals' features must equal the C oracle's."""
+    import socket
+
+    import torch.distributed as dist
+
+    from fdx.distributed import ShardedPipeline
+
+    base, n_c, n_t = 375_000, 125_000, 2_000_000
+    arrays, z = _model()
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    g = synth.generate_device(n_c, n_t, 365, seed=77, customer_offset=base, device=dev)
+    n = g["ts"].numel()
+    assert n > 60_000_000
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
+    pipe = FraudPipeline(forest=forest)
+    ws = ops.workspace(forest.workspace_size(n * 11 // 10), dev)
+    p_single = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(args[0], args[1] - base, *args[2:], n_c, n_t, p_single, ws)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        sp = ShardedPipeline(pipe, world=1, rank=0, n_terminals_total=n_t, customer_base=base, n_customers_local=n_c)
+        p_shard = torch.zeros(n, dtype=torch.float64, device=dev)
+        sp.run(*args, p_shard, ws)
+        assert torch.equal(p_shard, p_single)
+        X = sp.featurize(*args)
+    finally:
+        dist.destroy_process_group()
+    d = {k: v.cpu().numpy() for k, v in g.items() if k in ("ts", "customer", "terminal", "amount", "fraud")}
+    rng = np.random.default_rng(5)
+    cust = rng.choice(n_c, 64, replace=False) + base
+    term = rng.choice(n_t, 256, replace=False)
+    for keys, col, cols, c0 in ((cust, "customer", CUST_COLS, 3), (term, "terminal", TERM_COLS, 9)):
+        m = np.isin(d[col], keys)
+        assert m.sum() > 1000
+        f = oracle.featurize_arrays(d["ts"][m], d["customer"][m], d["terminal"][m], d["amount"][m], d["fraud"][m])
+        rows = torch.from_numpy(np.flatnonzero(m)).to(dev)
+        got = X[rows].cpu().numpy()
+        for j, c in enumerate(cols):
+            np.testing.assert_array_equal(got[:, c0 + j], f[c], err_msg=c)
+        np.testing.assert_array_equal(p_single[rows].cpu().numpy(),
+                                      oracle.forest_predict(got, arrays, z["mean"], z["scale"]))

@@ -97,3 +97,39 @@ def test_terminal_records_unsorted_runs(dev, parts):
     got = ops.terminal_windows_packed_unsorted(rts, rfr, gseg, rows=gperm).cpu().numpy()  # by receive index
     np.testing.assert_array_equal(got, ref[order])
     assert n > 0
+
+
+@pytest.mark.parametrize("parts", [8, 100, 2500])
+def test_terminal_records_hot_terminals_long_segments(dev, parts):
+    """Segments far longer than the LDS stage (8 terminals, ~9k rows each): the global-memory
+    path of k_terminal_g -- prefix fraud counts in scratch, binary searches per run -- for 8
+    and 100 runs, and the direct count past the long run list (2,500 runs > 2,047).  The
+    records must equal the time-sorted input's row by row, and the oracle's on one terminal."""
+    import oracle
+
+    d = synth.generate(n_customers=2500, n_terminals=8, nb_days=15, r=200, seed=21)
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    n = len(d["ts"])
+    assert np.bincount(d["terminal"]).max() > 4 * 1024
+    ts, term, fr = T(d["ts"], torch.int64), T(d["terminal"], torch.int32), T(d["fraud"], torch.uint8)
+    tperm, tseg, _ = ops.rekey(term, 8)
+    ref = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()   # by input row
+    m = d["terminal"] == 3
+    f = oracle.featurize_arrays(d["ts"][m], d["customer"][m], d["terminal"][m], d["amount"][m], d["fraud"][m])
+    w = ref[m]
+    for j, win in enumerate((1, 7, 30)):
+        nb, frc = (w[:, j] & 0xFFFFFFFF).astype(np.int64), w[:, j] >> 32
+        np.testing.assert_array_equal(nb, f[f"TERMINAL_ID_NB_TX_{win}DAY_WINDOW"])
+        risk = np.where(nb > 0, frc / np.maximum(nb, 1), 0.0)
+        np.testing.assert_array_equal(risk, f[f"TERMINAL_ID_RISK_{win}DAY_WINDOW"])
+    order = np.argsort(d["customer"] % parts, kind="stable")
+    rts, rterm, rfr = T(d["ts"][order], torch.int64), T(d["terminal"][order], torch.int32), \
+        T(d["fraud"][order], torch.uint8)
+    gperm, gseg, _ = ops.rekey(rterm, 8)
+    got = ops.terminal_windows_packed_unsorted(rts, rfr, gseg, rows=gperm).cpu().numpy()  # by receive index
+    np.testing.assert_array_equal(got, ref[order])
+    # the owner side's own path: payload re-key (fraud in bit 31 of the perm), grouped runs
+    perm, seg, gts, _ = ops.rekey_payload(rterm, 8, rts, flag=rfr)
+    got = ops.terminal_windows_grouped(gts, seg, rows=perm, runs=True).cpu().numpy()
+    np.testing.assert_array_equal(got, ref[order])
+    assert n > 0
