@@ -5,7 +5,8 @@ A step = one pass of the hot path over one batch already resident in HBM:
   terminal delayed-risk windows -> time flags + assemble the 15 input_features +
   StandardScaler -> RandomForest(100 trees, depth 20) predict_proba.
 Workload per GPU (BASELINE.json configs[1]): 50k customers / 100k terminals / 183 days
-(~17.7M tx), synthetic data from the handbook distributions (fdx.synth), scored with the
+(~17.7M tx), synthetic data from the handbook distributions generated on the GPU
+(fdx.synth.generate_device; no host generation inside the GPU lease), scored with the
 config-3 model (bench_assets/rf100_d20.npz, trained with sklearn on config-1 features).
 
 N GPUs: one process per GPU.  Launched by torch.distributed.run (RANK / WORLD_SIZE set) or,
@@ -99,6 +100,8 @@ def parse():
                     help="rows of the sklearn predict_proba sample in the CPU baseline")
     ap.add_argument("--forest-variant", type=int, default=-1,
                     help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
+    ap.add_argument("--isolated-steps", type=int, default=3,
+                    help="extra untimed steps with every stage on one stream: per-kernel times for the roofline table")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
@@ -276,9 +279,14 @@ def main():
     # weak scaling: rank r owns customers [r * C, (r + 1) * C) and adds its own terminals to
     # one shared terminal map
     base = rank * args.customers
-    data = synth.generate(args.customers, args.terminals * world, args.days, seed=1234 + rank,
-                          customer_offset=base)
-    n_local = len(data["ts"])
+    t_gen = time.perf_counter()
+    # generated on the GPU (HIP Philox generator, csrc/fdx_synth.hip): the handbook
+    # distributions of fdx.synth.generate, pinned by tests/test_gpu_synth.py; inputs resident
+    g = synth.generate_device(args.customers, args.terminals * world, args.days, seed=1234 + rank,
+                              customer_offset=base, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen
+    n_local = g["ts"].numel()
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
     default_variant = forest.variant
@@ -290,8 +298,7 @@ def main():
     if not np.array_equal(got, check_proba):
         raise SystemExit("forest parity check against sklearn failed")
 
-    ts, cust, term = T(data["ts"], torch.int64), T(data["customer"], torch.int32), T(data["terminal"], torch.int32)
-    amt, fr = T(data["amount"], torch.float64), T(data["fraud"], torch.uint8)
+    ts, cust, term, amt, fr = g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"]
     pipe = FraudPipeline(forest=forest)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
@@ -309,7 +316,7 @@ def main():
     else:
         lcust = cust  # rank 0 of a 1-GPU run: base 0
 
-        def step(record):
+        def step(record, overlap=None, into=None):
             marks = {}   # stage -> (start event, end event) on the stage's own stream
 
             last = {}
@@ -322,8 +329,11 @@ def main():
                         marks[name] = (last[id(st)], e)
                     last[id(st)] = e
 
-            pipe.run_fused(ts, lcust, term, amt, fr, args.customers, args.terminals, proba, ws, mark=mark)
-            if record:
+            pipe.run_fused(ts, lcust, term, amt, fr, args.customers, args.terminals, proba, ws, mark=mark,
+                           overlap=overlap)
+            if record and into is not None:
+                into.append(marks)
+            elif record:
                 marks_all.append(marks)
                 trav.append(marks["forest_traverse"])
 
@@ -351,6 +361,11 @@ def main():
     else:
         n_total = n_local
 
+    iso_all = []  # per-kernel times: every stage alone on the GPU (after the timed region)
+    if marks_all and args.isolated_steps > 0:
+        for _ in range(args.isolated_steps):
+            step(True, overlap=False, into=iso_all)
+        torch.cuda.synchronize()
     trav_ms = sum(a.elapsed_time(b) for a, b in trav) / max(len(trav), 1)
     launches = forest.n_chunks
     fvar = forest.variant
@@ -381,7 +396,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: handbook-distribution generator (fdx.synth, seed 1234+rank), resident in HBM",
+        "setup_s": {"generate_on_gpu": round(t_gen, 2)},
+        "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234+rank), "
+                "resident in HBM",
         "config": {"workload": f"configs[1]: {args.customers} customers / {args.terminals} terminals / "
                                f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
                    "tx_per_gpu": n_local, "global_tx": n_total,
@@ -408,8 +425,13 @@ def main():
         for name, unit, kernels in STAGES:
             ms = [mk[name][0].elapsed_time(mk[name][1]) for mk in marks_all]
             t_ms = sum(ms) / len(ms)
-            table.append({"stage": name, "unit": unit, "ms": round(t_ms, 4),
-                          "kernels": [k for k, _ in kernels], "pmc_bytes": pmc_bytes(kernels)})
+            row = {"stage": name, "unit": unit, "ms_in_step": round(t_ms, 4)}
+            if iso_all:
+                iso = [mk[name][0].elapsed_time(mk[name][1]) for mk in iso_all]
+                row["ms_isolated"] = round(sum(iso) / len(iso), 4)
+            row["ms"] = row.get("ms_isolated", row["ms_in_step"])
+            row.update({"kernels": [k for k, _ in kernels], "pmc_bytes": pmc_bytes(kernels)})
+            table.append(row)
         # §8(d) units: K1-cust = layout + walk, K3 = assemble + traverse
         units = {}
         for row in table:
@@ -431,18 +453,21 @@ def main():
                           "frac": round(gbs / HBM_PEAK_GBS, 4),
                           "pmc_traffic_bytes": round(u["pmc"]) if u["pmc_ok"] and pmc else None,
                           "traffic_over_alg": round(u["pmc"] / alg, 2) if u["pmc_ok"] and pmc else None})
-        step_ms = sum(r["ms"] for r in table)
+        step_ms = sum(r["ms_in_step"] for r in table)
         e2e = ALG["end-to-end"] * n_local / (dt / args.steps) / 1e9
         out["kernels"] = {"per_stage": table, "per_unit": krows, "stage_sum_ms": round(step_ms, 3),
                           "streams": "rekey_terminal + terminal_windows run on a side stream, concurrently with the "
-                                     "customer stages, so stage_sum_ms exceeds ms_per_step by the overlap",
+                                     "customer stages, so stage_sum_ms (of ms_in_step) exceeds ms_per_step by the "
+                                     "overlap; ms = ms_isolated: the same stages in extra steps with every stage on "
+                                     "one stream (no concurrent kernel), the per-kernel durations the rooflines use",
                           "end_to_end": {"alg_bytes_per_tx": ALG["end-to-end"], "achieved_GBs": round(e2e, 1),
                                          "time": "ms_per_step",
                                          "frac": round(e2e / HBM_PEAK_GBS, 4)},
-                          "note": "ms = HIP events around each stage on its stream, mean over the timed steps; "
+                          "note": "ms_in_step = HIP events around each stage on its stream, mean over the timed steps; "
                                   "alg bytes = SURVEY.md §8(d) per tx x tx; pmc = rocprofv3 FETCH/WRITE per "
                                   "dispatch x dispatches (profiles/pmc_kernels.json)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        data = {k: g[k].cpu().numpy() for k in ("ts", "customer", "terminal", "amount", "fraud")}
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, check_X, check_proba, args.cpu_score_rows)
     if args.sweep_variant and rank == 0 and world == 1 and not args.sharded:
         # each variant: one full untimed pipeline pass (the prepared row format depends on

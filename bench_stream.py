@@ -68,7 +68,12 @@ def main():
     n_c = args.customers // world
     base = rank * n_c
     t_gen = time.perf_counter()
-    d = synth.generate(n_c, args.terminals, args.history_days + 1, seed=4321 + rank, customer_offset=base)
+    # generated on the GPU (csrc/fdx_synth.hip), then copied to host: the micro-batches arrive
+    # from pinned host memory, as CDC batches would
+    g = synth.generate_device(n_c, args.terminals, args.history_days + 1, seed=4321 + rank, customer_offset=base,
+                              device=dev)
+    d = {k: g[k].cpu().numpy() for k in ("ts", "customer", "terminal", "amount", "fraud")}
+    del g
     t_gen = time.perf_counter() - t_gen
     split = synth.START_NS + args.history_days * 86400 * synth.NS
     h = int(np.searchsorted(d["ts"], split))
@@ -176,7 +181,7 @@ def main():
         "warmup": int(n_warm),
         "mean_batch_tx": round(total_rows / max(n_timed, 1), 1),
         "dtype": "f64",
-        "data": "synthetic: handbook-distribution generator (fdx.synth, seed 4321+rank)",
+        "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 4321+rank)",
         "config": {"workload": f"configs[4]: tail of configs[3] ({args.customers} customers / {args.terminals} "
                                f"terminals), {args.history_days} days of history in the state, then day "
                                f"{args.history_days} as micro-batches of {args.batch} tx",

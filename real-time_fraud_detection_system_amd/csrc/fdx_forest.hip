@@ -71,6 +71,7 @@ struct fdx_forest_s {
     // rank layout v2 (32 threshold-rank slots, see build_rank_layout)
     bool rank_v2 = false;
     bool rank_identity = false;  // v2 with slot s = feature s (<= 16 slots): v1 rank rows, compact planes
+    bool rank_pair = false;      // rank layout v3: sibling pairs (P16 = 4, see pair_walk)
     // host copies of the packed forest and scaler (set_variant rebuilds the rank layout in the
     // other node format when a variant needs it)
     std::vector<uint64_t> h_packed;
@@ -787,7 +788,11 @@ constexpr Variant kVariants[] = {
     // 44..: rank layout v2 (32 threshold-rank slots, u16 planes of 1,024 rows; p16 = 2)
     {1024, 1, 6, 0, 1, 2, 2}, {1024, 1, 4, 0, 1, 2, 2},
     // 46..: v2 nodes over 16 slots of 1,024 u16 rows (32 KiB of planes; slot = feature, v1 rows)
-    {1024, 1, 6, 0, 1, 3, 2}, {1024, 1, 8, 0, 1, 3, 2}};
+    {1024, 1, 6, 0, 1, 3, 2}, {1024, 1, 8, 0, 1, 3, 2},
+    // 48..: rank layout v3, sibling pairs (one LDS round trip per step; p16 = 4)
+    // (pipe = SEL of pair_walk: 0 compiler select, 1 v_bfi select, 2 grouped compares)
+    {1024, 1, 6, 0, 1, 4, 0}, {1024, 1, 6, 0, 1, 4, 1}, {1024, 1, 8, 0, 1, 4, 1}, {1024, 1, 6, 0, 1, 4, 2},
+    {1024, 1, 9, 0, 1, 4, 2}, {1024, 1, 4, 0, 1, 4, 1}};
 constexpr int kDefaultRankV2Variant = 44;
 constexpr int kDefaultRankCompactVariant = 46;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -1049,9 +1054,9 @@ __device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
 // offset (rank layout v1); 1 = the same nodes over u16 planes; 2 = rank layout v2: u16 planes
 // of 1,024 rows, a 5-bit SLOT field and an 11-bit right offset (see build_rank_layout).
 template <int P16>
-constexpr uint32_t kSlotMask = P16 >= 2 ? 0xF800u : 0xF000u;
+constexpr uint32_t kSlotMask = (P16 == 2 || P16 == 3) ? 0xF800u : 0xF000u;
 template <int P16>
-constexpr uint32_t kOffMask = P16 >= 2 ? 0x7FFu : 0xFFFu;
+constexpr uint32_t kOffMask = (P16 == 2 || P16 == 3) ? 0x7FFu : 0xFFFu;
 // 3 = the v2 node format over 16 u16 planes of 1,024 rows (32 KiB): forests whose every feature
 // fits one slot (slot = feature, the v1 row format); the node region starts at 32 KiB, so a
 // chunk holds a third more nodes than with 64 KiB of planes (fewer chunk launches per batch)
@@ -1152,6 +1157,165 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
     for (; d < depth; ++d) step();
 }
 
+__device__ __forceinline__ uint2 lds64(const char *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint2 *>(lds + byte_addr);
+}
+
+// Rank layout v3, the PAIR layout (P16 = 4): the two children of a node are adjacent words of
+// an 8-byte aligned pair, so one ds_read_b64 fetches both, issued together with the node's
+// feature-rank read: ONE dependent LDS round trip per step (the v1 step reads the rank, then
+// the next node: two).  Node word: [31:16] k+1 | [15:12] feature | [11:0] offset, in pairs,
+// of its children pair from the pair holding the node.  Row planes hold (r+1) << 16 (NaN:
+// 0xFFFFFFFF), so  r <= k  <=>  plane <= word  (one unsigned compare; the low 16 bits of the
+// word never decide it).  Ranks are capped at 32,766 (at most 32,766 thresholds per feature),
+// so planes and words stay below 2^31.  Leaves have offset 0, so their "children" pair is
+// their own pair, and are fixed points: a left leaf is 0x7FFF0000 (every plane value <=
+// 0x7FFF0000 compares <=, picks the left word = itself), a right leaf 0 (nothing compares
+// <=, picks itself).
+// Chain state: w = node word, q = LDS byte address of the pair holding it.  Step:
+//   c = q + (w & 0xFFF) * 8;  x = plane[(w & 0xF000) | lane];  pr = pair[c]
+//   w = x <= w ? pr.lo : pr.hi;  q = c                       (5 VALU, 1 b32 + 1 b64 read)
+// Software-pipelined: each chain's next two reads are issued right after its select, so
+// every chain of the wave has its reads in flight while the others wait / compute.
+// c = q + (w & 0xFFF) * 8 in 2 VALU (the compiler's form: shift, mask, add)
+__device__ __forceinline__ uint32_t pair_child(uint32_t w, uint32_t q) {
+    uint32_t c;
+    asm("v_and_b32 %0, 0xfff, %1\n\tv_lshl_add_u32 %0, %0, 3, %2" : "=&v"(c) : "v"(w), "v"(q));
+    return c;
+}
+
+// SEL = how a step selects the next word (same result):
+//   0  C: compare + v_cndmask (the compiler puts the gfx950 VCC wait, s_nop 1, between them)
+//   1  asm: d = w - x, m = d >> 31 (arithmetic), w = v_bfi(m, hi, lo) -- no lane mask, no
+//      wait states; needs w, x < 2^31 (v3 caps ranks at 32,766: x <= 0x7FFF0000)
+//   2  asm: chains in groups of 3, the 3 compares (to SGPR pairs) before the 3 selects, so
+//      every v_cndmask is 2 instructions after its compare (K a multiple of 3)
+// Every form then computes the next children-pair address and the rank address (3 VALU).
+template <int K, int SEL>
+__device__ __forceinline__ void pair_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&q)[K],
+                                          uint32_t (&w)[K], int depth) {
+    constexpr int S = (SEL == 2 && K % 3 != 0) ? 1 : SEL;  // tail groups of other widths: the bfi form
+    uint32_t x[K], c[K];
+    uint2 pr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        c[k] = pair_child(w[k], q[k]);
+        pr[k] = lds64(lds, c[k]);
+        x[k] = lds32(lds, (w[k] & 0xF000u) | lane_base[k]);
+    }
+    auto reads = [&](int k, uint32_t xa) {
+        pr[k] = lds64(lds, c[k]);  // pair first: the wait for x (younger) covers both
+        x[k] = lds32(lds, xa);
+    };
+    // one asm block per step of a chain (or of 3 chains): the compiler pads the boundary
+    // between two asm blocks with an s_nop
+    auto step = [&]() {
+        if constexpr (S == 2) {
+#pragma unroll
+            for (int k = 0; k < K; k += 3) {
+                uint64_t m0, m1, m2;
+                uint32_t t0, t1, t2, a0, a1, a2;
+                asm("v_cmp_le_u32_e64 %[m0], %[x0], %[w0]\n\t"
+                    "v_cmp_le_u32_e64 %[m1], %[x1], %[w1]\n\t"
+                    "v_cmp_le_u32_e64 %[m2], %[x2], %[w2]\n\t"
+                    "v_cndmask_b32_e64 %[w0], %[h0], %[l0], %[m0]\n\t"
+                    "v_cndmask_b32_e64 %[w1], %[h1], %[l1], %[m1]\n\t"
+                    "v_cndmask_b32_e64 %[w2], %[h2], %[l2], %[m2]\n\t"
+                    "v_and_b32 %[t0], 0xfff, %[w0]\n\t"
+                    "v_and_b32 %[t1], 0xfff, %[w1]\n\t"
+                    "v_and_b32 %[t2], 0xfff, %[w2]\n\t"
+                    "v_lshl_add_u32 %[c0], %[t0], 3, %[c0]\n\t"
+                    "v_lshl_add_u32 %[c1], %[t1], 3, %[c1]\n\t"
+                    "v_lshl_add_u32 %[c2], %[t2], 3, %[c2]\n\t"
+                    "v_and_or_b32 %[a0], %[w0], %[fm], %[b0]\n\t"
+                    "v_and_or_b32 %[a1], %[w1], %[fm], %[b1]\n\t"
+                    "v_and_or_b32 %[a2], %[w2], %[fm], %[b2]"
+                    : [w0] "+v"(w[k]), [w1] "+v"(w[k + 1]), [w2] "+v"(w[k + 2]), [c0] "+v"(c[k]),
+                      [c1] "+v"(c[k + 1]), [c2] "+v"(c[k + 2]), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+                      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2)
+                    : [x0] "v"(x[k]), [x1] "v"(x[k + 1]), [x2] "v"(x[k + 2]), [h0] "v"(pr[k].y),
+                      [l0] "v"(pr[k].x), [h1] "v"(pr[k + 1].y), [l1] "v"(pr[k + 1].x), [h2] "v"(pr[k + 2].y),
+                      [l2] "v"(pr[k + 2].x), [fm] "s"(0xF000u), [b0] "v"(lane_base[k]), [b1] "v"(lane_base[k + 1]),
+                      [b2] "v"(lane_base[k + 2]));
+                reads(k, a0);
+                reads(k + 1, a1);
+                reads(k + 2, a2);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if constexpr (S == 1) {
+                    uint32_t t, a;
+                    asm("v_sub_u32 %[t], %[w], %[x]\n\t"
+                        "v_ashrrev_i32 %[t], 31, %[t]\n\t"
+                        "v_bfi_b32 %[w], %[t], %[hi], %[lo]\n\t"
+                        "v_and_b32 %[t], 0xfff, %[w]\n\t"
+                        "v_lshl_add_u32 %[c], %[t], 3, %[c]\n\t"
+                        "v_and_or_b32 %[a], %[w], %[fm], %[b]"
+                        : [w] "+v"(w[k]), [c] "+v"(c[k]), [t] "=&v"(t), [a] "=&v"(a)
+                        : [x] "v"(x[k]), [hi] "v"(pr[k].y), [lo] "v"(pr[k].x), [fm] "s"(0xF000u),
+                          [b] "v"(lane_base[k]));
+                    reads(k, a);
+                } else {
+                    w[k] = x[k] <= w[k] ? pr[k].x : pr[k].y;
+                    c[k] = pair_child(w[k], c[k]);
+                    reads(k, (w[k] & 0xF000u) | lane_base[k]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    int d = 0;
+    bool done = false;
+    for (; d + kExitEvery <= depth; d += kExitEvery) {
+#pragma unroll
+        for (int e = 0; e < kExitEvery; ++e) step();
+        uint32_t moving = 0;  // leaves (and only leaves) have offset 0
+#pragma unroll
+        for (int k = 0; k < K; ++k) moving |= w[k] & 0xFFFu;
+        if (!__any(moving != 0)) {
+            done = true;
+            break;
+        }
+    }
+    if (!done)
+        for (; d < depth; ++d) step();
+#pragma unroll
+    for (int k = 0; k < K; ++k) q[k] = c[k];  // every chain at a leaf: its "children" pair is its own
+}
+
+// The pair walk for batches with NaN features: a NaN rank (0xFFFFFFFF) takes the node's
+// missing_go_to_left (mleft by node position; p = byte address of the chain's node), and
+// leaves stay put.  Returns the leaf addresses in p.
+template <int K>
+__device__ __forceinline__ void pair_walk_nan(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&q)[K],
+                                              uint32_t (&w)[K], uint32_t (&p)[K], int depth,
+                                              const uint8_t *__restrict__ mleft) {
+    for (int d = 0; d < depth; ++d) {
+        uint32_t x[K], c[K];
+        uint2 pr[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            c[k] = q[k] + ((w[k] & 0xFFFu) << 3);
+            x[k] = lds32(lds, (w[k] & 0xF000u) | lane_base[k]);
+            pr[k] = lds64(lds, c[k]);
+        }
+        uint32_t moving = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            bool left = x[k] <= w[k];
+            if (x[k] == 0xFFFFFFFFu)
+                left = (w[k] & 0xFFFu) == 0 ? w[k] >= 0x10000u : mleft[(p[k] - kRankNodeB) >> 2] != 0;
+            w[k] = left ? pr[k].x : pr[k].y;
+            p[k] = c[k] + (left ? 0u : 4u);
+            q[k] = c[k];
+            moving |= w[k] & 0xFFFu;
+        }
+        if (!__any(moving != 0)) return;
+    }
+}
+
 template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
@@ -1171,6 +1335,19 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
             nd[r * GG + g] = n0;
             lane_base[r * GG + g] = lrow[r];
         }
+    }
+    if constexpr (P16 == 4) {  // pair layout: pa (the root, a pair's left word) is q
+        uint32_t q[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) q[k] = pa[k];
+        if (any_nan) {
+            pair_walk_nan<K>(lds, lane_base, q, nd, pa, dmax, ml);
+        } else {
+            pair_walk<K, PIPE>(lds, lane_base, q, nd, dmax);
+#pragma unroll
+            for (int k = 0; k < K; ++k) pa[k] = q[k] + (nd[k] < 0x10000u ? 4u : 0u);  // right leaf: 2nd word
+        }
+        return;
     }
     if (any_nan)
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
@@ -1279,7 +1456,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const int tid = threadIdx.x;
     {
         const uint32_t *nb = nodes + node_base;
-        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = (P16 && P16 != 4) ? nb[i] ^ 0xFFFF0000u : nb[i];
     }
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
@@ -1294,7 +1471,7 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     const bool any_nan = *nan_flag != 0;  // uniform
     uint32_t lrow[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * (P16 ? 2 : 4));
+    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * ((P16 && P16 != 4) ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R], q2[R], q3[R];
@@ -1334,7 +1511,9 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
 #pragma unroll
                 for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
                     const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                    if (P16)
+                    if (P16 == 4)
+                        s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : (u + 1u) << 16;
+                    else if (P16)
                         s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
                     else
                         s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
@@ -1540,7 +1719,7 @@ struct RankLayout {
 constexpr int64_t kSlotSpan = 32767;
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
-                      RankLayout &L, bool v2 = false) {
+                      RankLayout &L, bool v2 = false, bool pair = false) {
     if (!v2 && d->n_features > 15) {
         set_error("rank layout: %d features > 15", d->n_features);
         return FDX_E_UNSUPPORTED;
@@ -1566,6 +1745,10 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         auto &u = U[f];
         std::sort(u.begin(), u.end());
         u.erase(std::unique(u.begin(), u.end(), [](float a, float b) { return a == b; }), u.end());
+        if (pair && (int64_t)u.size() > kRankMaxRank) {
+            set_error("rank layout v3: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank);
+            return FDX_E_UNSUPPORTED;
+        }
         if (!v2 && (int64_t)u.size() > kRankMaxRank + 1) {
             set_error("rank layout: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank + 1);
             return FDX_E_UNSUPPORTED;
@@ -1640,6 +1823,65 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         pend.pop_back();
         emit(w + (int64_t)((hi & 0xFFFFFFu) >> 3));
     };
+    if (pair) {
+        // v3 (see pair_walk): every tree is a run of 8-byte pairs, its root the left word of
+        // the first (the right word is never reached); pre-order over pairs, so a left child's
+        // children pair follows its own pair and the offsets are pair counts of left subtrees
+        int32_t dm = 0;
+        std::function<void(int64_t, int64_t, int32_t)> place = [&](int64_t w, int64_t pos, int32_t dep) {
+            const uint64_t nd = packed[(size_t)w];
+            if (!(nd >> 63)) {
+                double v;
+                memcpy(&v, &nd, 8);
+                L.nodes[(size_t)pos] = (pos & 1) ? 0u : 0x7FFF0000u;
+                L.orig[(size_t)pos] = worig[(size_t)w];
+                L.lval[(size_t)pos] = v;
+                dm = std::max(dm, dep);
+                return;
+            }
+            const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
+            const int f = (int)((hi >> 24) & 63);
+            float t;
+            memcpy(&t, &lo, 4);
+            const auto &u = U[f];
+            const int64_t k = std::lower_bound(u.begin(), u.end(), t) - u.begin();
+            const int64_t cp = (int64_t)L.nodes.size();
+            push(0u, -1, 0.0, 0);
+            push(0u, -1, 0.0, 0);
+            const int64_t off = cp / 2 - pos / 2;
+            if (off < 1 || off > 0xFFF) ok = false;
+            L.nodes[(size_t)pos] = ((uint32_t)(k + 1) << 16) | ((uint32_t)f << 12) | (uint32_t)(off & 0xFFF);
+            L.orig[(size_t)pos] = worig[(size_t)w];
+            L.ml[(size_t)pos] = (uint8_t)((hi >> 30) & 1);
+            place(w + 1, cp, dep + 1);
+            place(w + (int64_t)((hi & 0xFFFFFFu) >> 3), cp + 1, dep + 1);
+        };
+        for (int32_t tr = 0; tr < d->n_trees; ++tr) {
+            const int64_t tb = (int64_t)L.nodes.size();  // even: every tree is whole pairs
+            push(0u, -1, 0.0, 0);
+            push(0u, -1, 0.0, 0);
+            dm = 0;
+            place(d->node_offsets[tr], tb, 0);
+            if (!ok) {
+                set_error("rank layout v3: tree %d: a children pair is more than 4095 pairs away", tr);
+                return FDX_E_UNSUPPORTED;
+            }
+            const int64_t te = (int64_t)L.nodes.size();
+            if (te - tb > max_tree_nodes) {
+                set_error("rank layout v3: tree %d has %lld words > LDS budget %lld", tr, (long long)(te - tb),
+                          (long long)max_tree_nodes);
+                return FDX_E_UNSUPPORTED;
+            }
+            L.root.push_back((int32_t)tb);
+            L.depth.push_back(dm);
+            L.offsets.push_back(te);
+        }
+        if (L.nodes.size() >= (size_t(1) << 31)) {
+            set_error("rank layout: too many nodes");
+            return FDX_E_UNSUPPORTED;
+        }
+        return FDX_OK;
+    }
     for (int32_t tr = 0; tr < d->n_trees; ++tr) {
         const int64_t tb = (int64_t)L.nodes.size();
         margin = 2 * wdepth[(size_t)tr] + 16;
@@ -1687,7 +1929,10 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
 
 namespace fdx {
 namespace {
-int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair = false);
+// node format a variant runs on: 1 = rank layout v1, 2 = v2, 3 = v3 (sibling pairs)
+int variant_format(const Variant &v) { return v.p16 == 4 ? 3 : (v.p16 >= 2 ? 2 : 1); }
+int forest_format(const fdx_forest_s *F) { return F->rank_pair ? 3 : (F->rank_v2 ? 2 : 1); }
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
@@ -1752,13 +1997,13 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
         set_error("variant %d needs the rank layout, which this forest does not fit", variant);
         return FDX_E_UNSUPPORTED;
     }
-    if (kVariants[variant].rank && (kVariants[variant].p16 >= 2) != F->rank_v2) {
-        // the variant runs on the other node format: rebuild the rank layout in it
-        const bool want_v2 = kVariants[variant].p16 >= 2;
-        int rc = install_rank_layout(F, want_v2, nullptr);
+    if (kVariants[variant].rank && variant_format(kVariants[variant]) != forest_format(F)) {
+        // the variant runs on another node format: rebuild the rank layout in it
+        const int want = variant_format(kVariants[variant]), had = forest_format(F);
+        int rc = install_rank_layout(F, want == 2, nullptr, want == 3);
         if (rc) {
-            install_rank_layout(F, !want_v2, nullptr);  // restore the previous format
-            set_error("variant %d needs rank layout v%d, which this forest does not fit", variant, want_v2 ? 2 : 1);
+            install_rank_layout(F, had == 2, nullptr, had == 3);  // restore the previous format
+            set_error("variant %d needs rank layout v%d, which this forest does not fit", variant, want);
             return FDX_E_UNSUPPORTED;
         }
     }
@@ -1802,13 +2047,13 @@ static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL, int versio
     std::vector<int32_t> orig, root, depth;
     int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
-    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2);
+    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2, version == 3);
 }
 
 extern "C" int fdx_forest_rank_layout_size2(const fdx_forest_desc *d, int32_t version, int64_t *n_nodes,
                                             int32_t *n_thresholds, int32_t *n_slots) {
     FDX_REQUIRE(n_nodes && n_thresholds && n_slots, "null output");
-    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
+    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3");
     RankLayout RL;
     int rc = rank_layout_host(d, RL, version);
     if (rc) return rc;
@@ -1822,7 +2067,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
                                      int32_t *orig_out, double *leaf_value_out, uint8_t *missing_left_out,
                                      int32_t *root_out, int32_t *depth_out, float *thr_out, int32_t *thr_off_out,
                                      int32_t *slot_feat_out, int32_t *slot_base_out) {
-    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
+    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3");
     FDX_REQUIRE(nodes_out && orig_out && leaf_value_out && missing_left_out && root_out && depth_out && thr_off_out &&
                     slot_feat_out && slot_base_out,
                 "null output");
@@ -1848,7 +2093,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
 
 extern "C" int fdx_forest_layout(fdx_forest F, int32_t *layout, int32_t *n_slots) {
     FDX_REQUIRE(F && layout && n_slots, "null pointer");
-    *layout = !F->rank_ok ? 0 : (F->rank_v2 ? (F->rank_identity ? 3 : 2) : 1);
+    *layout = !F->rank_ok ? 0 : (F->rank_pair ? 4 : (F->rank_v2 ? (F->rank_identity ? 3 : 2) : 1));
     *n_slots = F->rank_v2 ? F->rn_slots : (F->rank_ok ? 16 : 0);
     return FDX_OK;
 }
@@ -1901,19 +2146,20 @@ void free_rank_buffers(fdx_forest_s *F) {
 // Build the rank layout (v2 nodes when `v2`, else v1) from the host copy of the packed forest
 // and upload it with its search tables; synchronous (creation / set_variant, off the hot path).
 // On FDX_E_UNSUPPORTED the forest has no rank layout (rank_ok = false).
-int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair) {
     free_rank_buffers(F);
-    F->rank_ok = F->rank_v2 = F->rank_identity = false;
+    F->rank_ok = F->rank_v2 = F->rank_identity = F->rank_pair = false;
     fdx_forest_desc d{};
     d.n_trees = F->n_trees;
     d.n_features = F->n_features;
     d.node_offsets = F->node_offsets.data();
     RankLayout RL;
     if (v2 && F->zstride != 16) return FDX_E_UNSUPPORTED;
-    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2);
+    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2, pair && !v2);
     if (rc) return rc;
     F->rank_ok = true;
     F->rank_v2 = v2;
+    F->rank_pair = pair && !v2;
     if (v2) {
         bool ident = RL.n_slots <= 16 && RL.n_slots == F->n_features;
         for (int j = 0; j < RL.n_slots && ident; ++j) ident = RL.slot_feat[j] == j && RL.slot_base[j] == 0;
@@ -2308,6 +2554,12 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                     case 45: FDX_LAUNCH_RANK(1024, 1, 4, 2, 2); break;
                     case 46: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                     case 47: FDX_LAUNCH_RANK(1024, 1, 8, 3, 2); break;
+                    case 48: FDX_LAUNCH_RANK(1024, 1, 6, 4, 0); break;
+                    case 49: FDX_LAUNCH_RANK(1024, 1, 6, 4, 1); break;
+                    case 50: FDX_LAUNCH_RANK(1024, 1, 8, 4, 1); break;
+                    case 51: FDX_LAUNCH_RANK(1024, 1, 6, 4, 2); break;
+                    case 52: FDX_LAUNCH_RANK(1024, 1, 9, 4, 2); break;
+                    case 53: FDX_LAUNCH_RANK(1024, 1, 4, 4, 1); break;
                     default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK

@@ -112,7 +112,7 @@ class FraudPipeline:
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
                   proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, mark=None,
-                  validate: bool = True):
+                  validate: bool = True, overlap: Optional[bool] = None):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
@@ -125,7 +125,8 @@ class FraudPipeline:
         meet at the row assembly.  mark(stage, stream) is called after each stage is enqueued
         on its stream (bench.py records a HIP event there).  validate: the customer / terminal
         ids must lie in [0, n_customers) / [0, n_terminals) (counted on the device, read at
-        the layout's host sync -- no extra stall)."""
+        the layout's host sync -- no extra stall).  overlap=False runs the terminal half on the
+        caller's stream too (None: FDX_OVERLAP, default on)."""
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         main = stream or torch.cuda.current_stream()
@@ -136,7 +137,7 @@ class FraudPipeline:
         if validate:
             rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
                   ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
-        if not _OVERLAP:
+        if not (_OVERLAP if overlap is None else overlap):
             side = main
         side.wait_stream(main)
         # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the

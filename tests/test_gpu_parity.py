@@ -307,7 +307,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(48)))
+@pytest.mark.parametrize("variant", list(range(54)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")
@@ -406,3 +406,26 @@ def test_fused_scoring_rank_table_overflows(dev):
     pipe.run_fused(*args, 400, 500, p1, ws)
     np.testing.assert_array_equal(p1.cpu().numpy(), p_ref.cpu().numpy())
     np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
+
+
+@pytest.mark.parametrize("variant", [41, 46, 48, 49, 51, 52])
+def test_fused_scoring_every_rank_format(dev, golden, variant):
+    """The fused scoring path (rank rows prepared in-pipeline) on each rank node format --
+    v1 (41), v2 compact (46), v3 sibling pairs (48, 50) -- equals featurize + float64 X +
+    predict on the wide layout (variant 1)."""
+    from fdx import synth
+    from fdx.pipeline import FraudPipeline
+
+    z = golden("forest_rf5d8.npz")
+    f = ops.Forest(_forest(z), 15, z["mean"], z["scale"])
+    d = synth.generate(n_customers=1500, n_terminals=3000, nb_days=50, seed=17)
+    args = (T(d["ts"], torch.int64, dev), T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev),
+            T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    n = len(d["ts"])
+    pipe = FraudPipeline(forest=f)
+    f.set_variant(1)
+    _, p_ref = pipe.run(*args, 1500, 3000)
+    f.set_variant(variant)
+    p = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 1500, 3000, p, ops.workspace(f.workspace_size(n * 2), dev))
+    np.testing.assert_array_equal(p.cpu().numpy(), p_ref.cpu().numpy())
