@@ -43,6 +43,7 @@ class Features:
 _OVERLAP = os.environ.get("FDX_OVERLAP", "1") != "0"            # terminal half on a side stream
 _CUST_PAYLOAD = os.environ.get("FDX_CUSTOMER_PAYLOAD", "1") != "0"  # re-key carries ts / amount
 _TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key carries ts + fraud bit
+_SIDE_PRIORITY = int(os.environ.get("FDX_SIDE_PRIORITY", "0"))        # side stream priority (-1 = high)
 
 
 class FraudPipeline:
@@ -131,7 +132,7 @@ class FraudPipeline:
         mk = mark or (lambda _name, _st: None)
         main = stream or torch.cuda.current_stream()
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
-            self._side = torch.cuda.Stream(device=ts_ns.device)
+            self._side = torch.cuda.Stream(device=ts_ns.device, priority=_SIDE_PRIORITY)
         side = self._side
         mk("start", main)
         if validate:

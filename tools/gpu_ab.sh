@@ -7,7 +7,7 @@ run() {  # run <name> <env assignments...>
     local name=$1; shift
     env "$@" timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 \
         > gpurun_out/${TAG}_ab_${name}.json 2>> gpurun_out/${TAG}_ab.err
-    python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_ab_${name}.json')); print('${name}', d['ms_per_step'], [(r['stage'], r['ms']) for r in d['kernels']['per_stage']])"
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_ab_${name}.json')); print('${name}', d['ms_per_step'], [(r['stage'], r['ms_in_step']) for r in d['kernels']['per_stage']])"
 }
 for spec in ${AB_RUNS:-base:FDX_OVERLAP=1}; do
     name=${spec%%:*}
