@@ -100,6 +100,8 @@ def parse():
                     help="rows of the sklearn predict_proba sample in the CPU baseline")
     ap.add_argument("--forest-variant", type=int, default=-1,
                     help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
+    ap.add_argument("--avg-mode", choices=("exact", "scan"), default="exact",
+                    help="customer averages: pandas-exact recurrence (default) or float64 prefix sums (SURVEY §7.4)")
     ap.add_argument("--isolated-steps", type=int, default=3,
                     help="extra untimed steps with every stage on one stream: per-kernel times for the roofline table")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
@@ -299,7 +301,7 @@ def main():
         raise SystemExit("forest parity check against sklearn failed")
 
     ts, cust, term, amt, fr = g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"]
-    pipe = FraudPipeline(forest=forest)
+    pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
     marks_all = []   # per timed step: [(stage, event), ...]
@@ -403,7 +405,8 @@ def main():
                                f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
                    "tx_per_gpu": n_local, "global_tx": n_total,
                    "parallelism": f"customer-sharded x{world}" + (" (RCCL all-to-all re-key)" if world > 1 else ""),
-                   "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)"},
+                   "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)",
+                   "customer_averages": args.avg_mode},
         "roofline": {"kernel": "k_forest_rank", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(max(fk)) if fk else None, "traffic_unit": "HBM bytes per launch (PMC)",

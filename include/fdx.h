@@ -104,6 +104,41 @@ int fdx_customer_layout_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, 
                                        int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
                                        double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
                                        int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes, void *stream);
+/* fdx_customer_layout over GROUPED ts / amount without the window starts (the scan mode's
+ * layout: fdx_customer_windows_scan computes the windows itself). */
+int fdx_customer_layout_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                const int64_t *gts_d, const double *gamount_d, int32_t n_windows,
+                                int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                                int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *workspace_d,
+                                size_t workspace_bytes, void *stream);
+/* Customer windows, SCAN mode (SURVEY.md §7 step 4 / §8(b) "exact|scan" mode flag;
+ * replaces the same feature_transformation.ipynb:1092-1093 call as fdx_customer_windows):
+ * the rolling sums from float64 prefix sums over each segment instead of pandas' sequential
+ * Kahan add/remove recurrence -- fully parallel (one wave per segment).  NB is exact; the
+ * SUM agrees with pandas to ~1e-13 relative, ~1e-13 absolute for a window whose amounts
+ * sum to 0 (NOT bit-exact; pandas' "n equal values -> prev * n" rule is not applied); SUM
+ * is NaN when NB == 0.  Inputs are grouped
+ * (fdx_rekey_payload outputs: segment s = rows [seg_off_d[s], seg_off_d[s+1]), time-sorted).
+ * Output: with sorder_d / goff_d (an interleaved layout of the same segments, n_out =
+ * n_slots): nb_d / val_d [W][n_out] by slot, exactly the shape of fdx_customer_windows_walk;
+ * else by grouped position (n_out >= n).  val = SUM when val_is_sum, else SUM / NB (the
+ * average, IEEE division).  Workspace: fdx_customer_windows_scan_workspace_size(n, n_seg)
+ * bytes (segments longer than 1,024 rows keep their prefix sums there). */
+size_t fdx_customer_windows_scan_workspace_size(int64_t n, int64_t n_seg);
+int fdx_customer_windows_scan(const int64_t *gts_d, const double *gamount_d, const int64_t *seg_off_d,
+                              int64_t n_seg, int64_t n, const int64_t *window_ns, int32_t n_windows,
+                              const int32_t *sorder_d, const uint32_t *goff_d, int64_t n_out, int32_t *nb_d,
+                              double *val_d, int32_t val_is_sum, void *workspace_d, size_t workspace_bytes,
+                              void *stream);
+/* The slot form of the scan mode over a layout built WITH window starts
+ * (fdx_customer_layout_starts_grouped): the window starts come from the layout, so the scan
+ * is two coalesced passes -- per-segment prefix sums (grouped order), then NB / SUM by slot.
+ * Same outputs and precision as fdx_customer_windows_scan(sorder_d, goff_d, ...); gamount_d
+ * grouped; workspace fdx_customer_windows_scan_workspace_size(n, n_seg). */
+int fdx_customer_windows_scan_slots(const double *gamount_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                    const int32_t *sorder_d, const uint32_t *goff_d, int64_t n_slots,
+                                    int32_t n_windows, const int32_t *starts_d, int32_t *nb_d, double *sum_d,
+                                    void *workspace_d, size_t workspace_bytes, void *stream);
 /* The sequential half of fdx_customer_windows_interleaved over the starts of
  * fdx_customer_layout_starts: nb_d / sum_d as there ([W][n_slots] by slot; n_windows >= 3,
  * i.e. <= 21 segments per wave). */

@@ -764,7 +764,7 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 // tile = 1: k_forest_tile (rows resident, trees streamed) instead of k_forest_chunk.
 // rank = 1: k_forest_rank over the rank layout (4-byte nodes, u16 rank rows).
 struct Variant {
-    int block, rows, group, tile, rank, p16 = 0, pipe = 0;
+    int block, rows, group, tile, rank, p16 = 0, pipe = 0, occ = 1;
 };
 constexpr int kDefaultRankVariant = 41;  // measured fastest on MI355X (r01: G=6 walks per lane, pipelined, paired waits)
 constexpr Variant kVariants[] = {
@@ -792,7 +792,9 @@ constexpr Variant kVariants[] = {
     // 48..: rank layout v3, sibling pairs (one LDS round trip per step; p16 = 4)
     // (pipe = SEL of pair_walk: 0 compiler select, 1 v_bfi select, 2 grouped compares)
     {1024, 1, 6, 0, 1, 4, 0}, {1024, 1, 6, 0, 1, 4, 1}, {1024, 1, 8, 0, 1, 4, 1}, {1024, 1, 6, 0, 1, 4, 2},
-    {1024, 1, 9, 0, 1, 4, 2}, {1024, 1, 4, 0, 1, 4, 1}};
+    {1024, 1, 9, 0, 1, 4, 2}, {1024, 1, 4, 0, 1, 4, 1},
+    // 54..: compact v2 nodes, two 1,024-thread blocks per CU (8 waves per SIMD, <= 64 VGPRs)
+    {1024, 1, 4, 0, 1, 3, 2, 2}, {1024, 1, 6, 0, 1, 3, 2, 2}, {1024, 1, 3, 0, 1, 3, 2, 2}};
 constexpr int kDefaultRankV2Variant = 44;
 constexpr int kDefaultRankCompactVariant = 46;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
@@ -1423,8 +1425,15 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-template <int BLOCK, int R, int G, int P16, int PIPE>
-__global__ void __launch_bounds__(BLOCK) k_forest_rank(
+// OCC = workgroups per CU: 2 halves the LDS budget (80 KiB: compact u16 planes + a smaller
+// node chunk) and caps the kernel at 64 VGPRs, so two 1,024-thread blocks -- 8 waves per SIMD
+// instead of 4 -- share a CU (more chunks, i.e. more row re-reads, for more issue-level
+// parallelism).
+template <int OCC>
+constexpr int kLdsBudget = OCC == 2 ? 80 * 1024 - 2048 : kLdsTotal;
+
+template <int BLOCK, int R, int G, int P16, int PIPE, int OCC = 1>
+__global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
     const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1, const double *__restrict__ lval,
@@ -1449,7 +1458,8 @@ __global__ void __launch_bounds__(BLOCK) k_forest_rank(
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
-    constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
+    constexpr int kNodeWords = (kLdsBudget<OCC> - kXW * 4) / 4;
+    static_assert(OCC == 1 || P16 == 3, "two blocks per CU fit with the 32 KiB compact planes only");
     __shared__ __align__(16) uint32_t s_mem[kXW + kNodeWords];
     uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
@@ -1937,6 +1947,7 @@ int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
 constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
+constexpr int64_t kRankNodeCapHalf = (kLdsBudget<2> - kRankXWords * 2) / 4 - 1;  // 2 blocks per CU
 
 bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
 
@@ -1946,7 +1957,7 @@ bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; 
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
     F->tile_ok = v.tile != 0;
-    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
+    const int64_t cap_nodes = v.rank ? (v.occ == 2 ? kRankNodeCapHalf : (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap))
                                      : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
@@ -2014,6 +2025,14 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     const int prev = F->variant;
     F->variant = variant;
     build_chunks(F);
+    bool rank_fits = true;  // a rank kernel walks LDS-resident chunks only
+    for (const auto &c : F->chunks) rank_fits = rank_fits && c.in_lds;
+    if (kVariants[variant].rank && !rank_fits) {
+        F->variant = prev;
+        build_chunks(F);
+        set_error("variant %d: a tree does not fit its LDS node budget", variant);
+        return FDX_E_UNSUPPORTED;
+    }
     if (kVariants[variant].tile && !F->tile_ok) {
         F->variant = prev;
         build_chunks(F);
@@ -2513,15 +2532,17 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             for (size_t c = 0; c < (tv ? 1 : nc); ++c) {
                 const auto &ch = F->chunks[c];
                 const int first = c == 0, last = c + 1 == nc;
-#define FDX_LAUNCH_RANK(B, R, G, P, ...)                                                                      \
+#define FDX_LAUNCH_RANK2(B, R, G, P, PIPE, OCC)                                                               \
     do {                                                                                                      \
         const int64_t tiles_ = ceil_div(s1 - s0, (int64_t)(B) * (R));                                         \
-        const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu), tv ? (unsigned)nc : 1u); \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, __VA_ARGS__ + 0>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,     \
-                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, s1, F->rlval_d, \
-                           F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first, last,     \
-                           F->chunk_t_d, F->chunk_base_d, tv, n);                                                \
+        const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu * (OCC)),         \
+                        tv ? (unsigned)nc : 1u);                                                              \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, OCC>), grid, dim3(B), 0, st, F->rnodes_d,         \
+                           ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, \
+                           s1, F->rlval_d, F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees,  \
+                           first, last, F->chunk_t_d, F->chunk_base_d, tv, n);                                \
     } while (0)
+#define FDX_LAUNCH_RANK(B, R, G, P, ...) FDX_LAUNCH_RANK2(B, R, G, P, __VA_ARGS__ + 0, 1)
                 switch (F->variant) {
                     case 17: FDX_LAUNCH_RANK(1024, 1, 2, false); break;
                     case 18: FDX_LAUNCH_RANK(512, 2, 2, false); break;
@@ -2560,9 +2581,13 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                     case 51: FDX_LAUNCH_RANK(1024, 1, 6, 4, 2); break;
                     case 52: FDX_LAUNCH_RANK(1024, 1, 9, 4, 2); break;
                     case 53: FDX_LAUNCH_RANK(1024, 1, 4, 4, 1); break;
+                    case 54: FDX_LAUNCH_RANK2(1024, 1, 4, 3, 2, 2); break;
+                    case 55: FDX_LAUNCH_RANK2(1024, 1, 6, 3, 2, 2); break;
+                    case 56: FDX_LAUNCH_RANK2(1024, 1, 3, 3, 2, 2); break;
                     default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
                 }
 #undef FDX_LAUNCH_RANK
+#undef FDX_LAUNCH_RANK2
                 FDX_LAUNCHED("k_forest_rank");
             }
         }

@@ -643,6 +643,190 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     }
 }
 
+// ------------------------------------------------ customer windows, scan mode
+// The averages from float64 prefix sums instead of pandas' sequential Kahan add/remove
+// recurrence: fully parallel, one wave per segment.  Counts are exact; sums agree with pandas
+// to ~1e-13 relative (the prefix magnitude over the window sum times 2^-52; tests use rtol
+// 1e-10); pandas' "n equal values -> prev * n" rule is not applied.  Per segment (grouped,
+// time-sorted rows): E[j] = sum of the non-NaN amounts of rows [0, j), C[j] = their count
+// (wave scans of 64 rows + carry; LDS for segments <= kScanLds rows, else the segment's
+// range of the global scratch), ts staged in LDS alike.  Row t, window w:
+//   start = first j in [0, t] with ts_j > ts_t - W_w   (pandas closed='right')
+//   NB = C[t+1] - C[start],  SUM = E[t+1] - E[start]   (NaN when NB == 0)
+// Output position: slot goff[si / S] + t*S + si % S of the interleaved layout (sorder given,
+// segment s = sorder[si]) -- val = SUM, the walk's outputs -- or grouped position
+// seg_off[s] + t -- val = SUM / NB (val_is_sum = 0) or SUM.
+constexpr int kScanLds = 1024;
+__global__ void __launch_bounds__(64) k_customer_scan(
+    const int64_t *__restrict__ gts, const double *__restrict__ gamt, const int64_t *__restrict__ seg_off,
+    int64_t n_seg, const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff, int32_t S, int64_t n_out,
+    WinArgs win, int32_t n_win, int32_t *__restrict__ nb_out, double *__restrict__ val_out, int val_is_sum,
+    double *__restrict__ ge, int32_t *__restrict__ gc) {
+    __shared__ int64_t s_ts[kScanLds];
+    __shared__ double s_e[kScanLds + 1];
+    __shared__ int32_t s_c[kScanLds + 1];
+    const int lane = threadIdx.x;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int64_t si = blockIdx.x; si < n_seg; si += gridDim.x) {
+        const int64_t s = sorder ? sorder[si] : si;
+        const int64_t b = seg_off[s], L = seg_off[s + 1] - b;
+        if (L <= 0) continue;
+        const bool in_lds = L <= kScanLds;
+        double *E = in_lds ? s_e : ge + b + s;  // L + 1 entries
+        int32_t *C = in_lds ? s_c : gc + b + s;
+        const int64_t *T = gts + b;
+        const int64_t obase = sorder ? (int64_t)goff[si / S] + si % S : b;
+        const int64_t ostride = sorder ? S : 1;
+        if (lane == 0) {
+            E[0] = 0.0;
+            C[0] = 0;
+        }
+        double carry = 0.0;
+        int32_t ccarry = 0;
+        for (int64_t t0 = 0; t0 < L; t0 += kWave) {
+            const int64_t t = t0 + lane;
+            double v = 0.0;
+            int32_t c = 0;
+            if (t < L) {
+                const double a = gamt[b + t];
+                if (in_lds) s_ts[t] = T[t];
+                if (a == a) {
+                    v = a;
+                    c = 1;
+                }
+            }
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const double u = __shfl_up(v, d, kWave);
+                const int32_t uc = __shfl_up(c, d, kWave);
+                if (lane >= d) {
+                    v += u;
+                    c += uc;
+                }
+            }
+            const double e = carry + v;
+            const int32_t cc = ccarry + c;
+            if (t < L) {
+                E[t + 1] = e;
+                C[t + 1] = cc;
+            }
+            carry = __shfl(e, kWave - 1, kWave);
+            ccarry = __shfl(cc, kWave - 1, kWave);
+        }
+        if (!in_lds) __threadfence();  // this wave's scratch writes before its reads below
+        wave_sync();
+        auto ts_at = [&](int64_t j) -> int64_t { return in_lds ? s_ts[j] : T[j]; };
+        int64_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound
+        for (int64_t t = lane; t < L; t += kWave) {
+            const int64_t tv = ts_at(t);
+            const double et = E[t + 1];
+            const int32_t ct = C[t + 1];
+            for (int w = 0; w < n_win; ++w) {
+                const int64_t bound = tv - win.w[w];
+                int64_t a = prev[w], e = t;  // first j in [prev, t] with ts_j > bound (j = t qualifies)
+                while (a < e) {
+                    const int64_t m = (a + e) >> 1;
+                    if (ts_at(m) > bound) e = m; else a = m + 1;
+                }
+                prev[w] = a;
+                const int32_t nb = ct - C[a];
+                const double sum = nb > 0 ? et - E[a] : __builtin_nan("");
+                const int64_t o = (int64_t)w * n_out + obase + t * ostride;
+                nb_out[o] = nb;
+                val_out[o] = val_is_sum ? sum : sum / (double)nb;
+            }
+        }
+        wave_sync();
+    }
+}
+
+// Slot form of the scan mode, in two coalesced passes around the layout's window starts
+// (k_interleave<true, true>, segment-contiguous): k_seg_prefix writes every segment's E / C
+// (grouped order, E[seg_off[s] + s + j], one wave per segment), then k_scan_slots -- one
+// block per group of S segments, threads over slots (t, l) as k_interleave's copy -- reads
+// the starts and four prefix entries per window and writes NB / SUM by slot, coalesced.
+__global__ void __launch_bounds__(256) k_seg_prefix(const double *__restrict__ gamt, const int64_t *__restrict__ seg_off,
+                                                    int64_t n_seg, double *__restrict__ ge, int32_t *__restrict__ gc) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int64_t nw = (int64_t)gridDim.x * blockDim.x / kWave;
+    for (int64_t s = w0; s < n_seg; s += nw) {
+        const int64_t b = seg_off[s], L = seg_off[s + 1] - b;
+        double *E = ge + b + s;
+        int32_t *C = gc + b + s;
+        if (lane == 0) {
+            E[0] = 0.0;
+            C[0] = 0;
+        }
+        double carry = 0.0;
+        int32_t ccarry = 0;
+        for (int64_t t0 = 0; t0 < L; t0 += kWave) {
+            const int64_t t = t0 + lane;
+            double v = 0.0;
+            int32_t c = 0;
+            if (t < L) {
+                const double a = gamt[b + t];
+                if (a == a) {
+                    v = a;
+                    c = 1;
+                }
+            }
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const double u = __shfl_up(v, d, kWave);
+                const int32_t uc = __shfl_up(c, d, kWave);
+                if (lane >= d) {
+                    v += u;
+                    c += uc;
+                }
+            }
+            const double e = carry + v;
+            const int32_t cc = ccarry + c;
+            if (t < L) {
+                E[t + 1] = e;
+                C[t + 1] = cc;
+            }
+            carry = __shfl(e, kWave - 1, kWave);
+            ccarry = __shfl(cc, kWave - 1, kWave);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_scan_slots(
+    const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder, const uint32_t *__restrict__ goff,
+    int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win, const int32_t *__restrict__ starts,
+    const double *__restrict__ ge, const int32_t *__restrict__ gc, int32_t *__restrict__ nb_out,
+    double *__restrict__ sum_out) {
+    const int64_t g = blockIdx.x;
+    const int rows_per_iter = blockDim.x / S;
+    const int l = threadIdx.x % S, tt = threadIdx.x / S;
+    if (tt >= rows_per_iter) return;
+    const int64_t s0 = sorder[g * S];
+    const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
+    const int64_t base = goff[g];
+    const int64_t si = g * S + l;
+    if (si >= n_seg) return;
+    const int64_t s = sorder[si];
+    const int64_t b = seg_off[s], L = seg_off[s + 1] - b;
+    const double *E = ge + b + s;
+    const int32_t *C = gc + b + s;
+    for (int64_t t = tt; t < L; t += rows_per_iter) {
+        const double et = E[t + 1];
+        const int32_t ct = C[t + 1];
+        for (int w = 0; w < n_win; ++w) {
+            const int32_t st = starts[(int64_t)w * n_slots + base + (int64_t)l * Lg + t];
+            const int32_t nb = ct - C[st];
+            const int64_t o = (int64_t)w * n_slots + base + t * S + l;
+            nb_out[o] = nb;
+            sum_out[o] = nb > 0 ? et - E[st] : __builtin_nan("");
+        }
+    }
+}
+
 // ------------------------------------------------------------------ terminal windows
 constexpr int kTermBlock = 256;
 constexpr int kTermWaves = kTermBlock / kWave;
@@ -1136,7 +1320,11 @@ static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_
         set_error("interleaved layout needs %u slots > max_slots %lld", total, (long long)max_slots);
         return FDX_E_WORKSPACE;
     }
-    if (starts_d && grouped)
+    if (!starts_d && grouped)
+        hipLaunchKernelGGL((k_interleave<false, true>), dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d,
+                           sorder_d, cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, WinArgs{},
+                           n_windows, (int32_t *)nullptr, (int64_t)total);
+    else if (starts_d && grouped)
         hipLaunchKernelGGL((k_interleave<true, true>), dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
                            cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
                            (int64_t)total);
@@ -1186,6 +1374,51 @@ extern "C" int fdx_customer_layout_starts_grouped(const int64_t *seg_off_d, int6
     FDX_REQUIRE(starts_d, "null pointer");
     return customer_layout(seg_off_d, n_seg, cperm_d, gts_d, gamount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
                            irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, &wa, starts_d, true);
+}
+
+extern "C" int fdx_customer_layout_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                           const int64_t *gts_d, const double *gamount_d, int32_t n_windows,
+                                           int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                                           int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                                           size_t ws_bytes, void *stream) {
+    return customer_layout(seg_off_d, n_seg, cperm_d, gts_d, gamount_d, n_windows, sorder_d, goff_d, its_d, iamt_d,
+                           irow_d, max_slots, n_slots_h, ws, ws_bytes, stream, nullptr, nullptr, true);
+}
+
+/* slot form of the scan mode over a layout built WITH window starts (fdx.h) */
+extern "C" int fdx_customer_windows_scan_slots(const double *gamount_d, const int64_t *seg_off_d, int64_t n_seg,
+                                               int64_t n, const int32_t *sorder_d, const uint32_t *goff_d,
+                                               int64_t n_slots, int32_t n_windows, const int32_t *starts_d,
+                                               int32_t *nb_d, double *sum_d, void *ws, size_t ws_bytes,
+                                               void *stream);
+
+extern "C" size_t fdx_customer_windows_scan_workspace_size(int64_t n, int64_t n_seg) {
+    if (n < 0 || n_seg < 0) return 0;
+    return al256((size_t)(n + n_seg + 1) * 8) + al256((size_t)(n + n_seg + 1) * 4);
+}
+
+extern "C" int fdx_customer_windows_scan(const int64_t *gts_d, const double *gamount_d, const int64_t *seg_off_d,
+                                         int64_t n_seg, int64_t n, const int64_t *window_ns, int32_t n_windows,
+                                         const int32_t *sorder_d, const uint32_t *goff_d, int64_t n_out,
+                                         int32_t *nb_d, double *val_d, int32_t val_is_sum, void *ws, size_t ws_bytes,
+                                         void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(n_seg >= 0 && n >= 0 && n_out >= 0, "negative size");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(gts_d && gamount_d && seg_off_d && nb_d && val_d && ws, "null pointer");
+    FDX_REQUIRE(!sorder_d || goff_d, "sorder_d needs goff_d");
+    FDX_REQUIRE(ws_bytes >= fdx_customer_windows_scan_workspace_size(n, n_seg), "workspace too small");
+    const int32_t S = kWave / n_windows;
+    FDX_REQUIRE(sorder_d || n_out >= n, "n_out < n");
+    double *ge = reinterpret_cast<double *>(ws);
+    int32_t *gc = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + al256((size_t)(n + n_seg + 1) * 8));
+    const unsigned grid = (unsigned)std::min<int64_t>(n_seg, 256 * 64);
+    hipLaunchKernelGGL(k_customer_scan, dim3(grid), dim3(kWave), 0, as_stream(stream), gts_d, gamount_d, seg_off_d,
+                       n_seg, sorder_d, goff_d, S, n_out, wa, n_windows, nb_d, val_d, val_is_sum, ge, gc);
+    FDX_LAUNCHED("k_customer_scan");
+    return FDX_OK;
 }
 
 // A side stream (per device, created once) for launches that fork from the caller's stream
@@ -1317,5 +1550,29 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     }
 #undef FDX_RING
     FDX_LAUNCHED("k_customer_ring");
+    return FDX_OK;
+}
+
+extern "C" int fdx_customer_windows_scan_slots(const double *gamount_d, const int64_t *seg_off_d, int64_t n_seg,
+                                               int64_t n, const int32_t *sorder_d, const uint32_t *goff_d,
+                                               int64_t n_slots, int32_t n_windows, const int32_t *starts_d,
+                                               int32_t *nb_d, double *sum_d, void *ws, size_t ws_bytes,
+                                               void *stream) {
+    FDX_REQUIRE(n_seg >= 0 && n >= 0 && n_slots >= 0, "negative size");
+    FDX_REQUIRE(n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad n_windows");
+    if (n_seg == 0 || n == 0) return FDX_OK;
+    FDX_REQUIRE(gamount_d && seg_off_d && sorder_d && goff_d && starts_d && nb_d && sum_d && ws, "null pointer");
+    FDX_REQUIRE(ws_bytes >= fdx_customer_windows_scan_workspace_size(n, n_seg), "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const int32_t S = kWave / n_windows;
+    const int64_t n_groups = ceil_div(n_seg, S);
+    double *ge = reinterpret_cast<double *>(ws);
+    int32_t *gc = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + al256((size_t)(n + n_seg + 1) * 8));
+    hipLaunchKernelGGL(k_seg_prefix, dim3(stream_grid(n_seg * kWave, 256, 256 * 32)), dim3(256), 0, st, gamount_d,
+                       seg_off_d, n_seg, ge, gc);
+    FDX_LAUNCHED("k_seg_prefix");
+    hipLaunchKernelGGL(k_scan_slots, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d, goff_d, n_seg,
+                       S, n_slots, n_windows, starts_d, ge, gc, nb_d, sum_d);
+    FDX_LAUNCHED("k_scan_slots");
     return FDX_OK;
 }

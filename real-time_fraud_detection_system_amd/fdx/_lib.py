@@ -95,6 +95,11 @@ SIGNATURES = {
     "fdx_terminal_windows_grouped": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P, P, P, P]),
     "fdx_customer_layout_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, P, P, P, P, c_i64, P, P,
                                                           c_sz, P]),
+    "fdx_customer_layout_grouped": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),
+    "fdx_customer_windows_scan_workspace_size": (c_sz, [c_i64, c_i64]),
+    "fdx_customer_windows_scan": (ctypes.c_int, [P, P, P, c_i64, c_i64, P, c_i32, P, P, c_i64, P, P, c_i32, P, c_sz,
+                                                 P]),
+    "fdx_customer_windows_scan_slots": (ctypes.c_int, [P, P, c_i64, c_i64, P, P, c_i64, c_i32, P, P, P, P, c_sz, P]),
     "fdx_argsort_i64_workspace_size": (c_sz, [c_i64]),
     "fdx_argsort_i64": (ctypes.c_int, [P, c_i64, P, P, c_sz, P]),
     "fdx_is_sorted_i64": (ctypes.c_int, [P, c_i64, P, P]),

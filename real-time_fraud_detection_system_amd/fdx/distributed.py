@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, ops
+from .pipeline import _SCAN_DIRECT
 from ._lib import check
 
 
@@ -220,7 +221,10 @@ class ShardedPipeline:
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")
         cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
-        cnb, cavg = ops.customer_windows(gts, gamt, cseg, p.windows_days)
+        if p.avg_mode == "scan":
+            cnb, cavg = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days)
+        else:
+            cnb, cavg = ops.customer_windows(gts, gamt, cseg, p.windows_days)
         n = ts.numel()
         ld = 16 if p.n_features <= 16 else p.n_features
         X = torch.empty((n, ld), dtype=torch.float64, device=ts.device)
@@ -254,7 +258,8 @@ class ShardedPipeline:
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
         cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
-        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, p.windows_days,
+        scan = p.avg_mode == "scan"
+        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, None if (scan and _SCAN_DIRECT) else p.windows_days,
                                   grouped=True)  # (host sync on main)
         rc.check()
         p._slots_hint = lay.its.numel()
@@ -262,7 +267,10 @@ class ShardedPipeline:
             back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
                                               self.n_terminals_total, p.windows_days, p.delay_days, self.group)
             sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
-        inb, isum = ops.customer_windows_walk(lay, cseg)
+        if scan:
+            inb, isum = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days, lay=lay)
+        else:
+            inb, isum = ops.customer_windows_walk(lay, cseg)
         main.wait_stream(side)
         back.record_stream(main)
         sinv.record_stream(main)

@@ -215,6 +215,40 @@ def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30
     return nb, risk
 
 
+def customer_windows_scan(gts, gamount, seg_off, windows_days=(1, 7, 30), lay=None, val_is_sum: bool = False,
+                          stream=None):
+    """Customer windows in SCAN mode (fdx_customer_windows_scan): grouped ts / amount
+    (rekey_payload outputs) -> (nb int32 [W, m], val float64 [W, m]), by grouped position
+    (m = n; val = the average SUM / NB, or SUM when val_is_sum) or, with lay (an interleaved
+    layout of the same segments), by slot (m = n_slots; val = SUM, what customer_windows_walk
+    returns).  NB exact; the sums agree with pandas' roll_sum to ~1e-13 relative, not bit for
+    bit."""
+    _dev(gts, torch.int64, "gts"); _dev(gamount, torch.float64, "gamount"); _dev(seg_off, torch.int64, "seg_off")
+    n = gts.numel()
+    n_seg = seg_off.numel() - 1
+    W = len(windows_days)
+    dev = gts.device
+    m = lay.n_slots if lay is not None else n
+    nb = torch.empty((W, m), dtype=torch.int32, device=dev)
+    val = torch.empty((W, m), dtype=torch.float64, device=dev)
+    L = _lib.load()
+    ws = workspace(L.fdx_customer_windows_scan_workspace_size(n, n_seg), dev)
+    if lay is not None and lay.starts is not None:  # the layout's starts: two coalesced passes
+        if tuple(lay.windows_days) != tuple(int(w) for w in windows_days):
+            raise FdxError("layout starts were built for other windows")
+        check(L.fdx_customer_windows_scan_slots(_ptr(gamount), _ptr(seg_off), n_seg, n, _ptr(lay.sorder),
+                                                _ptr(lay.goff), m, W, _ptr(lay.starts), _ptr(nb), _ptr(val),
+                                                _ptr(ws), ws.numel(), _s(stream)),
+              "fdx_customer_windows_scan_slots")
+        return nb, val
+    check(L.fdx_customer_windows_scan(_ptr(gts), _ptr(gamount), _ptr(seg_off), n_seg, n, _win_ns(windows_days), W,
+                                      _ptr(lay.sorder) if lay is not None else None,
+                                      _ptr(lay.goff) if lay is not None else None, m, _ptr(nb), _ptr(val),
+                                      int(bool(val_is_sum or lay is not None)), _ptr(ws), ws.numel(), _s(stream)),
+          "fdx_customer_windows_scan")
+    return nb, val
+
+
 class CustomerLayout:
     """The interleaved (lane-major) customer layout of the scoring pipeline (fdx.h).
     starts: the window starts [W * max_slots] int32 when built by customer_layout(windows_days=...)."""
@@ -228,7 +262,7 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
                     windows_days=None, grouped: bool = False) -> CustomerLayout:
     """windows_days: also compute the window starts in the layout kernel (for
     customer_windows_walk).  grouped: ts_ns / amount are in grouped order (rekey_payload
-    outputs) and are read as sequential streams (needs windows_days)."""
+    outputs) and are read as sequential streams."""
     _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(amount, torch.float64, "amount")
     n_seg = seg_off.numel() - 1
@@ -247,9 +281,10 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
         ns = ctypes.c_int64(0)
         if windows_days is None:
             starts = None
-            rc = L.fdx_customer_layout(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount), int(n_windows),
-                                       _ptr(sorder), _ptr(goff), _ptr(its), _ptr(iamt), _ptr(irow), max_slots,
-                                       ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
+            fn = L.fdx_customer_layout_grouped if grouped else L.fdx_customer_layout
+            rc = fn(_ptr(seg_off), n_seg, _ptr(cperm), _ptr(ts_ns), _ptr(amount), int(n_windows),
+                    _ptr(sorder), _ptr(goff), _ptr(its), _ptr(iamt), _ptr(irow), max_slots,
+                    ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
         else:
             if len(windows_days) != int(n_windows):
                 raise FdxError("windows_days must have n_windows entries")

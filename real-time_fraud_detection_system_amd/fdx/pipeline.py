@@ -44,11 +44,21 @@ _OVERLAP = os.environ.get("FDX_OVERLAP", "1") != "0"            # terminal half 
 _CUST_PAYLOAD = os.environ.get("FDX_CUSTOMER_PAYLOAD", "1") != "0"  # re-key carries ts / amount
 _TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key carries ts + fraud bit
 _SIDE_PRIORITY = int(os.environ.get("FDX_SIDE_PRIORITY", "0"))        # side stream priority (-1 = high)
+_SCAN_DIRECT = os.environ.get("FDX_SCAN_DIRECT", "0") != "0"  # scan mode: one kernel with its own start searches
 
 
 class FraudPipeline:
+    """avg_mode: "exact" -- the customer averages bit for bit as pandas' roll_sum (the
+    sequential Kahan add/remove recurrence, k_customer_walk) -- or "scan" -- float64 prefix
+    sums, fully parallel, within ~1e-13 relative of pandas (the counts
+    and every other feature stay exact)."""
+
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
-                 flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None):
+                 flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
+                 avg_mode: str = "exact"):
+        if avg_mode not in ("exact", "scan"):
+            raise ValueError("avg_mode must be 'exact' or 'scan'")
+        self.avg_mode = avg_mode
         self.windows_days = tuple(int(w) for w in windows_days)
         self.delay_days = int(delay_days)
         self.flags_mode = flags_mode
@@ -75,7 +85,10 @@ class FraudPipeline:
         we, ni = ops.time_flags(ts_ns, self.flags_mode, stream)
         # the re-keys carry the columns the window kernels read (grouped, sequential)
         cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=stream)
-        cnb, cavg = ops.customer_windows(gts, gamt, cseg, self.windows_days, stream)
+        if self.avg_mode == "scan":
+            cnb, cavg = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, stream=stream)
+        else:
+            cnb, cavg = ops.customer_windows(gts, gamt, cseg, self.windows_days, stream)
         tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, stream=stream)
         tnb, trisk = ops.terminal_windows_grouped(tgts, tseg, gfraud=ops.gather(fraud, tperm, stream),
                                                   delay_days=self.delay_days, windows_days=self.windows_days,
@@ -161,11 +174,12 @@ class FraudPipeline:
         for t in (ts_ns, terminal, fraud):
             t.record_stream(side)  # inputs in use on the side stream
         # customer half (caller's stream): the re-key carries ts and amount into grouped order
-        if _CUST_PAYLOAD:
+        scan = self.avg_mode == "scan"
+        if _CUST_PAYLOAD or scan:
             cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
             mk("rekey_customer", main)
-            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint, self.windows_days,
-                                      grouped=True)
+            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
+                                      None if (scan and _SCAN_DIRECT) else self.windows_days, grouped=True)
         else:  # round-1 form: plain re-key, the layout gathers ts / amount through the perm
             cperm, cseg, _ = ops.rekey(customer, n_customers, main)
             mk("rekey_customer", main)
@@ -176,7 +190,10 @@ class FraudPipeline:
                 c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
-        inb, isum = ops.customer_windows_walk(lay, cseg, main)
+        if scan:  # the windows straight from the grouped rows into the layout's slots
+            inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
+        else:
+            inb, isum = ops.customer_windows_walk(lay, cseg, main)
         mk("customer_walk", main)
         main.wait_stream(side)
         trec.record_stream(main)

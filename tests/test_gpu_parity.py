@@ -307,7 +307,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(54)))
+@pytest.mark.parametrize("variant", list(range(57)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")
@@ -408,7 +408,7 @@ def test_fused_scoring_rank_table_overflows(dev):
     np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
 
 
-@pytest.mark.parametrize("variant", [41, 46, 48, 49, 51, 52])
+@pytest.mark.parametrize("variant", [41, 46, 48, 49, 51, 52, 54, 55])
 def test_fused_scoring_every_rank_format(dev, golden, variant):
     """The fused scoring path (rank rows prepared in-pipeline) on each rank node format --
     v1 (41), v2 compact (46), v3 sibling pairs (48, 50) -- equals featurize + float64 X +
