@@ -130,6 +130,15 @@ def spawn_ranks(n):
     return rc
 
 
+def stdout_to_stderr():
+    """Route this process's fd 1 to stderr (RCCL prints a version banner on stdout when a
+    communicator comes up) and return a file for the one JSON line on the real stdout."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def load_model(path):
     import numpy as np
 
@@ -258,6 +267,7 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    json_out = stdout_to_stderr()
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -498,7 +508,7 @@ def main():
         forest.set_variant(args.forest_variant if args.forest_variant >= 0 else default_variant)
         print(json.dumps({"variant_sweep_traverse": res}), file=sys.stderr)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1 or args.sharded:
         dist.destroy_process_group()
 

@@ -44,10 +44,11 @@ def parse():
 
 def main():
     args = parse()
-    from bench import load_model, spawn_ranks
+    from bench import load_model, spawn_ranks, stdout_to_stderr
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))  # one process per GPU, before this one touches the GPU
+    json_out = stdout_to_stderr()
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -191,7 +192,7 @@ def main():
         "setup_s": {"generate": round(t_gen, 1), "history_stream": round(t_hist, 1)},
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

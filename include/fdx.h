@@ -529,6 +529,11 @@ int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream);
 /* Non-blocking form: enqueues the copy of the status bits to flags_pinned_h (pinned host
  * memory, valid once the stream reaches this point); does not clear them. */
 int fdx_stream_status_async(fdx_stream s, int32_t *flags_pinned_h, void *stream);
+/* A HIP stream limited to the CUs whose bits are set in cu_mask (n_words x 32 bits, CU i =
+ * bit i % 32 of word i / 32; hipExtStreamCreateWithCUMask) -- for running two overlapped
+ * halves of a step on disjoint CU sets -- and its release. */
+int fdx_hip_stream_create_cu_mask(const uint32_t *cu_mask, int32_t n_words, void **stream_out);
+int fdx_hip_stream_destroy(void *stream);
 int fdx_stream_destroy(fdx_stream s);
 
 /* f-4 delay-aware split and Card-Precision@k (shared_functions.py:133-188, :352-411).

@@ -82,6 +82,8 @@ SIGNATURES = {
     "fdx_stream_status": (ctypes.c_int, [P, P, P]),
     "fdx_stream_status_async": (ctypes.c_int, [P, P, P]),
     "fdx_stream_destroy": (ctypes.c_int, [P]),
+    "fdx_hip_stream_create_cu_mask": (ctypes.c_int, [P, c_i32, ctypes.POINTER(P)]),
+    "fdx_hip_stream_destroy": (ctypes.c_int, [P]),
     "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,
                                             c_sz, P, P]),
     "fdx_card_precision_workspace_size": (ctypes.c_size_t, [c_i32]),

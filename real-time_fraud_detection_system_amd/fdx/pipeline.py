@@ -45,6 +45,22 @@ _CUST_PAYLOAD = os.environ.get("FDX_CUSTOMER_PAYLOAD", "1") != "0"  # re-key car
 _TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key carries ts + fraud bit
 _SIDE_PRIORITY = int(os.environ.get("FDX_SIDE_PRIORITY", "0"))        # side stream priority (-1 = high)
 _SCAN_DIRECT = os.environ.get("FDX_SCAN_DIRECT", "0") != "0"  # scan mode: one kernel with its own start searches
+_CU_SPLIT = os.environ.get("FDX_CU_SPLIT", "")  # "k/8": side stream on the CUs with index % 8 < k
+
+
+def _masked_stream(device, eighths: int):
+    """A torch stream over the HIP stream limited to the CUs with index % 8 < eighths."""
+    import ctypes
+
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = [0] * ((n_cu + 31) // 32)
+    for i in range(n_cu):
+        if i % 8 < eighths:
+            words[i // 32] |= 1 << (i % 32)
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    h = ctypes.c_void_p()
+    check(_lib.load().fdx_hip_stream_create_cu_mask(arr, len(words), ctypes.byref(h)), "fdx_hip_stream_create_cu_mask")
+    return torch.cuda.ExternalStream(h.value, device=device)
 
 
 class FraudPipeline:
@@ -145,7 +161,8 @@ class FraudPipeline:
         mk = mark or (lambda _name, _st: None)
         main = stream or torch.cuda.current_stream()
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
-            self._side = torch.cuda.Stream(device=ts_ns.device, priority=_SIDE_PRIORITY)
+            self._side = (_masked_stream(ts_ns.device, int(_CU_SPLIT.split("/")[0])) if _CU_SPLIT else
+                          torch.cuda.Stream(device=ts_ns.device, priority=_SIDE_PRIORITY))
         side = self._side
         mk("start", main)
         if validate:
