@@ -96,6 +96,16 @@ def _frame_out(df, perm_np, cols: dict, index_name="TRANSACTION_ID"):
     return out
 
 
+def _empty_out(df, names, index_name="TRANSACTION_ID"):
+    out = df.copy()
+    for name in names:
+        out[name] = np.zeros(0, np.float64)
+    if index_name in out.columns:
+        out.index = out[index_name].values
+        out.index.name = index_name
+    return out
+
+
 def get_customer_spending_behaviour_features(customer_transactions: pd.DataFrame,
                                              windows_size_in_days: Sequence[int] = (1, 7, 30),
                                              mode: str = "exact"):
@@ -106,6 +116,9 @@ def get_customer_spending_behaviour_features(customer_transactions: pd.DataFrame
         raise ValueError("mode must be 'exact' or 'scan'")
     dev = ops.require_gpu()
     df = customer_transactions
+    if len(df) == 0:  # pandas' groupby.apply of an empty frame: no rows, the new columns
+        return _empty_out(df, [f"CUSTOMER_ID_{k}_{w}DAY_WINDOW" for w in windows_size_in_days
+                               for k in ("NB_TX", "AVG_AMOUNT")])
     perm, seg, ts_d = _grouped_order(df, "CUSTOMER_ID", dev)
     amt_d = _to_dev(df["TX_AMOUNT"].values.astype(np.float64), torch.float64, dev)
     if mode == "scan":
@@ -127,6 +140,8 @@ def get_count_risk_rolling_window(terminal_transactions: pd.DataFrame, delay_per
     """feature_transformation.ipynb:1495-1522 for one or many keys of `feature` at once."""
     dev = ops.require_gpu()
     df = terminal_transactions
+    if len(df) == 0:
+        return _empty_out(df, [f"{feature}_{k}_{w}DAY_WINDOW" for w in windows_size_in_days for k in ("NB_TX", "RISK")])
     perm, seg, ts_d = _grouped_order(df, feature, dev)
     fr_d = _to_dev((df["TX_FRAUD"].values != 0).astype(np.uint8), torch.uint8, dev)
     nb, risk = ops.terminal_windows(ops.gather(ts_d, perm), ops.gather(fr_d, perm), seg, delay_period,

@@ -231,6 +231,8 @@ def customer_windows_scan(gts, gamount, seg_off, windows_days=(1, 7, 30), lay=No
     m = lay.n_slots if lay is not None else n
     nb = torch.empty((W, m), dtype=torch.int32, device=dev)
     val = torch.empty((W, m), dtype=torch.float64, device=dev)
+    if n == 0 or m == 0:
+        return nb, val
     L = _lib.load()
     ws = workspace(L.fdx_customer_windows_scan_workspace_size(n, n_seg), dev)
     if lay is not None and lay.starts is not None:  # the layout's starts: two coalesced passes
@@ -270,6 +272,13 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
     S = 64 // int(n_windows)
     dev = ts_ns.device
     L = _lib.load()
+    if n == 0:  # no rows: an empty layout (every consumer then has zero slots to process)
+        z32 = torch.zeros(0, dtype=torch.int32, device=dev)
+        return CustomerLayout(z32, torch.zeros(1, dtype=torch.int32, device=dev),
+                              torch.zeros(0, dtype=torch.int64, device=dev),
+                              torch.zeros(0, dtype=torch.float64, device=dev), z32, 0,
+                              None if windows_days is None else z32,
+                              None if windows_days is None else tuple(windows_days))
     max_slots = int(_slots_hint or (n + S * 4096))
     sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
     goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
@@ -311,6 +320,8 @@ def customer_windows_walk(lay: CustomerLayout, seg_off, stream=None):
     dev = lay.its.device
     nb = torch.empty((W, lay.n_slots), dtype=torch.int32, device=dev)
     sm = torch.empty((W, lay.n_slots), dtype=torch.float64, device=dev)
+    if lay.n_slots == 0:
+        return nb, sm
     check(_lib.load().fdx_customer_windows_walk(_ptr(lay.iamt), _ptr(seg_off), _ptr(lay.sorder), _ptr(lay.goff),
                                                 seg_off.numel() - 1, lay.n_slots, W, _ptr(lay.starts), _ptr(nb),
                                                 _ptr(sm), _s(stream)),

@@ -160,6 +160,8 @@ class FraudPipeline:
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         main = stream or torch.cuda.current_stream()
+        if ts_ns.numel() == 0:  # an empty table: nothing to score
+            return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
             self._side = (_masked_stream(ts_ns.device, int(_CU_SPLIT.split("/")[0])) if _CU_SPLIT else
                           torch.cuda.Stream(device=ts_ns.device, priority=_SIDE_PRIORITY))
