@@ -38,6 +38,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # row's feature rank), each 2 LDS-array cycles per wave64 instruction (MI355X_MICROARCH.md
 # §LDS table, ds_read_b32); one LDS-array cycle per clock per CU, 256 CUs at 2.4 GHz
 LDS_PEAK_STEPS = 256 * 2.4e9 / 4 * 64
+# ... and the MEASURED ceiling of that access pattern: random-address ds_read_b32 from a 64 KiB
+# LDS table, 1,024-thread block per CU, 32 independent reads in flight per lane, no
+# dependency: 1.561e11 wave-reads/s chip-wide (tools/lds_probe.hip, profiles/r02_lds_probe.txt;
+# conflict-free reads reach 2.9e11) -> node steps/s at 2 reads per step
+LDS_RANDOM_STEPS = 1.561e11 * 64 / 2
 
 # SURVEY.md §8(d) algorithmic bytes per transaction (compact logical I/O, read once + write once)
 ALG = {"K2": 30, "K1-cust": 58, "K1-term": 49, "K3": 90, "end-to-end": 107}
@@ -431,7 +436,11 @@ def main():
                            "achieved": float(f"{ach_steps:.4g}"), "peak": float(f"{LDS_PEAK_STEPS:.4g}"),
                            "frac": round(ach_steps / LDS_PEAK_STEPS, 4), "node_steps_per_row_max": steps_max,
                            "note": "2 ds_read per step at 2 LDS cycles each; steps = sum of tree depths (upper "
-                                   "bound: wave-wide early exit), so frac is an upper bound"}
+                                   "bound: wave-wide early exit), so frac is an upper bound",
+                           "measured_random_read_peak": float(f"{LDS_RANDOM_STEPS:.4g}"),
+                           "frac_of_measured_random_read_peak": round(ach_steps / LDS_RANDOM_STEPS, 4),
+                           "measured_peak_source": "tools/lds_probe.hip (profiles/r02_lds_probe.txt): random "
+                                                   "ds_read_b32, 32 independent reads in flight per lane"}
     if marks_all:
         table = []
         names = [s for s, _, _ in STAGES]
