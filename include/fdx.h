@@ -229,6 +229,13 @@ int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, 
                                  const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
                                  const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
                                  double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream);
+/* fdx_terminal_windows_grouped writing the count record of row r at rec_d[dest_map_d[r]]
+ * (e.g. the row's scoring slot from fdx_invert_slots, so the row assembly reads the records
+ * in slot order -- sequential -- instead of by row). */
+int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                                      const int32_t *dest_map_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
+                                      int64_t delay_ns, const int64_t *window_ns, int32_t n_windows, int32_t runs,
+                                      int64_t *rec_d, int32_t *scratch_d, void *stream);
 
 /* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
  * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /

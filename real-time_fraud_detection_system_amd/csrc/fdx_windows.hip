@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
     int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
-    int32_t *__restrict__ scratch) {
+    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap) {
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
     __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
     __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
@@ -897,7 +897,10 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     int64_t *lts = s_ts[wv];
     int32_t *lf = s_f[wv];
     auto fraud_of = [&](int64_t q) -> int { return gfraud ? (gfraud[q] != 0) : (int)((uint32_t)rows[q] >> 31); };
-    auto dest_of = [&](int64_t q) -> int64_t { return rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q; };
+    auto dest_of = [&](int64_t q) -> int64_t {
+        const int64_t r = rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q;
+        return dmap ? (int64_t)dmap[r] : r;  // dmap: row -> record position (e.g. its scoring slot)
+    };
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1133,10 +1136,10 @@ static int terminal_input_order(const int64_t *ts_ns_d, const uint8_t *fraud_d, 
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     if (runs)
         hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
-                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch);
+                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, (const int32_t *)nullptr);
     else
         hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
-                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch);
+                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, (const int32_t *)nullptr);
     e = hipGetLastError();
     (void)hipFreeAsync(tmp, st);
     if (e != hipSuccess) {
@@ -1221,10 +1224,10 @@ extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, cons
                            true, stream);
 }
 
-extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
-                                            const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                                            const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
-                                            double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream) {
+static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                            const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                            const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d, double *risk_d,
+                            int64_t *rec_d, int32_t *scratch_d, const int32_t *dest_map_d, void *stream) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -1234,15 +1237,36 @@ extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t 
     FDX_REQUIRE(gts_d && seg_off_d && scratch_d, "null pointer");
     FDX_REQUIRE(gfraud_d || rows_d, "fraud comes from gfraud_d or bit 31 of rows_d");
     FDX_REQUIRE(rec_d || (nb_d && risk_d), "no output");
+    FDX_REQUIRE(!dest_map_d || rec_d, "dest_map_d places count records");
     unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
     if (runs)
         hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
-                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d);
+                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d,
+                           dest_map_d);
     else
         hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
-                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d);
+                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d,
+                           dest_map_d);
     FDX_LAUNCHED("k_terminal_g");
     return FDX_OK;
+}
+
+extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                                            const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                            const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
+                                            double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream) {
+    return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs, nb_d,
+                            risk_d, rec_d, scratch_d, nullptr, stream);
+}
+
+extern "C" int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfraud_d,
+                                                 const int32_t *rows_d, const int32_t *dest_map_d,
+                                                 const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                                 const int64_t *window_ns, int32_t n_windows, int32_t runs,
+                                                 int64_t *rec_d, int32_t *scratch_d, void *stream) {
+    FDX_REQUIRE(dest_map_d, "null dest_map_d");
+    return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs,
+                            nullptr, nullptr, rec_d, scratch_d, dest_map_d, stream);
 }
 
 extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,

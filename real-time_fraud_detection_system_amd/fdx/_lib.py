@@ -95,6 +95,8 @@ SIGNATURES = {
     "fdx_rekey_payload_workspace_size": (c_sz, [c_i64, c_i32, c_i32]),
     "fdx_rekey_payload": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_terminal_windows_grouped": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P, P, P, P]),
+    "fdx_terminal_windows_grouped_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
+                                                         P]),
     "fdx_customer_layout_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, P, P, P, P, c_i64, P, P,
                                                           c_sz, P]),
     "fdx_customer_layout_grouped": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),

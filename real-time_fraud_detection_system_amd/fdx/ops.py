@@ -365,6 +365,27 @@ def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1
     return rec
 
 
+def terminal_windows_grouped_dest(gts, seg_off, rows, dest_map, n_out: int, gfraud=None, delay_days=7,
+                                  windows_days=(1, 7, 30), runs: bool = False, stream=None):
+    """terminal_windows_grouped's count records written at dest_map[row] of an [n_out, W]
+    int64 array (e.g. the rows' scoring slots: invert_slots); positions no row maps to are
+    left unwritten."""
+    _dev(gts, torch.int64, "gts"); _dev(seg_off, torch.int64, "seg_off"); _dev(rows, torch.int32, "rows")
+    _dev(dest_map, torch.int32, "dest_map")
+    if gfraud is not None:
+        _dev(gfraud, torch.uint8, "gfraud")
+    n = gts.numel()
+    W = len(windows_days)
+    rec = torch.empty((int(n_out), W), dtype=torch.int64, device=gts.device)
+    scratch = torch.empty(max(n, 1), dtype=torch.int32, device=gts.device)
+    check(_lib.load().fdx_terminal_windows_grouped_dest(_ptr(gts), _ptr(gfraud), _ptr(rows), _ptr(dest_map),
+                                                        _ptr(seg_off), seg_off.numel() - 1, n,
+                                                        int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W,
+                                                        int(bool(runs)), _ptr(rec), _ptr(scratch), _s(stream)),
+          "fdx_terminal_windows_grouped_dest")
+    return rec
+
+
 def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
                              runs: bool = False, records: bool = True, stream=None):
     """Terminal windows over grouped inputs (rekey_payload(terminal, ts, flag=fraud) outputs):

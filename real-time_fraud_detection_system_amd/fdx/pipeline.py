@@ -46,6 +46,9 @@ _TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key car
 _SIDE_PRIORITY = int(os.environ.get("FDX_SIDE_PRIORITY", "0"))        # side stream priority (-1 = high)
 _SCAN_DIRECT = os.environ.get("FDX_SCAN_DIRECT", "0") != "0"  # scan mode: one kernel with its own start searches
 _CU_SPLIT = os.environ.get("FDX_CU_SPLIT", "")  # "k/8": side stream on the CUs with index % 8 < k
+# terminal records written at their scoring slots (the row assembly then reads them in slot
+# order); the terminal windows wait for the customer layout
+_TERM_SLOTS = os.environ.get("FDX_TERM_SLOTS", "0") != "0"
 
 
 def _masked_stream(device, eighths: int):
@@ -177,9 +180,13 @@ class FraudPipeline:
         # perm); the records come out in input row order, read by the row assembly through irow.
         # Allocated under the side stream's context, so that the caching allocator hands
         # these buffers to nothing on the main stream while the side stream still uses them.
+        by_slot = _TERM_SLOTS and _TERM_PAYLOAD
         with torch.cuda.stream(side):
             mk("start", side)
-            if _TERM_PAYLOAD:
+            if by_slot:  # the windows come after the customer layout (below)
+                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+                mk("rekey_terminal", side)
+            elif _TERM_PAYLOAD:
                 tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
                 mk("rekey_terminal", side)
                 trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
@@ -189,7 +196,8 @@ class FraudPipeline:
                 mk("rekey_terminal", side)
                 trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days,
                                                    rows=tperm, stream=side)
-            mk("terminal_windows", side)
+            if not by_slot:
+                mk("terminal_windows", side)
         for t in (ts_ns, terminal, fraud):
             t.record_stream(side)  # inputs in use on the side stream
         # customer half (caller's stream): the re-key carries ts and amount into grouped order
@@ -209,6 +217,14 @@ class FraudPipeline:
                 c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
+        if by_slot:
+            slot_of = ops.invert_slots(lay.irow, ts_ns.numel(), lay.n_slots, main)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                trec = ops.terminal_windows_grouped_dest(tgts, tseg, tperm, slot_of, lay.n_slots,
+                                                         delay_days=self.delay_days,
+                                                         windows_days=self.windows_days, stream=side)
+                mk("terminal_windows", side)
         if scan:  # the windows straight from the grouped rows into the layout's slots
             inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
         else:
@@ -218,7 +234,7 @@ class FraudPipeline:
         trec.record_stream(main)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                   ws, main, n=lay.n_slots, val_is_sum=True)
+                                   ws, main, n=lay.n_slots, val_is_sum=True, term_by_slot=by_slot)
         mk("assemble_rows", main)
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
         mk("forest_traverse", main)

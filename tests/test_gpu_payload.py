@@ -142,3 +142,28 @@ def test_fused_pipeline_hot_terminal_matches_oracle(dev, golden):
         np.testing.assert_array_equal(X[:, 9 + j], ref[c], err_msg=c)
     for j, c in enumerate(oracle.CUSTOMER_COLS):
         np.testing.assert_array_equal(X[:, 3 + j], ref[c], err_msg=c)
+
+
+def test_terminal_records_at_scoring_slots(dev, monkeypatch):
+    """FDX_TERM_SLOTS form of run_fused: the terminal records written at the rows' scoring
+    slots (fdx_terminal_windows_grouped_dest over fdx_invert_slots), read in slot order by
+    the row assembly -- the same probabilities as the by-row records, every row."""
+    import os
+
+    from fdx import pipeline
+
+    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench_assets",
+                             "rf100_d20.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    g = synth.generate_device(3000, 6000, 90, seed=5, device=dev)
+    n = g["ts"].numel()
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
+    ws = ops.workspace(forest.workspace_size(n * 2), dev)
+    p_row = torch.empty(n, dtype=torch.float64, device=dev)
+    FraudPipeline(forest=forest).run_fused(*args, 3000, 6000, p_row, ws)
+    monkeypatch.setattr(pipeline, "_TERM_SLOTS", True)
+    p_slot = torch.empty(n, dtype=torch.float64, device=dev)
+    FraudPipeline(forest=forest).run_fused(*args, 3000, 6000, p_slot, ws)
+    assert torch.equal(p_row, p_slot)
