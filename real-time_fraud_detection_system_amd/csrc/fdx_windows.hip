@@ -890,6 +890,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
     __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
     __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
+    // RUNS, LDS-staged segments: the merged order's staging index | fraud << 15
+    __shared__ uint16_t s_q[RUNS ? kTermWaves : 1][RUNS ? kTermLdsRows : 1];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
@@ -962,17 +964,74 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
             nruns = nr;
             wave_sync();
         }
+        // LDS-staged segment of several runs: merge the runs in LDS (each element's merged
+        // position = its index in its run + the elements of the other runs before it, by
+        // binary search; ties: lower run first), then the single-run closed form -- (runs - 1)
+        // searches per element once, instead of runs x 4 searches per element
+        bool merged = false;
+        if constexpr (RUNS) {
+            if (in_lds && nruns > 1 && nruns <= max_runs) {
+                uint16_t *lq = s_q[wv];
+                constexpr int kCh = kTermLdsRows / kWave;
+                int32_t mpos[kCh];
+                int64_t mts[kCh];
+#pragma unroll
+                for (int k = 0; k < kCh; ++k) {
+                    const int64_t j = (int64_t)k * kWave + lane;
+                    mpos[k] = -1;
+                    if (j < L) {
+                        const int64_t tj = lts[j];
+                        int r = 0;
+                        while (r + 1 < nruns && lr[r + 1] <= j) ++r;
+                        int64_t m = j - lr[r];
+                        for (int r2 = 0; r2 < nruns; ++r2) {
+                            if (r2 == r) continue;
+                            int64_t lo = lr[r2], hi = lr[r2 + 1];
+                            while (lo < hi) {  // r2 < r: count ts <= tj; r2 > r: count ts < tj
+                                const int64_t mid = (lo + hi) >> 1;
+                                const int64_t x = lts[mid];
+                                if (r2 < r ? x <= tj : x < tj) lo = mid + 1; else hi = mid;
+                            }
+                            m += lo - lr[r2];
+                        }
+                        mpos[k] = (int32_t)m;
+                        mts[k] = tj;
+                    }
+                }
+                wave_sync();  // every read of the staging order's timestamps done
+#pragma unroll
+                for (int k = 0; k < kCh; ++k)
+                    if (mpos[k] >= 0) {
+                        const int64_t j = (int64_t)k * kWave + lane;
+                        lts[mpos[k]] = mts[k];
+                        lq[mpos[k]] = (uint16_t)(j | ((lf[j + 1] - lf[j]) << 15));  // lf: still staging order
+                    }
+                wave_sync();
+                int c2 = 0;  // prefix fraud counts in the merged order
+                for (int64_t c = 0; c < L; c += kWave) {
+                    const int64_t j = c + lane;
+                    const int f = j < L ? (int)(lq[j] >> 15) : 0;
+                    const int inc = wave_incl_scan(f, lane) + c2;
+                    if (j < L) lf[j + 1] = inc;
+                    c2 = __shfl(inc, kWave - 1, kWave);
+                }
+                wave_sync();
+                merged = true;
+            }
+        }
         for (int64_t i = lane; i < L; i += kWave) {
             const int64_t t = T(i);
-            const int64_t row = dest_of(b + i);
+            // merged: i is a position in the merged order; its record belongs to staging index qi
+            const int64_t qi = merged ? (int64_t)(s_q[RUNS ? wv : 0][i] & 0x7FFF) : i;
+            const int64_t row = dest_of(b + qi);
             int32_t nbh = 0, frh = 0;
-            if (!RUNS || nruns == 1) {
+            if (!RUNS || nruns == 1 || merged) {
                 const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
                 nbh = (int32_t)hi;
                 frh = F(hi);
                 for (int w = 0; w < n_win; ++w) {
                     const int64_t lo = ub(0, hi, t - delay - win.w[w]);
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, (int32_t)(hi - lo), frh - F(lo));
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, (int32_t)(hi - lo), frh - F(lo));
                 }
             } else if (nruns <= max_runs) {
                 for (int r = 0; r < nruns; ++r) {

@@ -67,13 +67,14 @@ class GpuKernels:
         return ops.terminal_windows_packed_unsorted(ts, fraud, seg, delay_days, windows_days, rows=rows)
 
     @staticmethod
-    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days):
+    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days, runs=True):
         """owner side: stable re-key of the receive buffer by local terminal id carrying ts
         (and the fraud bit in the perm), then the records of segments made of per-rank
-        time-sorted runs, indexed by receive position"""
+        time-sorted runs (runs=False: one rank -- every segment one run), indexed by receive
+        position"""
         perm, seg, gts, _ = ops.rekey_payload(rterm, n_local_terms, rts, flag=rfraud)
         return ops.terminal_windows_grouped(gts, seg, rows=perm, delay_days=delay_days, windows_days=windows_days,
-                                            runs=True)
+                                            runs=runs)
 
     @staticmethod
     def reply_assemble(reply, perm, W, X, col0):
@@ -151,7 +152,8 @@ def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows
     n_local_terms = (n_terminals_total + world - 1) // world
     # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
     # the records kernel handles such segments itself (no global time sort of the receive buffer)
-    reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days)  # by receive index
+    reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days,
+                                     runs=world > 1)  # by receive index
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
     alltoallv(back, reply, sc, rc, group)
     return back, send_perm

@@ -71,7 +71,7 @@ class CpuKernels:
         return torch.from_numpy(rec)
 
     @staticmethod
-    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days):
+    def terminal_records_rekey(rts, rterm, rfraud, n_local_terms, delay_days, windows_days, runs=True):
         perm, seg = CpuKernels.rekey(rterm, n_local_terms)
         return CpuKernels.terminal_records(rts, rfraud, perm, seg, delay_days, windows_days)
 
