@@ -616,6 +616,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
     for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
     stage_samples(s_smp, rt);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const bool rec16 = ((uintptr_t)term_rec & 15) == 0;  // uniform
     auto row_of = [&](int64_t j) -> int32_t { return j < n ? (cust_perm ? cust_perm[j] : (int32_t)j) : -1; };
     auto load = [&](int64_t j, int32_t r, PrepRow &L) {
         L.r = r;
@@ -628,8 +629,23 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
             L.cv[w] = cval[(int64_t)w * n + j];
         }
         const int64_t q_ = (val_is_sum & 2) ? j : (term_inv ? term_inv[r] : r);
+        const int64_t *src = term_rec + q_ * W;
+        if (rec16) {  // the 24-byte record in two loads (16-byte aligned pair first or second)
+            if ((q_ & 1) == 0) {
+                const longlong2 p = *reinterpret_cast<const longlong2 *>(src);
+                L.tw[0] = p.x;
+                L.tw[1] = p.y;
+                L.tw[2] = src[2];
+            } else {
+                const longlong2 p = *reinterpret_cast<const longlong2 *>(src + 1);
+                L.tw[0] = src[0];
+                L.tw[1] = p.x;
+                L.tw[2] = p.y;
+            }
+        } else {
 #pragma unroll
-        for (int w = 0; w < W; ++w) L.tw[w] = term_rec[q_ * W + w];
+            for (int w = 0; w < W; ++w) L.tw[w] = src[w];
+        }
     };
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     PrepRow cur;

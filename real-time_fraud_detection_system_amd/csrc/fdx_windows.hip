@@ -831,6 +831,10 @@ __global__ void __launch_bounds__(256) k_scan_slots(
 constexpr int kTermBlock = 256;
 constexpr int kTermWaves = kTermBlock / kWave;
 constexpr int kTermLdsRows = 1024;  // rows of one segment staged per wave (12 KB)
+// The short-segment pass: segments of <= kTermShortRows rows run in a kernel with a 256-row
+// stage (3 KB per wave instead of 12: about twice the resident waves for this latency-bound
+// kernel), the longer ones in a second launch with the full stage (see terminal_launch).
+constexpr int kTermShortRows = 256;
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
@@ -858,7 +862,11 @@ __device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, in
 // staged in LDS; a long segment does not use the LDS stage, so its run list takes the stage's
 // timestamp words instead (kMaxRunsLong entries).
 constexpr int kMaxRuns = 64;
-constexpr int kMaxRunsLong = 2 * kTermLdsRows - 1;
+// A/B switch (compile time): W = 3 count records stored as two wide stores
+#ifndef FDX_REC_PAIR
+#define FDX_REC_PAIR 1
+#endif
+constexpr bool kRecPair = FDX_REC_PAIR != 0;
 
 // Terminal windows over GROUPED inputs (fdx_rekey_payload carried ts -- and the fraud bit in
 // bit 31 of the perm -- through the re-key): every read is sequential within a segment.
@@ -874,24 +882,27 @@ constexpr int kMaxRunsLong = 2 * kTermLdsRows - 1;
 //   NB_w = hi - lo_w,  FRAUD_w = F[hi] - F[lo_w]  (F = prefix count of fraud rows)
 //   RISK_w = NB_w > 0 ? FRAUD_w / NB_w : 0   (fillna(0) of 0/0)
 // RUNS: every count is summed over the segment's time-sorted runs, each searched separately.
-// Segments of <= kTermLdsRows rows are staged in LDS.  Longer ones -- a hot terminal, or one
+// Segments of <= LR rows are staged in LDS.  Longer ones -- a hot terminal, or one
 // terminal's rows from every rank on its owner -- use global memory: the segment's wave
 // first writes the inclusive prefix fraud count of every position to scratch[q], then each
 // row binary-searches its window bounds in gts (per run) and reads two prefix counts:
 // O(L log L) per segment.  Only a segment of more unsorted runs than its run list holds
-// (> 64 in LDS, > 2047 long -- never the owner side, which has one run per source rank)
-// is counted directly, O(L) per row.
-template <bool RUNS>
+// (> 64 in LDS, > 2 LR - 1 long -- never the owner side, which has one run per source rank)
+// is counted directly, O(L) per row.  Only segments with len_lo < L <= len_hi are processed
+// (the short / long passes of terminal_launch).
+template <bool RUNS, int LR = kTermLdsRows>
 __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
     int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
-    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap) {
-    __shared__ int64_t s_ts[kTermWaves][kTermLdsRows];
-    __shared__ int32_t s_f[kTermWaves][kTermLdsRows + 1];
+    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap, int64_t len_lo, int64_t len_hi) {
+    static_assert(LR % kWave == 0 && LR <= 32768, "the merge packs a staging index in 15 bits");
+    constexpr int kMaxRunsLong = 2 * LR - 1;  // a long segment's run list in the stage's ts words
+    __shared__ int64_t s_ts[kTermWaves][LR];
+    __shared__ int32_t s_f[kTermWaves][LR + 1];
     __shared__ int32_t s_runs[RUNS ? kTermWaves : 1][kMaxRuns + 1];
     // RUNS, LDS-staged segments: the merged order's staging index | fraud << 15
-    __shared__ uint16_t s_q[RUNS ? kTermWaves : 1][RUNS ? kTermLdsRows : 1];
+    __shared__ uint16_t s_q[RUNS ? kTermWaves : 1][RUNS ? LR : 1];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int64_t gwave = (int64_t)blockIdx.x * kTermWaves + wv;
@@ -911,8 +922,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     for (int64_t seg = gwave; seg < n_seg; seg += nwaves) {
         const int64_t b = seg_off[seg], e = seg_off[seg + 1];
         const int64_t L = e - b;
-        if (L <= 0) continue;
-        const bool in_lds = L <= kTermLdsRows;
+        if (L <= len_lo || L > len_hi) continue;
+        const bool in_lds = L <= LR;
         // stage ts (LDS) and the inclusive prefix fraud counts (LDS: lf[j + 1]; global: scratch[b + j])
         int carry = 0;
         if (in_lds && lane == 0) lf[0] = 0;
@@ -972,7 +983,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
         if constexpr (RUNS) {
             if (in_lds && nruns > 1 && nruns <= max_runs) {
                 uint16_t *lq = s_q[wv];
-                constexpr int kCh = kTermLdsRows / kWave;
+                constexpr int kCh = LR / kWave;
                 int32_t mpos[kCh];
                 int64_t mts[kCh];
 #pragma unroll
@@ -1029,9 +1040,28 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                 const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
                 nbh = (int32_t)hi;
                 frh = F(hi);
-                for (int w = 0; w < n_win; ++w) {
-                    const int64_t lo = ub(0, hi, t - delay - win.w[w]);
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, (int32_t)(hi - lo), frh - F(lo));
+                if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
+                    // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
+                    // 16-byte alignment) instead of three: fewer random write transactions
+                    int64_t wd[3];
+#pragma unroll
+                    for (int w = 0; w < 3; ++w) {
+                        const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                        wd[w] = term_word((int32_t)(hi - lo), frh - F(lo));
+                    }
+                    int64_t *dst = rec_out + row * 3;
+                    if ((row & 1) == 0) {
+                        *reinterpret_cast<longlong2 *>(dst) = make_longlong2(wd[0], wd[1]);
+                        dst[2] = wd[2];
+                    } else {
+                        dst[0] = wd[0];
+                        *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(wd[1], wd[2]);
+                    }
+                } else {
+                    for (int w = 0; w < n_win; ++w) {
+                        const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                        term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, (int32_t)(hi - lo), frh - F(lo));
+                    }
                 }
             } else if (nruns <= max_runs) {
                 for (int r = 0; r < nruns; ++r) {
@@ -1152,6 +1182,32 @@ extern "C" int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount
     return FDX_OK;
 }
 
+// Every terminal-window launch: the short-segment pass (<= kTermShortRows rows, small LDS
+// stage, more resident waves) then the long pass (the 1,024-row stage, global memory beyond);
+// each skips the other's segments.  FDX_TERM_SPLIT=0: one launch with the 1,024-row stage.
+static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, const int32_t *rows,
+                            const int64_t *seg_off, int64_t n_seg, int64_t n, int64_t delay_ns, const WinArgs &wa,
+                            int32_t n_windows, int32_t *nb_d, double *risk_d, int64_t *rec_d, int32_t *scratch,
+                            const int32_t *dmap, hipStream_t st) {
+    static const bool split = [] {
+        const char *e = getenv("FDX_TERM_SPLIT");
+        return !(e && atoi(e) == 0);
+    }();
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
+    const int64_t lo = split ? kTermShortRows : 0, inf = INT64_MAX;
+#define FDX_TERM_LAUNCH(R, LRV, A, B)                                                                           \
+    hipLaunchKernelGGL((k_terminal_g<R, LRV>), dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off, n_seg, \
+                       n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, dmap, (int64_t)(A), (int64_t)(B))
+    if (runs) {
+        if (split) FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
+        FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
+    } else {
+        if (split) FDX_TERM_LAUNCH(false, kTermShortRows, 0, kTermShortRows);
+        FDX_TERM_LAUNCH(false, kTermLdsRows, lo, inf);
+    }
+#undef FDX_TERM_LAUNCH
+}
+
 // The input-order entry points (round 1's interface: ts / fraud in input order, segments
 // through the re-key perm) run the grouped kernel: a gather puts ts / fraud / destination in
 // grouped order first (stream-ordered temporaries), so every terminal kernel is k_terminal_g.
@@ -1192,13 +1248,8 @@ static int terminal_input_order(const int64_t *ts_ns_d, const uint8_t *fraud_d, 
         grow = (const int32_t *)(tmp + b_ts + b_fr);
     }
     int32_t *scratch = (int32_t *)(tmp + b_ts + b_fr + b_row);
-    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    if (runs)
-        hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
-                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, (const int32_t *)nullptr);
-    else
-        hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, grow, seg_off_d, n_seg,
-                           n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, (const int32_t *)nullptr);
+    terminal_launch(runs, gts, gfr, grow, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch,
+                    nullptr, st);
     e = hipGetLastError();
     (void)hipFreeAsync(tmp, st);
     if (e != hipSuccess) {
@@ -1297,15 +1348,8 @@ static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const
     FDX_REQUIRE(gfraud_d || rows_d, "fraud comes from gfraud_d or bit 31 of rows_d");
     FDX_REQUIRE(rec_d || (nb_d && risk_d), "no output");
     FDX_REQUIRE(!dest_map_d || rec_d, "dest_map_d places count records");
-    unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    if (runs)
-        hipLaunchKernelGGL(k_terminal_g<true>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
-                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d,
-                           dest_map_d);
-    else
-        hipLaunchKernelGGL(k_terminal_g<false>, dim3(grid), dim3(kTermBlock), 0, as_stream(stream), gts_d, gfraud_d,
-                           rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch_d,
-                           dest_map_d);
+    terminal_launch(runs != 0, gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d,
+                    rec_d, scratch_d, dest_map_d, as_stream(stream));
     FDX_LAUNCHED("k_terminal_g");
     return FDX_OK;
 }
@@ -1506,6 +1550,10 @@ extern "C" int fdx_customer_windows_scan(const int64_t *gts_d, const double *gam
 
 // A side stream (per device, created once) for launches that fork from the caller's stream
 // and join back before the call returns: the caller still sees one stream-ordered call.
+// Created at the HIGH priority level: HIP gives each priority level its own pool of
+// GPU_MAX_HW_QUEUES hardware queues, and a normal-priority stream created after torch's and
+// RCCL's was measured on the caller's own hardware queue (rocprofv3 Queue_Id) -- the two
+// walks then ran back to back.  FDX_FORK_PRIORITY=0 restores the normal level (A/B runs).
 struct ForkStream {
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -1517,7 +1565,11 @@ static int fork_stream(ForkStream **out) {
     FDX_REQUIRE(dev >= 0 && dev < 64, "device id out of range");
     ForkStream &f = per_dev[dev];
     if (!f.side) {
-        FDX_HIP(hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking));
+        int least = 0, greatest = 0;
+        FDX_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const char *e = getenv("FDX_FORK_PRIORITY");
+        const int prio = (e && atoi(e) == 0) ? 0 : greatest;
+        FDX_HIP(hipStreamCreateWithPriority(&f.side, hipStreamNonBlocking, prio));
         FDX_HIP(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming));
         FDX_HIP(hipEventCreateWithFlags(&f.join, hipEventDisableTiming));
     }

@@ -28,6 +28,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+import os
+
 from . import _lib, ops
 from .pipeline import _SCAN_DIRECT
 from ._lib import check
@@ -89,6 +91,13 @@ class GpuKernels:
 # written as batched isend/irecv in chunks of at most this many bytes: both ends of a pair
 # derive the same chunking from the same count, so no rank needs another's sizes.
 P2P_CHUNK_BYTES = 256 << 20
+
+# Priority of ShardedPipeline's exchange stream.  HIP hands a new stream one of
+# GPU_MAX_HW_QUEUES (4) hardware queues per priority level; after RCCL's and torch's own
+# streams the normal-priority side stream was measured on the SAME hardware queue as the
+# caller's stream (rocprofv3 Queue_Id), which serialises the exchange behind the customer
+# half.  A high-priority stream draws from a separate queue pool, so the two halves overlap.
+_SHARD_SIDE_PRIORITY = int(os.environ.get("FDX_SHARD_SIDE_PRIORITY", "-1"))
 
 
 def alltoallv(out, inp, out_splits, in_splits, group=None):
@@ -252,7 +261,7 @@ class ShardedPipeline:
         # two meet at the scoring-row assembly.
         main = torch.cuda.current_stream()
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=ts.device)
+            self._side = torch.cuda.Stream(device=ts.device, priority=_SHARD_SIDE_PRIORITY)
         side = self._side
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -260,15 +269,18 @@ class ShardedPipeline:
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
         cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        # the exchange's split-size sync waits only for the (short) owner re-key on the side
+        # stream; enqueueing the whole exchange before the layout's host sync keeps the side
+        # stream busy while the customer re-key runs
+        with torch.cuda.stream(side):
+            back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
+                                              self.n_terminals_total, p.windows_days, p.delay_days, self.group)
+            sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
         scan = p.avg_mode == "scan"
         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, None if (scan and _SCAN_DIRECT) else p.windows_days,
                                   grouped=True)  # (host sync on main)
         rc.check()
         p._slots_hint = lay.its.numel()
-        with torch.cuda.stream(side):
-            back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
-                                              self.n_terminals_total, p.windows_days, p.delay_days, self.group)
-            sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
         if scan:
             inb, isum = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days, lay=lay)
         else:
