@@ -236,6 +236,17 @@ int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfrau
                                       const int32_t *dest_map_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
                                       int64_t delay_ns, const int64_t *window_ns, int32_t n_windows, int32_t runs,
                                       int64_t *rec_d, int32_t *scratch_d, void *stream);
+/* fdx_terminal_windows_grouped (count records by row) in the COMPACT format, n_windows = 3:
+ * rec_d is int64[5 n], 16-byte aligned.  Words [2 r, 2 r + 2) hold row r's record as
+ * lo = NB_0 | NB_1 << 21 | NB_2 << 42, hi = FRAUD_0 | FRAUD_1 << 21 | FRAUD_2 << 42 -- one
+ * aligned 16-byte store (and load, FDX_PREP_TERM_COMPACT) per row instead of a 24-byte record
+ * across two.  A row with a window count above 2^21 - 1 instead gets lo = (1 << 63) | o,
+ * hi = 0, with its full 3-word record (NB | FRAUD << 32 per window) at rec_d[o], o = 2 n + 3 r
+ * (the overflow area [2 n, 5 n), written only for such rows).  Exact for any counts. */
+int fdx_terminal_windows_grouped_compact(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
+                                         const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
+                                         const int64_t *window_ns, int32_t n_windows, int32_t runs, int64_t *rec_d,
+                                         int32_t *scratch_d, void *stream);
 
 /* ---- a-4: re-key (stable radix sort by key + segment offsets) -------------------------
  * Replaces the regrouping done by pandas groupby('CUSTOMER_ID') / sort_values /
@@ -459,6 +470,8 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
 #define FDX_PREP_VAL_IS_SUM 1   /* cust_avg_d holds rolling sums: average = sum / nb here      */
 #define FDX_PREP_TERM_BY_SLOT 2 /* term_rec_d[i] is row i's record (fdx_terminal_windows_packed_
                                    dest with the slot map); term_inv_d is ignored           */
+#define FDX_PREP_TERM_COMPACT 4 /* term_rec_d holds COMPACT records (fdx_terminal_windows_
+                                   grouped_compact; n_windows = 3, 16-byte aligned)          */
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
                                int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                const int32_t *cust_nb_d, const double *cust_avg_d,

@@ -517,6 +517,8 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             bool nan = v[0] != v[0];
             const int64_t q_ = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
             const int64_t *rec = term_rec + q_ * W;
+            int64_t ctw[3] = {0, 0, 0};
+            if (val_is_sum & 4) compact_load(term_rec, q_, ctw);  // (W = 3, checked by the host)
 #pragma unroll
             for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
                 if (w < W) {
@@ -524,7 +526,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                     const double cv = cval[(int64_t)w * n + i];
                     count(3 + 2 * w, c);
                     v[4 + 2 * w] = zval((val_is_sum & 1) ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
-                    const int64_t tw = rec[w];
+                    const int64_t tw = (val_is_sum & 4) ? ctw[w < 3 ? w : 0] : rec[w];
                     const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
                     count(3 + 2 * W + 2 * w, tnb);
                     const int fr_ = 4 + 2 * W + 2 * w;
@@ -566,6 +568,8 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         bool nan = v[0] != v[0];
         const int64_t q = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
         const int64_t *rec = term_rec + q * W;
+        int64_t ctw[3] = {0, 0, 0};
+        if (val_is_sum & 4) compact_load(term_rec, q, ctw);  // (W = 3, checked by the host)
 #pragma unroll
         for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
             if (w < W) {
@@ -573,7 +577,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
                 const double cv = cval[(int64_t)w * n + i];
                 v[3 + 2 * w] = zval((double)c, mean, scale, 3 + 2 * w);
                 v[4 + 2 * w] = zval((val_is_sum & 1) ? cv / (double)c : cv, mean, scale, 4 + 2 * w);
-                const int64_t tw = rec[w];
+                const int64_t tw = (val_is_sum & 4) ? ctw[w < 3 ? w : 0] : rec[w];
                 v[3 + 2 * W + 2 * w] = zval((double)term_nb(tw), mean, scale, 3 + 2 * W + 2 * w);
                 v[4 + 2 * W + 2 * w] = zval(term_risk(tw), mean, scale, 4 + 2 * W + 2 * w);
                 nan |= (v[4 + 2 * w] != v[4 + 2 * w]) | (v[4 + 2 * W + 2 * w] != v[4 + 2 * W + 2 * w]);
@@ -630,7 +634,9 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
         }
         const int64_t q_ = (val_is_sum & 2) ? j : (term_inv ? term_inv[r] : r);
         const int64_t *src = term_rec + q_ * W;
-        if (rec16) {  // the 24-byte record in two loads (16-byte aligned pair first or second)
+        if (val_is_sum & 4) {
+            compact_load(term_rec, q_, L.tw);
+        } else if (rec16) {  // the 24-byte record in two loads (16-byte aligned pair first or second)
             if ((q_ & 1) == 0) {
                 const longlong2 p = *reinterpret_cast<const longlong2 *>(src);
                 L.tw[0] = p.x;
@@ -2779,6 +2785,8 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                 3 + 4 * n_windows);
     if (n == 0) return FDX_OK;
     FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && term_rec_d, "null pointer");
+    FDX_REQUIRE(!(cust_val_is_sum & 4) || (n_windows == 3 && ((uintptr_t)term_rec_d & 15) == 0),
+                "compact terminal records: W = 3 and a 16-byte aligned record array");
     float *z;
     double *acc;
     int32_t *flag;

@@ -56,6 +56,28 @@ __device__ __forceinline__ double term_risk(int64_t w) {
     return nb > 0 ? (double)fr / (double)nb : 0.0;
 }
 
+// COMPACT count records (fdx_terminal_windows_grouped_compact, W = 3): 16 bytes per row,
+// lo = NB_0 | NB_1 << 21 | NB_2 << 42, hi = FRAUD_0 | FRAUD_1 << 21 | FRAUD_2 << 42 (one
+// aligned 16-byte access instead of a 24-byte record over two).  A row whose window count
+// does not fit 21 bits has bit 63 of lo set and the low 63 bits = the word offset, from the
+// start of the record array, of its full 3-word record (the array's overflow area).
+constexpr int kCompactBits = 21;
+constexpr int64_t kCompactMax = (1LL << kCompactBits) - 1;
+__device__ __forceinline__ void compact_load(const int64_t *rec, int64_t q, int64_t (&tw)[3]) {
+    const longlong2 p = *reinterpret_cast<const longlong2 *>(rec + 2 * q);
+    if (p.x < 0) {
+        const int64_t *wide = rec + (p.x & INT64_MAX);
+        tw[0] = wide[0];
+        tw[1] = wide[1];
+        tw[2] = wide[2];
+    } else {
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+            tw[w] = term_word((int32_t)((p.x >> (kCompactBits * w)) & kCompactMax),
+                              (int32_t)((p.y >> (kCompactBits * w)) & kCompactMax));
+    }
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t round_up(size_t a, size_t m) { return (a + m - 1) / m * m; }
 

@@ -288,6 +288,155 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     }
 }
 
+// The same stable scatter with a BLOCKED tile: wave w owns the 1,024 consecutive input
+// positions [w * 1024, (w + 1) * 1024) of the tile (item r of lane l at w * 1024 + r * 64 + l,
+// still coalesced loads).  Input order inside the tile is then (wave, item, lane), so each
+// wave ranks its 16 items against wave-private digit counters (ballot multisplit; the leader
+// lane of each digit group bumps the counter) with no block barrier, and one barrier later the
+// per-digit scan over the four waves' counts gives each wave its offset: 3 barriers per tile
+// instead of 3 per item.  The tile's global digit offsets are staged in LDS once.
+template <typename K, int BITS, int PW>
+__global__ void __launch_bounds__(kBlock) k_radix_scatter_b(
+    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
+    int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out, const uint8_t *__restrict__ flag_in, const uint64_t *__restrict__ p0_in,
+    const uint64_t *__restrict__ p1_in, uint64_t *__restrict__ p0_out, uint64_t *__restrict__ p1_out) {
+    constexpr int kBins = 1 << BITS, kPer = kBins / kBlock;
+    static_assert(kBins % kBlock == 0, "digit bins must be a multiple of the block");
+    constexpr int kWaveSpan = kTile / kWavesPerBlock;  // 1,024 input positions per wave
+    __shared__ uint32_t s_cnt[kWavesPerBlock][kBins];  // wave-private counts, then wave offsets
+    __shared__ int32_t s_goff[kBins];                  // global destination of tile position 0 per digit
+    constexpr int kKeyWords = (int)(sizeof(K) / 4);
+    __shared__ __align__(16) uint32_t s_kv[(kKeyWords + 1) * kTile];
+    K *s_key = reinterpret_cast<K *>(s_kv);
+    uint32_t *s_val = s_kv + kKeyWords * kTile;
+
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int64_t wbase = base + (int64_t)wv * kWaveSpan + lane;  // + r * 64: item r of this lane
+    for (int d = tid; d < kBins; d += kBlock)
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) s_cnt[w][d] = 0;
+    __syncthreads();
+
+    K key[kItems];
+    uint32_t val[kItems], rank[kItems], dig[kItems];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t *cnt = s_cnt[wv];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = wbase + (int64_t)r * kWave;
+        const bool valid = i < n;
+        key[r] = valid ? keys_in[i] : (K)0;
+        val[r] = valid ? (vals_in ? vals_in[i] : ((uint32_t)i | (flag_in && flag_in[i] ? 0x80000000u : 0u))) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = wbase + (int64_t)r * kWave;
+        const bool valid = i < n;
+        const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
+        dig[r] = d;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < BITS; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t in_wave = (uint32_t)__popcll(peers & lt_mask);
+        const uint32_t old = valid ? cnt[d] : 0u;
+        // every lane's read of the counter before the leader's update (LDS ops of a wave
+        // execute in order; the fences keep the compiler from moving them)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && in_wave == 0) cnt[d] = old + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        rank[r] = old + in_wave;
+    }
+    __syncthreads();
+    // per digit: tile start (exclusive scan over digits of the tile totals), each wave's offset
+    // (tile start + the counts of the earlier waves) and the global destination of position 0
+    {
+        uint32_t c[kPer][kWavesPerBlock], tot_d[kPer], sum = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            tot_d[q] = 0;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                c[q][w] = s_cnt[w][tid * kPer + q];
+                tot_d[q] += c[q][w];
+            }
+            sum += tot_d[q];
+        }
+        uint32_t tot;
+        uint32_t ex = block_excl_scan(sum, &tot);  // (its own barriers: every s_cnt read above is done)
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int d = tid * kPer + q;
+            uint32_t o = ex;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                s_cnt[w][d] = o;
+                o += c[q][w];
+            }
+            s_goff[d] = (int32_t)offsets[(int64_t)d * n_tiles + blockIdx.x] - (int32_t)ex;
+            ex += tot_d[q];
+        }
+    }
+    __syncthreads();
+    uint32_t pos[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        if (wbase + (int64_t)r * kWave < n) {
+            const uint32_t p = cnt[dig[r]] + rank[r];
+            pos[r] = p;
+            s_key[p] = key[r];
+            s_val[p] = val[r];
+        }
+    }
+    __syncthreads();
+    const int64_t tcnt = std::min<int64_t>(kTile, n - base);
+    int32_t dsts[kItems];  // destination of tile position tid + j * kBlock
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int p = tid + j * kBlock;
+        if (p < tcnt) {
+            const K k = s_key[p];
+            const int32_t dst = s_goff[digit_of<K, BITS>(k, shift, flip)] + p;
+            dsts[j] = dst;
+            keys_out[dst] = k;
+            vals_out[dst] = s_val[p];
+        }
+    }
+    if constexpr (PW > 0) {
+        uint64_t *s_pay = reinterpret_cast<uint64_t *>(s_kv);
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+            const uint64_t *pin = q == 0 ? p0_in : p1_in;
+            uint64_t *pout = q == 0 ? p0_out : p1_out;
+            uint64_t v[kItems];
+#pragma unroll
+            for (int r = 0; r < kItems; ++r) {  // coalesced, input order
+                const int64_t i = wbase + (int64_t)r * kWave;
+                v[r] = i < n ? pin[i] : 0ull;
+            }
+            __syncthreads();  // the previous contents of the LDS slots are consumed
+#pragma unroll
+            for (int r = 0; r < kItems; ++r)
+                if (wbase + (int64_t)r * kWave < n) s_pay[pos[r]] = v[r];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const int p = tid + j * kBlock;
+                if (p < tcnt) pout[dsts[j]] = s_pay[p];
+            }
+        }
+    }
+}
+
 __global__ void k_iota(uint32_t *__restrict__ out, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -380,8 +529,18 @@ template <typename K, int BITS, int PW>
 void launch_scatter(const K *kin, const uint32_t *vin, int64_t n, int shift, K flip, int64_t tiles,
                     const uint32_t *hist, K *kout, uint32_t *vout, const uint8_t *flag_in, const uint64_t *const (&pin)[2],
                     uint64_t *const (&pout)[2], hipStream_t st) {
-    hipLaunchKernelGGL((k_radix_scatter<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n, shift,
-                       flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
+    // A/B switch: FDX_RADIX_BLOCKED=1 selects the blocked-tile scatter (k_radix_scatter_b; not yet
+    // validated on the GPU -- the default stays the per-item-ranking kernel until it is)
+    static const bool blocked = [] {
+        const char *e = getenv("FDX_RADIX_BLOCKED");
+        return e && atoi(e) != 0;
+    }();
+    if (!blocked)
+        hipLaunchKernelGGL((k_radix_scatter<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
+                           shift, flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
+    else
+        hipLaunchKernelGGL((k_radix_scatter_b<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
+                           shift, flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
 }
 
 template <typename K>

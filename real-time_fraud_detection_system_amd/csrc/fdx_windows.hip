@@ -895,7 +895,8 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
     int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
-    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap, int64_t len_lo, int64_t len_hi) {
+    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap, int64_t len_lo, int64_t len_hi,
+    int64_t compact_n) {
     static_assert(LR % kWave == 0 && LR <= 32768, "the merge packs a staging index in 15 bits");
     constexpr int kMaxRunsLong = 2 * LR - 1;  // a long segment's run list in the stage's ts words
     __shared__ int64_t s_ts[kTermWaves][LR];
@@ -1036,31 +1037,17 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
             const int64_t qi = merged ? (int64_t)(s_q[RUNS ? wv : 0][i] & 0x7FFF) : i;
             const int64_t row = dest_of(b + qi);
             int32_t nbh = 0, frh = 0;
+            int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
             if (!RUNS || nruns == 1 || merged) {
                 const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
                 nbh = (int32_t)hi;
                 frh = F(hi);
-                if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
-                    // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
-                    // 16-byte alignment) instead of three: fewer random write transactions
-                    int64_t wd[3];
 #pragma unroll
-                    for (int w = 0; w < 3; ++w) {
+                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                    if (w < n_win) {
                         const int64_t lo = ub(0, hi, t - delay - win.w[w]);
-                        wd[w] = term_word((int32_t)(hi - lo), frh - F(lo));
-                    }
-                    int64_t *dst = rec_out + row * 3;
-                    if ((row & 1) == 0) {
-                        *reinterpret_cast<longlong2 *>(dst) = make_longlong2(wd[0], wd[1]);
-                        dst[2] = wd[2];
-                    } else {
-                        dst[0] = wd[0];
-                        *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(wd[1], wd[2]);
-                    }
-                } else {
-                    for (int w = 0; w < n_win; ++w) {
-                        const int64_t lo = ub(0, hi, t - delay - win.w[w]);
-                        term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, (int32_t)(hi - lo), frh - F(lo));
+                        cn[w] = (int32_t)(hi - lo);
+                        cf[w] = frh - F(lo);
                     }
                 }
             } else if (nruns <= max_runs) {
@@ -1069,14 +1056,18 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                     nbh += (int32_t)(h - lr[r]);
                     frh += F(h) - F(lr[r]);
                 }
-                for (int w = 0; w < n_win; ++w) {
-                    int32_t nbl = 0, frl = 0;
-                    for (int r = 0; r < nruns; ++r) {
-                        const int64_t lo = ub(lr[r], lr[r + 1], t - delay - win.w[w]);
-                        nbl += (int32_t)(lo - lr[r]);
-                        frl += F(lo) - F(lr[r]);
+#pragma unroll
+                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                    if (w < n_win) {
+                        int32_t nbl = 0, frl = 0;
+                        for (int r = 0; r < nruns; ++r) {
+                            const int64_t lo = ub(lr[r], lr[r + 1], t - delay - win.w[w]);
+                            nbl += (int32_t)(lo - lr[r]);
+                            frl += F(lo) - F(lr[r]);
+                        }
+                        cn[w] = nbh - nbl;
+                        cf[w] = frh - frl;
                     }
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl, frh - frl);
                 }
             } else {  // more unsorted runs than the run list holds: count directly (any order)
                 int32_t nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
@@ -1092,8 +1083,41 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                             frl[w] += fj;
                         }
                 }
+#pragma unroll
+                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                    cn[w] = nbh - nbl[w];
+                    cf[w] = frh - frl[w];
+                }
+            }
+            if (compact_n > 0) {  // W = 3 compact record (+ the full record in the overflow area)
+                const bool fits = cn[0] <= kCompactMax && cn[1] <= kCompactMax && cn[2] <= kCompactMax;
+                int64_t lo, hi;
+                if (fits) {
+                    lo = (int64_t)cn[0] | ((int64_t)cn[1] << kCompactBits) | ((int64_t)cn[2] << (2 * kCompactBits));
+                    hi = (int64_t)cf[0] | ((int64_t)cf[1] << kCompactBits) | ((int64_t)cf[2] << (2 * kCompactBits));
+                } else {
+                    const int64_t off = 2 * compact_n + 3 * row;
+#pragma unroll
+                    for (int w = 0; w < 3; ++w) rec_out[off + w] = term_word(cn[w], cf[w]);
+                    lo = off | INT64_MIN;
+                    hi = 0;
+                }
+                *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
+            } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
+                // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
+                // 16-byte alignment) instead of three: fewer random write transactions
+                int64_t *dst = rec_out + row * 3;
+                const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
+                if ((row & 1) == 0) {
+                    *reinterpret_cast<longlong2 *>(dst) = make_longlong2(w0, w1);
+                    dst[2] = w2;
+                } else {
+                    dst[0] = w0;
+                    *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(w1, w2);
+                }
+            } else {
                 for (int w = 0; w < n_win; ++w)
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + i, row, w, nbh - nbl[w], frh - frl[w]);
+                    term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, cn[w], cf[w]);
             }
         }
         wave_sync();
@@ -1188,7 +1212,7 @@ extern "C" int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount
 static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, const int32_t *rows,
                             const int64_t *seg_off, int64_t n_seg, int64_t n, int64_t delay_ns, const WinArgs &wa,
                             int32_t n_windows, int32_t *nb_d, double *risk_d, int64_t *rec_d, int32_t *scratch,
-                            const int32_t *dmap, hipStream_t st) {
+                            const int32_t *dmap, hipStream_t st, int64_t compact_n = 0) {
     static const bool split = [] {
         const char *e = getenv("FDX_TERM_SPLIT");
         return !(e && atoi(e) == 0);
@@ -1197,7 +1221,8 @@ static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, c
     const int64_t lo = split ? kTermShortRows : 0, inf = INT64_MAX;
 #define FDX_TERM_LAUNCH(R, LRV, A, B)                                                                           \
     hipLaunchKernelGGL((k_terminal_g<R, LRV>), dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off, n_seg, \
-                       n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, dmap, (int64_t)(A), (int64_t)(B))
+                       n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, dmap, (int64_t)(A), (int64_t)(B), \
+                       compact_n)
     if (runs) {
         if (split) FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
@@ -1337,7 +1362,8 @@ extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, cons
 static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
                             const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
                             const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d, double *risk_d,
-                            int64_t *rec_d, int32_t *scratch_d, const int32_t *dest_map_d, void *stream) {
+                            int64_t *rec_d, int32_t *scratch_d, const int32_t *dest_map_d, void *stream,
+                            bool compact = false) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -1348,8 +1374,10 @@ static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const
     FDX_REQUIRE(gfraud_d || rows_d, "fraud comes from gfraud_d or bit 31 of rows_d");
     FDX_REQUIRE(rec_d || (nb_d && risk_d), "no output");
     FDX_REQUIRE(!dest_map_d || rec_d, "dest_map_d places count records");
+    FDX_REQUIRE(!compact || (rec_d && n_windows == 3 && !dest_map_d && ((uintptr_t)rec_d & 15) == 0),
+                "compact records: W = 3, a 16-byte aligned record array, records by row");
     terminal_launch(runs != 0, gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d,
-                    rec_d, scratch_d, dest_map_d, as_stream(stream));
+                    rec_d, scratch_d, dest_map_d, as_stream(stream), compact ? n : 0);
     FDX_LAUNCHED("k_terminal_g");
     return FDX_OK;
 }
@@ -1360,6 +1388,15 @@ extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t 
                                             double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream) {
     return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs, nb_d,
                             risk_d, rec_d, scratch_d, nullptr, stream);
+}
+
+extern "C" int fdx_terminal_windows_grouped_compact(const int64_t *gts_d, const uint8_t *gfraud_d,
+                                                    const int32_t *rows_d, const int64_t *seg_off_d, int64_t n_seg,
+                                                    int64_t n, int64_t delay_ns, const int64_t *window_ns,
+                                                    int32_t n_windows, int32_t runs, int64_t *rec_d,
+                                                    int32_t *scratch_d, void *stream) {
+    return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs,
+                            nullptr, nullptr, rec_d, scratch_d, nullptr, stream, true);
 }
 
 extern "C" int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfraud_d,

@@ -97,6 +97,8 @@ SIGNATURES = {
     "fdx_terminal_windows_grouped": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P, P, P, P]),
     "fdx_terminal_windows_grouped_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
                                                          P]),
+    "fdx_terminal_windows_grouped_compact": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
+                                                            P]),
     "fdx_customer_layout_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, P, P, P, P, c_i64, P, P,
                                                           c_sz, P]),
     "fdx_customer_layout_grouped": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),

@@ -386,6 +386,46 @@ def terminal_windows_grouped_dest(gts, seg_off, rows, dest_map, n_out: int, gfra
     return rec
 
 
+def terminal_windows_compact(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
+                             runs: bool = False, stream=None):
+    """terminal_windows_grouped's count records by row in the COMPACT format (3 windows): an
+    int64 [5 n] array, row r's 16-byte record at words [2 r, 2 r + 2), the overflow area
+    [2 n, 5 n) (fdx.h fdx_terminal_windows_grouped_compact).  compact_records_unpack turns it
+    into the [n, 3] records."""
+    _dev(gts, torch.int64, "gts"); _dev(seg_off, torch.int64, "seg_off")
+    if rows is not None:
+        _dev(rows, torch.int32, "rows")
+    if gfraud is not None:
+        _dev(gfraud, torch.uint8, "gfraud")
+    if rows is None and gfraud is None:
+        raise FdxError("fraud comes from gfraud or from bit 31 of rows")
+    if len(windows_days) != 3:
+        raise FdxError("compact records hold 3 windows")
+    n = gts.numel()
+    rec = torch.empty(max(5 * n, 2), dtype=torch.int64, device=gts.device)  # 256-byte aligned
+    scratch = torch.empty(max(n, 1), dtype=torch.int32, device=gts.device)
+    check(_lib.load().fdx_terminal_windows_grouped_compact(_ptr(gts), _ptr(gfraud), _ptr(rows), _ptr(seg_off),
+                                                           seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
+                                                           _win_ns(windows_days), 3, int(bool(runs)), _ptr(rec),
+                                                           _ptr(scratch), _s(stream)),
+          "fdx_terminal_windows_grouped_compact")
+    return rec
+
+
+def compact_records_unpack(rec: torch.Tensor, n: int) -> torch.Tensor:
+    """terminal_windows_compact's array -> the [n, 3] int64 count records (NB | FRAUD << 32),
+    with torch ops (tests and inspection; the scoring path reads the compact form itself)."""
+    pair = rec[: 2 * n].view(n, 2)
+    lo, hi = pair[:, 0], pair[:, 1]
+    m = (1 << 21) - 1
+    out = torch.stack([((lo >> (21 * w)) & m) | (((hi >> (21 * w)) & m) << 32) for w in range(3)], dim=1)
+    esc = lo < 0
+    if bool(esc.any()):
+        off = (lo[esc] & ((1 << 63) - 1)).long()
+        out[esc] = torch.stack([rec[off + w] for w in range(3)], dim=1)
+    return out
+
+
 def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
                              runs: bool = False, records: bool = True, stream=None):
     """Terminal windows over grouped inputs (rekey_payload(terminal, ts, flag=fraud) outputs):
@@ -600,12 +640,14 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_by_slot: bool = False):
+                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_by_slot: bool = False,
+                           term_compact: bool = False):
     """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
-    term_by_slot: term_rec[i] is scoring row i's record (terminal_windows_packed_dest)."""
+    term_by_slot: term_rec[i] is scoring row i's record (terminal_windows_packed_dest);
+    term_compact: term_rec is terminal_windows_compact's array."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
-    opts = (1 if val_is_sum else 0) | (2 if term_by_slot else 0)
+    opts = (1 if val_is_sum else 0) | (2 if term_by_slot else 0) | (4 if term_compact else 0)
     check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
                                                  _ptr(camt), _ptr(cnb),
                                                  _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),

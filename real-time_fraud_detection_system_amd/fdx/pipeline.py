@@ -49,6 +49,9 @@ _CU_SPLIT = os.environ.get("FDX_CU_SPLIT", "")  # "k/8": side stream on the CUs 
 # terminal records written at their scoring slots (the row assembly then reads them in slot
 # order); the terminal windows wait for the customer layout
 _TERM_SLOTS = os.environ.get("FDX_TERM_SLOTS", "0") != "0"
+# terminal count records in the compact 16-byte format (one aligned store / load per row);
+# opt-in until it is measured and validated on the GPU
+_TERM_COMPACT = os.environ.get("FDX_TERM_COMPACT", "0") != "0"
 
 
 def _masked_stream(device, eighths: int):
@@ -181,6 +184,7 @@ class FraudPipeline:
         # Allocated under the side stream's context, so that the caching allocator hands
         # these buffers to nothing on the main stream while the side stream still uses them.
         by_slot = _TERM_SLOTS and _TERM_PAYLOAD
+        compact = _TERM_COMPACT and _TERM_PAYLOAD and not by_slot and W == 3
         with torch.cuda.stream(side):
             mk("start", side)
             if by_slot:  # the windows come after the customer layout (below)
@@ -189,8 +193,12 @@ class FraudPipeline:
             elif _TERM_PAYLOAD:
                 tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
                 mk("rekey_terminal", side)
-                trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                    windows_days=self.windows_days, stream=side)
+                if compact:
+                    trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                        windows_days=self.windows_days, stream=side)
+                else:
+                    trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                        windows_days=self.windows_days, stream=side)
             else:  # round-1 form: plain re-key, the kernel gathers ts / fraud through the perm
                 tperm, tseg, _ = ops.rekey(terminal, n_terminals, side)
                 mk("rekey_terminal", side)
@@ -234,7 +242,8 @@ class FraudPipeline:
         trec.record_stream(main)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                   ws, main, n=lay.n_slots, val_is_sum=True, term_by_slot=by_slot)
+                                   ws, main, n=lay.n_slots, val_is_sum=True, term_by_slot=by_slot,
+                                   term_compact=compact)
         mk("assemble_rows", main)
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
         mk("forest_traverse", main)

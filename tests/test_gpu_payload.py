@@ -167,3 +167,59 @@ def test_terminal_records_at_scoring_slots(dev, monkeypatch):
     p_slot = torch.empty(n, dtype=torch.float64, device=dev)
     FraudPipeline(forest=forest).run_fused(*args, 3000, 6000, p_slot, ws)
     assert torch.equal(p_row, p_slot)
+
+
+def test_compact_records_equal_full_records(dev):
+    """fdx_terminal_windows_grouped_compact: the 16-byte records unpack to the full count
+    records (oracle), for the sorted single-run form and the multi-run owner form."""
+    rng = np.random.default_rng(33)
+    ts, term, fraud = _hot_table(rng)
+    ref = _oracle_records(ts, fraud, term, 40)
+    perm, seg, gts, _ = ops.rekey_payload(T(term, torch.int32, dev), 40, T(ts, torch.int64, dev),
+                                          flag=T(fraud, torch.uint8, dev))
+    rec = ops.terminal_windows_compact(gts, seg, rows=perm)
+    assert rec.numel() == 5 * len(ts)
+    assert not bool((rec[: 2 * len(ts)].view(-1, 2)[:, 0] < 0).any())  # everything fits 21 bits
+    np.testing.assert_array_equal(ops.compact_records_unpack(rec, len(ts)).cpu().numpy(), ref)
+    src = rng.integers(0, 8, len(ts))
+    order = np.argsort(src, kind="stable")
+    perm, seg, gts, _ = ops.rekey_payload(T(term[order], torch.int32, dev), 40, T(ts[order], torch.int64, dev),
+                                          flag=T(fraud[order], torch.uint8, dev))
+    rec = ops.terminal_windows_compact(gts, seg, rows=perm, runs=True)
+    np.testing.assert_array_equal(ops.compact_records_unpack(rec, len(ts)).cpu().numpy(), ref[order])
+
+
+def test_compact_records_overflow_rows(dev, golden, monkeypatch):
+    """Window counts above 2^21 - 1 (one terminal with 2.2M rows in one day, then later rows
+    whose delayed windows hold all of them): those rows escape to full records in the overflow
+    area -- exact; the run_fused row assembly reads both kinds."""
+    n_hot, n_late = 2_200_000, 300
+    rng = np.random.default_rng(44)
+    # late rows at 7.6 days: their 1-day delayed window (6.6, 7.6] days back covers every hot row
+    ts = np.concatenate([np.sort(rng.integers(0, DAY // 2, n_hot)), 7 * DAY + 6 * DAY // 10 + np.arange(n_late) * 10**9])
+    ts = ts.astype(np.int64)
+    term = np.zeros(len(ts), np.int32)
+    term[rng.random(len(ts)) < 0.001] = 1  # a second, small terminal
+    fraud = (rng.random(len(ts)) < 0.01).astype(np.uint8)
+    tsd, termd, frd = T(ts, torch.int64, dev), T(term, torch.int32, dev), T(fraud, torch.uint8, dev)
+    perm, seg, gts, _ = ops.rekey_payload(termd, 2, tsd, flag=frd)
+    full = ops.terminal_windows_grouped(gts, seg, rows=perm)
+    rec = ops.terminal_windows_compact(gts, seg, rows=perm)
+    n = len(ts)
+    esc = (rec[: 2 * n].view(n, 2)[:, 0] < 0).cpu().numpy()
+    assert esc.sum() > 0 and esc[:n_hot].sum() == 0
+    assert torch.equal(ops.compact_records_unpack(rec, n), full)
+    assert int((full[:, 0] & 0xFFFFFFFF).max()) > (1 << 21)
+    z = golden("forest_rf5d8.npz")
+    arrays = {k: z[k] for k in ("left", "right", "feature", "threshold", "missing_left", "value1", "node_offsets")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    cust = T(rng.integers(0, 100, n).astype(np.int32), torch.int32, dev)
+    amt = T(np.round(rng.uniform(1, 300, n), 2), torch.float64, dev)
+    pipe = FraudPipeline(forest=forest)
+    _, p64 = pipe.run(tsd, cust, termd, amt, frd, 100, 2)
+    from fdx import pipeline
+
+    monkeypatch.setattr(pipeline, "_TERM_COMPACT", True)  # the fused path on compact records
+    proba = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(tsd, cust, termd, amt, frd, 100, 2, proba)
+    assert torch.equal(proba, p64)
