@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FDX_ABI_VERSION 1
+#define FDX_ABI_VERSION 2
 
 #define FDX_OK 0
 #define FDX_E_INVALID (-1)     /* bad argument (null pointer, size, unsupported shape) */
@@ -161,10 +161,15 @@ int fdx_customer_windows_interleaved(const int64_t *its_d, const double *iamt_d,
  * `groupby('TERMINAL_ID').apply(...)` (:2435), for all segments at once.
  *   nb_d[w*n+i]   = #rows of the segment with t in (t_i - delay - w, t_i - delay]
  *   risk_d[w*n+i] = (#fraud rows in that window) / nb, or 0.0 when nb == 0 (fillna(0))
- * fraud_d: 0/1 bytes. */
+ * fraud_d: 0/1 bytes.  Rows grouped by segment (seg_off_d), time order inside each segment
+ * (fdx_rekey of a time-ordered table; fdx_argsort_i64 first otherwise).  workspace_d: caller
+ * device memory of at least fdx_terminal_windows_workspace_size(n) bytes (the prefix fraud
+ * counts of segments longer than the kernel's 1,024-row LDS stage); the call allocates nothing. */
+size_t fdx_terminal_windows_workspace_size(int64_t n);
 int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int64_t *seg_off_d,
                          int64_t n_seg, int64_t n, int64_t delay_ns, const int64_t *window_ns,
-                         int32_t n_windows, int32_t *nb_d, double *risk_d, void *stream);
+                         int32_t n_windows, int32_t *nb_d, double *risk_d, void *workspace_d,
+                         size_t workspace_bytes, void *stream);
 
 /* Assemble the 15-feature scoring matrix in the column order of `input_features`
  * (model_training.ipynb:457-463 = pyspark/scripts/fraud_detection.py:126-132):
@@ -182,46 +187,14 @@ int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
                           const int32_t *term_nb_d, const double *term_risk_d, double *X_d, int64_t ld,
                           void *stream);
 
-/* Same windows as fdx_terminal_windows, as one COUNT RECORD per row: n_windows int64 words,
- * word w = NB_w | FRAUD_w << 32 (both uint32; RISK_w = NB_w > 0 ? (double)FRAUD_w / NB_w : 0,
- * the same IEEE division fdx_terminal_windows does).  The consumers (fdx_forest_prepare_grouped,
- * fdx_forest_prepare_reply, fdx_reply_assemble) do that division.
- * row_d == NULL: ts/fraud are in grouped order and record q is rec_d[q].
- * row_d != NULL: grouped position q is input row row_d[q] (the re-key perm): ts/fraud are
- * read as ts[row_d[q]] and the record is written to rec_d[row_d[q]] -- records come out in
- * input row order with no separate gather/invert pass.  rec_d: [ts rows][n_windows] int64. */
-int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
-                                const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                                const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
-                                void *stream);
-
-/* Same records, written to rec_d[dest_d[row]] instead of rec_d[row] (dest_d: input row ->
- * output position, e.g. fdx_invert_slots of the interleaved customer layout, so that the
- * terminal half of a scoring row sits at its slot and fdx_forest_prepare_grouped reads it
- * sequentially: FDX_PREP_TERM_BY_SLOT).  rec_d: [max dest + 1][n_windows]. */
-int fdx_terminal_windows_packed_dest(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
-                                     const int32_t *dest_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
-                                     int64_t delay_ns, const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
-                                     void *stream);
-/* slot_of_d[irow_d[s]] = s for every slot s < n_slots with 0 <= irow_d[s] < n_rows (inverse of
- * the interleaved layout's slot -> row map; padding slots are skipped). */
-int fdx_invert_slots(const int32_t *irow_d, int64_t n_slots, int32_t *slot_of_d, int64_t n_rows, void *stream);
-
-/* Same records when the segments are NOT in time order (the multi-GPU owner side: a
- * terminal's rows arrive as one time-sorted run per source rank, so a stable re-key by
- * terminal gives segments of concatenated runs).  Each segment is time-sorted inside the
- * kernel (LDS bitonic sort; direct O(L^2) counts past 1024 rows) -- no global time sort.
- * The features are tie-order independent, so the records equal the sorted-input ones. */
-int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
-                                         const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                                         const int64_t *window_ns, int32_t n_windows, int64_t *rec_d,
-                                         void *stream);
-
 /* The terminal windows over GROUPED inputs (the scoring pipeline's form): gts_d[q] = ts of
  * grouped position q (fdx_rekey_payload output); fraud of q = gfraud_d[q], or bit 31 of
  * rows_d[q] when gfraud_d is NULL (fdx_rekey_payload's packed flag); rows_d[q] & 0x7FFFFFFF =
- * the row whose record is written (NULL: q).  Output: count records rec_d[row][n_windows] (as
- * fdx_terminal_windows_packed) or, when rec_d is NULL, nb_d / risk_d [w*n + q].  runs != 0:
+ * the row whose record is written (NULL: q).  Output: COUNT RECORDS rec_d[row][n_windows] --
+ * word w = NB_w | FRAUD_w << 32 (both uint32; RISK_w = NB_w > 0 ? (double)FRAUD_w / NB_w : 0,
+ * the IEEE division fdx_terminal_windows does; the consumers fdx_forest_prepare_grouped,
+ * fdx_forest_prepare_reply and fdx_reply_assemble divide) -- or, when rec_d is NULL,
+ * nb_d / risk_d [w*n + q].  runs != 0:
  * segments are concatenations of time-sorted runs (multi-GPU owner side).  scratch_d: int32[n]
  * (prefix fraud counts of segments longer than the kernel's LDS stage, 1,024 rows; such
  * segments cost O(L log L)). */
@@ -229,13 +202,6 @@ int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, 
                                  const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
                                  const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
                                  double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream);
-/* fdx_terminal_windows_grouped writing the count record of row r at rec_d[dest_map_d[r]]
- * (e.g. the row's scoring slot from fdx_invert_slots, so the row assembly reads the records
- * in slot order -- sequential -- instead of by row). */
-int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
-                                      const int32_t *dest_map_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
-                                      int64_t delay_ns, const int64_t *window_ns, int32_t n_windows, int32_t runs,
-                                      int64_t *rec_d, int32_t *scratch_d, void *stream);
 /* fdx_terminal_windows_grouped (count records by row) in the COMPACT format, n_windows = 3:
  * rec_d is int64[5 n], 16-byte aligned.  Words [2 r, 2 r + 2) hold row r's record as
  * lo = NB_0 | NB_1 << 21 | NB_2 << 42, hi = FRAUD_0 | FRAUD_1 << 21 | FRAUD_2 << 42 -- one
@@ -299,11 +265,11 @@ int fdx_scatter(const void *src_d, int32_t elem_bytes, const int32_t *perm_d, in
  * Rows are sharded by customer; the terminal windows need every row of a terminal on its
  * owner rank, owner(t) = t % world.  Per step: fdx_key_map(MOD) -> fdx_rekey(owner) ->
  * fdx_exchange_pack -> RCCL all-to-all (16 B/row) -> fdx_exchange_unpack (local terminal
- * id = t / world) -> fdx_rekey -> fdx_terminal_windows_packed_unsorted with row_d = the
- * grouped -> receive-position perm (count records indexed by receive position) -> RCCL
- * all-to-all back -> fdx_forest_prepare_grouped / fdx_reply_assemble.
+ * id = t / world) -> fdx_rekey_payload (ts payload, fraud flag) -> fdx_terminal_windows_grouped
+ * with runs = 1 (a segment = one time-sorted run per source rank; count records indexed by
+ * receive position) -> RCCL all-to-all back -> fdx_forest_prepare_grouped / fdx_reply_assemble.
  * Record layouts: exchange rec[j] = {ts, term<<32 | fraud<<31 | source row}; reply rows
- * are the count records of fdx_terminal_windows_packed (n_windows words). */
+ * are count records (n_windows words, fdx_terminal_windows_grouped). */
 #define FDX_KEY_MOD 0 /* out = key % param  (owner rank of a terminal)          */
 #define FDX_KEY_DIV 1 /* out = key / param  (owner-local terminal id)           */
 #define FDX_KEY_SUB 2 /* out = key - param  (shard-local customer id)           */
@@ -392,8 +358,8 @@ int fdx_forest_pack_rank2(const fdx_forest_desc *desc, int32_t version, uint32_t
                           double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out, int32_t *depth_out,
                           float *thr_out, int32_t *thr_off_out /* [33] */, int32_t *slot_feat_out /* [32] */,
                           int32_t *slot_base_out /* [32] */);
-/* *layout = 0 (wide 8-byte nodes), 1 (rank v1), 2 (rank v2) or 3 (rank v2 with one slot per
- * feature: v1 row format, compact 32 KiB row planes -- the default when the forest fits it);
+/* *layout = 0 (wide 8-byte nodes), 1 (rank v1, the default when the forest fits it), 2 (rank
+ * v2) or 3 (rank v2 with one slot per feature: v1 row format, compact 32 KiB row planes);
  * *n_slots = rank slots.  fdx_forest_set_variant rebuilds the rank layout in the other node
  * format when the requested variant needs it. */
 int fdx_forest_layout(fdx_forest forest, int32_t *layout, int32_t *n_slots);
@@ -414,26 +380,19 @@ int fdx_forest_predict(fdx_forest forest, const double *X_d, int64_t n, int64_t 
                        size_t workspace_bytes, void *stream);
 
 /* The two halves of fdx_forest_predict, for callers that time or overlap them:
- * prepare = scale + float32 cast into the workspace; traverse = the tree walk (one
- * k_forest_chunk launch per LDS-sized chunk of trees) reading that workspace. */
+ * prepare = scale + float32 cast (+ threshold ranks) into the workspace; traverse = the tree
+ * walk (one launch per LDS-sized chunk of trees) reading that workspace. */
 int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t row_stride,
                        int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
                         void *workspace_d, size_t workspace_bytes, void *stream);
-/* Rows per traversal slab (all chunks run over one slab before the next, so that the
- * per-chunk re-reads hit the Infinity Cache); 0 = default (env FDX_FOREST_SLAB_ROWS, else all rows in one slab). */
-int fdx_forest_set_slab_rows(fdx_forest forest, int64_t rows);
-/* Traversal kernel shape.  Wide layout (8-byte nodes, float32 rows): 0 = 512 threads x 1
- * row x 4 trees per lane, 1 = 1024 x 1 x 4, 2 = 512 x 2 x 4, 3 = 512 x 2 x 2, 4 = 256 x 2 x 4,
- * 5 = 1024 x 1 x 3, 6 = 512 x 1 x 3, 7 = 768 x 1 x 3, 8 = 768 x 1 x 4, 9 = 1024 x 1 x 2,
- * 10 = 768 x 1 x 2, 11 = 768 x 2 x 2, 12-15 = rows-resident tile kernels.  Rank layout
- * (4-byte nodes, u16 rank rows; see fdx_forest_pack_rank): 16 = 1024 x 1 x 4 (the default
- * when the forest fits the rank layout), 17 = 1024 x 1 x 2, 18 = 512 x 2 x 2,
- * 19 = 512 x 2 x 4, 20 = 1024 x 1 x 3, 21 = 768 x 1 x 4, 22 = 256 x 4 x 2, 23 = 1024 x 1 x 6,
- * ..., 41 = 1024 x 1 x 6 pipelined (v1); rank layout v2: 44 = 1024 x 1 x 6 (32 slots, the default
- * of forests needing more than one slot for a feature), 45 = 1024 x 1 x 4; v2 over compact 16-slot
- * planes: 46 = 1024 x 1 x 6 (the default when every feature fits one slot), 47 = 1024 x 1 x 8.
- * Variants > 0 need <= 16 features, 16+ need the rank layout (FDX_E_UNSUPPORTED otherwise).
+/* Traversal kernel shape (one per layout; 4-6 exist for the latency-hiding study of DESIGN.md §4):
+ *   0 = wide layout (8-byte nodes, float32 rows; any forest, the only one for > 15 features),
+ *   1 = rank layout v1, 1,024 threads x 6 trees per lane (the default when the forest fits v1),
+ *   2 = rank layout v2, 32 threshold slots (the default for forests v1 cannot hold),
+ *   3 = v2 nodes over 16 compact u16 planes (every feature in one slot),
+ *   4 / 5 / 6 = rank layout v1 with 8 / 10 / 12 trees per lane.
+ * Variants > 0 need <= 15 features and the rank layout (FDX_E_UNSUPPORTED otherwise).
  * Re-cuts the LDS chunks; results are identical for every variant.  The row format of a
  * prepared workspace depends on the layout: prepare again after switching layouts. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
@@ -459,17 +418,15 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
  * transaction r = cust_perm[i]; cust_ts/cust_amount/cust_nb/cust_avg are the customer-grouped
  * copies and outputs (flags are derived from cust_ts with flags_mode), the terminal half
  * is the count record term_rec[term_inv[r]] (term_inv may be NULL = identity: the
- * fdx_terminal_windows_packed output with row_d = the terminal perm is already in row
+ * fdx_terminal_windows_grouped output with rows_d = the terminal perm is already in row
  * order; the multi-GPU reply records need term_inv = inverse of the send perm).  Follow
  * with fdx_forest_traverse_perm(out_perm = cust_perm)
  * so that proba lands in row order.  The same call serves the interleaved customer layout
  * (cust_* = slot arrays, cust_perm = irow): slots with cust_perm < 0 are padding (zero
  * row, never written back).  cust_val_is_sum: FDX_PREP_* option bits (1 = cust_avg_d
- * holds rolling sums and the average is computed here as sum / nb; 2 = terminal records
- * by scoring row). */
+ * holds rolling sums and the average is computed here as sum / nb; 4 = compact terminal
+ * records). */
 #define FDX_PREP_VAL_IS_SUM 1   /* cust_avg_d holds rolling sums: average = sum / nb here      */
-#define FDX_PREP_TERM_BY_SLOT 2 /* term_rec_d[i] is row i's record (fdx_terminal_windows_packed_
-                                   dest with the slot map); term_inv_d is ignored           */
 #define FDX_PREP_TERM_COMPACT 4 /* term_rec_d holds COMPACT records (fdx_terminal_windows_
                                    grouped_compact; n_windows = 3, 16-byte aligned)          */
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
@@ -503,12 +460,26 @@ int fdx_segment_first_in_range(const int64_t *ts_d, const int32_t *perm_d, const
  *     in ns.  Any output may be NULL; *bad_d = 1 if a record has 0 or > 8 bytes.
  *   fdx_dedup_latest: ROW_NUMBER() OVER (PARTITION BY tx_id ORDER BY timestamp DESC) = 1
  *     (:180): keep_d[i] = 1 for the record with the largest Kafka timestamp of each key (ties:
- *     the last in batch order), 0 otherwise; sorted_perm_d = a STABLE argsort of key_d
- *     (fdx_argsort_i64). */
+ *     the last in batch order), 0 otherwise.  O(n): an open-addressing hash table in the
+ *     workspace (fdx_dedup_latest_workspace_size), no sort.  *bad_d = 1 if a key is -1 (the
+ *     table's empty pattern; bad_d is not cleared by the call).
+ *   fdx_cdc_compact: the kept records (keep_d) of a decoded micro-batch, in batch order, as the
+ *     stream state's input columns -- customer / terminal ids narrowed to int32 (an id outside
+ *     int32 becomes -1: fdx_stream_update then reports it out of range), ts (ns), amount,
+ *     fraud (fraud_d may be NULL: zeros; the CDC topic carries no label), row_out_d (optional)
+ *     = the batch position of each kept record; *count_d = the number kept (device int64).
+ *     The chain decode -> dedup -> compact -> fdx_stream_update -> forest stays on the device
+ *     (one host read: count_d, to size the update). */
 int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, const int64_t *us_d, int64_t n,
                    int64_t *unscaled_d, double *amount_d, int64_t *ts_ns_d, int32_t *bad_d, void *stream);
-int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d, int64_t n,
-                     uint8_t *keep_d, void *stream);
+size_t fdx_dedup_latest_workspace_size(int64_t n);
+int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, int64_t n, uint8_t *keep_d, int32_t *bad_d,
+                     void *workspace_d, size_t workspace_bytes, void *stream);
+size_t fdx_cdc_compact_workspace_size(int64_t n);
+int fdx_cdc_compact(const uint8_t *keep_d, int64_t n, const int64_t *customer_d, const int64_t *terminal_d,
+                    const int64_t *ts_ns_d, const double *amount_d, const uint8_t *fraud_d, int32_t *customer_out_d,
+                    int32_t *terminal_out_d, int64_t *ts_out_d, double *amount_out_d, uint8_t *fraud_out_d,
+                    int32_t *row_out_d, int64_t *count_d, void *workspace_d, size_t workspace_bytes, void *stream);
 /* ---- config 5: streaming micro-batches with incremental window state ------------------
  * BASELINE.json config 5 ("micro-batches of 64k CDC transactions: incremental window-state
  * update + scoring").  The reference's streaming job (pyspark/scripts/fraud_detection.py:
@@ -527,7 +498,7 @@ int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int3
  *   Writes X_d row r (leading dimension ld): [amount, weekend, night, (NB_w, AVG_w) x W] from
  *   the customer half and (NB_w, RISK_w) x W at column term_col0 (-1 = 3 + 2W) from the
  *   terminal half -- or, when term_rec_d != NULL, the terminal half as count records
- *   term_rec_d[r][W] (NB | FRAUD << 32, as fdx_terminal_windows_packed) for the multi-GPU
+ *   term_rec_d[r][W] (NB | FRAUD << 32, as fdx_terminal_windows_grouped) for the multi-GPU
  *   return exchange.  When cust_nb_d / cust_sum_d are given, the customer half goes there
  *   instead ([W][n] planes: NB int32 and the rolling SUM, bit-exact pandas roll_sum), and X_d
  *   may be NULL: the scoring layout of fdx_forest_prepare_grouped (cust_val_is_sum = 1,
@@ -549,11 +520,6 @@ int fdx_stream_status(fdx_stream s, int32_t *flags_h, void *stream);
 /* Non-blocking form: enqueues the copy of the status bits to flags_pinned_h (pinned host
  * memory, valid once the stream reaches this point); does not clear them. */
 int fdx_stream_status_async(fdx_stream s, int32_t *flags_pinned_h, void *stream);
-/* A HIP stream limited to the CUs whose bits are set in cu_mask (n_words x 32 bits, CU i =
- * bit i % 32 of word i / 32; hipExtStreamCreateWithCUMask) -- for running two overlapped
- * halves of a step on disjoint CU sets -- and its release. */
-int fdx_hip_stream_create_cu_mask(const uint32_t *cu_mask, int32_t n_words, void **stream_out);
-int fdx_hip_stream_destroy(void *stream);
 int fdx_stream_destroy(fdx_stream s);
 
 /* f-4 delay-aware split and Card-Precision@k (shared_functions.py:133-188, :352-411).

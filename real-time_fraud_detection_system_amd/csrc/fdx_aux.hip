@@ -112,28 +112,95 @@ __global__ void __launch_bounds__(256) k_cdc_decode(const uint8_t *__restrict__ 
     }
 }
 
-// Latest record per key over a stable argsort of the keys (sorted position i -> record
-// perm[i]): the run head scans its run and keeps the record with the largest Kafka
-// timestamp (ties: the last one in batch order).  keep[record] = 1 for the kept ones (the
-// host zeroes keep first).
-__global__ void __launch_bounds__(256) k_dedup_latest(const int64_t *__restrict__ key, const int64_t *__restrict__ kts,
-                                                      const int32_t *__restrict__ perm, int64_t n,
-                                                      uint8_t *__restrict__ keep) {
+// Latest record per key (ROW_NUMBER() OVER (PARTITION BY tx_id ORDER BY timestamp DESC) = 1)
+// with an open-addressing hash table in the caller's workspace -- O(n), four short launches,
+// no sort (a micro-batch's dedup was a full 64-bit radix argsort: 8 passes).  Slot h holds
+// the key (EMPTY until claimed), the largest Kafka timestamp seen (order-preserving unsigned
+// encoding) and the largest batch position holding that timestamp (ties: the last record in
+// batch order, the documented choice where Spark's tie order is arbitrary).
+constexpr unsigned long long kDedupEmpty = 0xFFFFFFFFFFFFFFFFull;  // reserved: key INT64_MAX ^ sign... see below
+__device__ __forceinline__ unsigned long long dedup_ukey(int64_t k) { return (unsigned long long)k; }
+__device__ __forceinline__ unsigned long long dedup_uts(int64_t t) {  // signed -> order-preserving unsigned
+    return (unsigned long long)t ^ 0x8000000000000000ull;
+}
+__device__ __forceinline__ uint32_t dedup_hash(unsigned long long k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
+__global__ void __launch_bounds__(256) k_dedup_init(unsigned long long *__restrict__ tkey,
+                                                    unsigned long long *__restrict__ tts, int32_t *__restrict__ tpos,
+                                                    int64_t cap) {
+    for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < cap; h += (int64_t)gridDim.x * blockDim.x) {
+        tkey[h] = kDedupEmpty;
+        tts[h] = 0ull;
+        tpos[h] = -1;
+    }
+}
+// claim (or find) the key's slot, raise its timestamp; slot_of[i] = the slot.  A key equal
+// to the EMPTY pattern (-1 as int64 tx_id) would alias empty slots: flagged as bad.
+__global__ void __launch_bounds__(256) k_dedup_insert(const int64_t *__restrict__ key, const int64_t *__restrict__ kts,
+                                                      int64_t n, unsigned long long *__restrict__ tkey,
+                                                      unsigned long long *__restrict__ tts, int64_t cap,
+                                                      int32_t *__restrict__ slot_of, int32_t *__restrict__ bad) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t r = perm[i];
-        const int64_t k = key[r];
-        if (i > 0 && key[perm[i - 1]] == k) continue;  // not a run head
-        int32_t best = r;
-        int64_t bt = kts[r];
-        for (int64_t j = i + 1; j < n; ++j) {
-            const int32_t q = perm[j];
-            if (key[q] != k) break;
-            if (kts[q] >= bt) {  // stable sort: q is later in batch order than best
-                bt = kts[q];
-                best = q;
-            }
+        const unsigned long long k = dedup_ukey(key[i]);
+        if (k == kDedupEmpty) {
+            *bad = 1;
+            slot_of[i] = -1;
+            continue;
         }
-        keep[best] = 1;
+        uint32_t h = dedup_hash(k) & (uint32_t)(cap - 1);
+        for (;;) {  // cap >= 2 n: a free slot always exists, the probe ends
+            const unsigned long long prev = atomicCAS(tkey + h, kDedupEmpty, k);
+            if (prev == kDedupEmpty || prev == k) break;
+            h = (h + 1) & (uint32_t)(cap - 1);
+        }
+        atomicMax(tts + h, dedup_uts(kts[i]));
+        slot_of[i] = (int32_t)h;
+    }
+}
+__global__ void __launch_bounds__(256) k_dedup_pos(const int64_t *__restrict__ kts, int64_t n,
+                                                   const unsigned long long *__restrict__ tts,
+                                                   const int32_t *__restrict__ slot_of, int32_t *__restrict__ tpos) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t h = slot_of[i];
+        if (h >= 0 && dedup_uts(kts[i]) == tts[h]) atomicMax(tpos + h, (int32_t)i);
+    }
+}
+__global__ void __launch_bounds__(256) k_dedup_keep(int64_t n, const int32_t *__restrict__ slot_of,
+                                                    const int32_t *__restrict__ tpos, uint8_t *__restrict__ keep) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t h = slot_of[i];
+        keep[i] = (h >= 0 && tpos[h] == (int32_t)i) ? 1 : 0;
+    }
+}
+
+// The kept records of a micro-batch, compacted in batch order into the stream state's input
+// columns: pos = exclusive scan of keep; ids narrowed to int32 (an id outside int32 becomes
+// -1, which fdx_stream_update reports as a key out of range instead of wrapping into range).
+__global__ void __launch_bounds__(256) k_cdc_compact(const uint8_t *__restrict__ keep, const uint32_t *__restrict__ pos,
+                                                     int64_t n, const int64_t *__restrict__ cust,
+                                                     const int64_t *__restrict__ term, const int64_t *__restrict__ ts,
+                                                     const double *__restrict__ amt, const uint8_t *__restrict__ fraud,
+                                                     int32_t *__restrict__ cust_out, int32_t *__restrict__ term_out,
+                                                     int64_t *__restrict__ ts_out, double *__restrict__ amt_out,
+                                                     uint8_t *__restrict__ fraud_out, int32_t *__restrict__ row_out,
+                                                     int64_t *__restrict__ count) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i == n - 1) *count = (int64_t)pos[i] + (keep[i] ? 1 : 0);
+        if (!keep[i]) continue;
+        const int64_t j = pos[i];
+        const int64_t c = cust[i], t = term[i];
+        cust_out[j] = (c >= 0 && c <= INT32_MAX) ? (int32_t)c : -1;
+        term_out[j] = (t >= 0 && t <= INT32_MAX) ? (int32_t)t : -1;
+        ts_out[j] = ts[i];
+        amt_out[j] = amt[i];
+        fraud_out[j] = fraud ? (uint8_t)(fraud[i] != 0) : 0;
+        if (row_out) row_out[j] = (int32_t)i;
     }
 }
 
@@ -336,14 +403,86 @@ extern "C" int fdx_cdc_decode(const uint8_t *bytes_d, const int64_t *offsets_d, 
     return FDX_OK;
 }
 
-extern "C" int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, const int32_t *sorted_perm_d,
-                                int64_t n, uint8_t *keep_d, void *stream) {
-    FDX_REQUIRE(n >= 0, "negative size");
+static int64_t dedup_cap(int64_t n) {
+    int64_t cap = 2;
+    while (cap < 2 * n) cap <<= 1;
+    return cap;
+}
+
+extern "C" size_t fdx_dedup_latest_workspace_size(int64_t n) {
+    if (n < 0) n = 0;
+    const int64_t cap = dedup_cap(n);
+    return round_up((size_t)cap * 8, 256) * 2 + round_up((size_t)cap * 4, 256) + round_up((size_t)n * 4, 256) + 256;
+}
+
+extern "C" int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, int64_t n, uint8_t *keep_d,
+                                int32_t *bad_d, void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     if (n == 0) return FDX_OK;
-    FDX_REQUIRE(key_d && kafka_ts_d && sorted_perm_d && keep_d, "null pointer");
-    FDX_HIP(hipMemsetAsync(keep_d, 0, (size_t)n, as_stream(stream)));
-    hipLaunchKernelGGL(k_dedup_latest, dim3(stream_grid(n, 256)), dim3(256), 0, as_stream(stream), key_d, kafka_ts_d,
-                       sorted_perm_d, n, keep_d);
-    FDX_LAUNCHED("k_dedup_latest");
+    FDX_REQUIRE(key_d && kafka_ts_d && keep_d && bad_d, "null pointer");
+    const size_t need = fdx_dedup_latest_workspace_size(n);
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("dedup workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    const int64_t cap = dedup_cap(n);
+    char *w = reinterpret_cast<char *>(workspace_d);
+    auto *tkey = reinterpret_cast<unsigned long long *>(w);
+    auto *tts = reinterpret_cast<unsigned long long *>(w + round_up((size_t)cap * 8, 256));
+    auto *tpos = reinterpret_cast<int32_t *>(w + 2 * round_up((size_t)cap * 8, 256));
+    auto *slot = reinterpret_cast<int32_t *>(w + 2 * round_up((size_t)cap * 8, 256) + round_up((size_t)cap * 4, 256));
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_dedup_init, dim3(stream_grid(cap, 256)), dim3(256), 0, st, tkey, tts, tpos, cap);
+    FDX_LAUNCHED("k_dedup_init");
+    hipLaunchKernelGGL(k_dedup_insert, dim3(stream_grid(n, 256)), dim3(256), 0, st, key_d, kafka_ts_d, n, tkey, tts,
+                       cap, slot, bad_d);
+    FDX_LAUNCHED("k_dedup_insert");
+    hipLaunchKernelGGL(k_dedup_pos, dim3(stream_grid(n, 256)), dim3(256), 0, st, kafka_ts_d, n, tts, slot, tpos);
+    FDX_LAUNCHED("k_dedup_pos");
+    hipLaunchKernelGGL(k_dedup_keep, dim3(stream_grid(n, 256)), dim3(256), 0, st, n, slot, tpos, keep_d);
+    FDX_LAUNCHED("k_dedup_keep");
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_cdc_compact_workspace_size(int64_t n) {
+    if (n < 0) n = 0;
+    return round_up((size_t)n * 4, 256) + fdx_exclusive_scan_u32_workspace_size(n) + 256;
+}
+
+__global__ void k_u8_to_u32(const uint8_t *__restrict__ in, int64_t n, uint32_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i] ? 1u : 0u;
+}
+
+extern "C" int fdx_cdc_compact(const uint8_t *keep_d, int64_t n, const int64_t *customer_d, const int64_t *terminal_d,
+                               const int64_t *ts_ns_d, const double *amount_d, const uint8_t *fraud_d,
+                               int32_t *customer_out_d, int32_t *terminal_out_d, int64_t *ts_out_d,
+                               double *amount_out_d, uint8_t *fraud_out_d, int32_t *row_out_d, int64_t *count_d,
+                               void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(count_d, "null count");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        FDX_HIP(hipMemsetAsync(count_d, 0, sizeof(int64_t), st));
+        return FDX_OK;
+    }
+    FDX_REQUIRE(keep_d && customer_d && terminal_d && ts_ns_d && amount_d && customer_out_d && terminal_out_d &&
+                    ts_out_d && amount_out_d && fraud_out_d,
+                "null pointer");
+    const size_t need = fdx_cdc_compact_workspace_size(n);
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("cdc compact workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    auto *pos = reinterpret_cast<uint32_t *>(workspace_d);
+    void *scan_ws = reinterpret_cast<char *>(workspace_d) + round_up((size_t)n * 4, 256);
+    hipLaunchKernelGGL(k_u8_to_u32, dim3(stream_grid(n, 256)), dim3(256), 0, st, keep_d, n, pos);
+    FDX_LAUNCHED("k_u8_to_u32");
+    int rc = fdx_exclusive_scan_u32(pos, n, scan_ws, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_cdc_compact, dim3(stream_grid(n, 256)), dim3(256), 0, st, keep_d, pos, n, customer_d,
+                       terminal_d, ts_ns_d, amount_d, fraud_d, customer_out_d, terminal_out_d, ts_out_d, amount_out_d,
+                       fraud_out_d, row_out_d, count_d);
+    FDX_LAUNCHED("k_cdc_compact");
     return FDX_OK;
 }

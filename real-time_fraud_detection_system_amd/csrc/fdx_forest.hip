@@ -48,10 +48,8 @@ struct fdx_forest_s {
         bool in_lds;
     };
     std::vector<Chunk> chunks;
-    int32_t *chunk_t_d = nullptr;     // [n_trees+1] first tree of each chunk (tile kernels)
+    int32_t *chunk_t_d = nullptr;     // [n_trees+1] first tree of each chunk (all-chunks-at-once launch)
     int64_t *chunk_base_d = nullptr;  // [n_trees+1] first node of each chunk
-    bool tile_ok = false;             // every chunk of the tile variant fits its LDS budget
-    int64_t slab_rows = 0;  // 0 = default (FDX_FOREST_SLAB_ROWS or all rows)
     int variant = 0;        // index into kVariants
     std::vector<int64_t> node_offsets;  // host copy (chunking)
     // rank layout (4-byte nodes over per-feature threshold ranks, see "Rank layout" below)
@@ -67,11 +65,12 @@ struct fdx_forest_s {
     float *rseg_d = nullptr, *rsmp_d = nullptr;  // two-level rank search tables
     uint16_t *ritab_d = nullptr;                  // [16][kIntTab] ranks of small integer values
     uint16_t *rrat_d = nullptr;                   // [16][kRatN][kRatN] ranks of small ratios fr / nb
+    float *retab_d = nullptr;                     // Eytzinger sample tables (RankTab::etab)
+    int32_t reoff[4] = {}, relev[4] = {}, rnetab = 0;
     int32_t ruoff[32] = {}, rsoff[32] = {}, rscnt[32] = {}, rseg = 16, rnsmp = 0;
     // rank layout v2 (32 threshold-rank slots, see build_rank_layout)
     bool rank_v2 = false;
     bool rank_identity = false;  // v2 with slot s = feature s (<= 16 slots): v1 rank rows, compact planes
-    bool rank_pair = false;      // rank layout v3: sibling pairs (P16 = 4, see pair_walk)
     // host copies of the packed forest and scaler (set_variant rebuilds the rank layout in the
     // other node format when a variant needs it)
     std::vector<uint64_t> h_packed;
@@ -134,7 +133,16 @@ struct RankTab {
     // rat[(f * kRatN + nb) * kRatN + fr] = rank of the scaled ratio fr / nb (0 when nb == 0,
     // the reference's fillna(0)) for nb < kRatN: the terminal risks are such ratios
     const uint16_t *rat;
+    // Eytzinger form of the segment samples of the reference layout's searched features
+    // (kW3Search: amount + the three averages), for k_zfill_grouped_w3: feature kW3Search[s]'s
+    // samples padded with +inf to 2^elev[s] - 1 entries, BFS order, entry k (1-based) at
+    // etab[eoff[s] + k].  A lane's descent reads level d from a window of 2^d consecutive words,
+    // so the first levels are bank-conflict free (the sorted table's binary search puts every
+    // probe of a level on one bank: stride n / 2^d).  NULL when the tables exceed the LDS budget.
+    const float *etab;
+    int32_t eoff[4], elev[4], n_etab;
 };
+constexpr int kW3Search[4] = {0, 4, 6, 8};  // TX_AMOUNT, CUSTOMER_ID_AVG_AMOUNT_{1,7,30}DAY_WINDOW
 constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
 constexpr int kIntTab = 256;           // integer rank table entries per feature (8 KiB in LDS)
 constexpr int kRatN = 128;             // ratio rank table: nb, fr < kRatN (32 KiB per feature, global)
@@ -245,6 +253,15 @@ __device__ __forceinline__ void rank_fixed(const float (&v)[16], const int (&fs)
         }
         out[f] = v[f] != v[f] ? 0xFFFFu : r;
     }
+}
+
+// ranks of the features in `need` by a full lower_bound over U_f in global memory (the rare
+// fallback of k_zfill_grouped_w3: values outside its integer / ratio rank tables)
+__device__ __forceinline__ void rank_row_global(const float (&v)[16], const RankTab &rt, uint32_t (&out)[16],
+                                             uint32_t need) {
+#pragma unroll
+    for (int f = 0; f < 16; ++f)
+        if ((need >> f) & 1u) out[f] = rank_of(v[f], rt.u + rt.off[f], rt.cnt[f]);
 }
 
 // every thread of the block: stage the sample table into LDS (prepare kernels, RANK mode)
@@ -515,7 +532,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             q[15] = 0u;
             v[0] = zval(camt[i], mean, scale, 0);
             bool nan = v[0] != v[0];
-            const int64_t q_ = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
+            const int64_t q_ = term_inv ? term_inv[r] : r;
             const int64_t *rec = term_rec + q_ * W;
             int64_t ctw[3] = {0, 0, 0};
             if (val_is_sum & 4) compact_load(term_rec, q_, ctw);  // (W = 3, checked by the host)
@@ -566,7 +583,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
         v[1] = zval((double)we, mean, scale, 1);
         v[2] = zval((double)ni, mean, scale, 2);
         bool nan = v[0] != v[0];
-        const int64_t q = (val_is_sum & 2) ? i : (term_inv ? term_inv[r] : r);
+        const int64_t q = term_inv ? term_inv[r] : r;
         const int64_t *rec = term_rec + q * W;
         int64_t ctw[3] = {0, 0, 0};
         if (val_is_sum & 4) compact_load(term_rec, q, ctw);  // (W = 3, checked by the host)
@@ -614,11 +631,12 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
     int32_t *__restrict__ nan_flag, RankTab rt) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     constexpr int W = 3, nf = 15;
-    constexpr int kFix[4] = {0, 4, 6, 8};  // amount + the three averages: searched
-    __shared__ float s_smp[kMaxRankSamples];
+    __shared__ float s_e[kMaxRankSamples];  // Eytzinger sample tables (RankTab::etab)
     __shared__ uint16_t s_itab[16 * kIntTab];
     for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
-    stage_samples(s_smp, rt);
+    for (int e = threadIdx.x; e < rt.n_etab; e += blockDim.x) s_e[e] = rt.etab[e];
+    __syncthreads();
+    const int e_lmax = max(max(rt.elev[0], rt.elev[1]), max(rt.elev[2], rt.elev[3]));
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const bool rec16 = ((uintptr_t)term_rec & 15) == 0;  // uniform
     auto row_of = [&](int64_t j) -> int32_t { return j < n ? (cust_perm ? cust_perm[j] : (int32_t)j) : -1; };
@@ -632,7 +650,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
             L.c[w] = cnb[(int64_t)w * n + j];
             L.cv[w] = cval[(int64_t)w * n + j];
         }
-        const int64_t q_ = (val_is_sum & 2) ? j : (term_inv ? term_inv[r] : r);
+        const int64_t q_ = term_inv ? term_inv[r] : r;
         const int64_t *src = term_rec + q_ * W;
         if (val_is_sum & 4) {
             compact_load(term_rec, q_, L.tw);
@@ -712,39 +730,27 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
             // unconditional read (index clamped to 0 when the table does not apply)
             rq[w] = rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
         }
-        // two-level search of the 4 continuous features: LDS samples, then all segments at once
-        int32_t lo[4], cnt[4];
+        // two-level search of the 4 continuous features: the Eytzinger descent over the LDS
+        // samples (cs = #samples < v: k - 2^L after L levels), then all 4 segments at once
+        int32_t ek[4] = {1, 1, 1, 1};
+        for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            lo[s] = rt.soff[kFix[s]];
-            cnt[s] = rt.scnt[kFix[s]];
-        }
-        int32_t nmax = max(max(cnt[0], cnt[1]), max(cnt[2], cnt[3]));
-        while (nmax > 1) {
-            nmax = 0;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (cnt[s] > 1) {
-                    const int32_t h = cnt[s] >> 1;
-                    lo[s] = (s_smp[lo[s] + h] < v[kFix[s]]) ? lo[s] + h : lo[s];
-                    cnt[s] -= h;
-                }
-                nmax = max(nmax, cnt[s]);
-            }
+            for (int s = 0; s < 4; ++s)
+                if (l < rt.elev[s]) ek[s] = 2 * ek[s] + (s_e[rt.eoff[s] + ek[s]] < v[kW3Search[s]] ? 1 : 0);
         }
         int32_t cs[4];
         float4 sg[4][4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const int f = kFix[s];
-            cs[s] = cnt[s] > 0 ? lo[s] - rt.soff[f] + (s_smp[lo[s]] < v[f] ? 1 : 0) : 0;
+            const int f = kW3Search[s];
+            cs[s] = ek[s] - (1 << rt.elev[s]);
             const float4 *p = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)max(cs[s] - 1, 0) * 16);
 #pragma unroll
             for (int k = 0; k < 4; ++k) sg[s][k] = p[k];
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const int f = kFix[s];
+            const int f = kW3Search[s];
             uint32_t k = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -766,7 +772,7 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
         }
         if (nan) *nan_flag = 1;
         need &= (1u << nf) - 1u;
-        if (__any(need != 0)) rank_row(v, nf, rt, s_smp, q, need);  // table overflows (rare)
+        if (need) rank_row_global(v, rt, q, need);  // table overflows (rare): full lower_bound in HBM
         q[15] = 0u;
         uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
         dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
@@ -781,44 +787,28 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
     return *reinterpret_cast<const uint64_t *>(gbase + byte_off);
 }
 
-// Kernel variants (block size, rows per lane R, trees per walk group G).  LDS holds the
-// row features [FS][BLOCK*R] float32 and, in the rest of the 160 KiB, the chunk's nodes.
-// tile = 1: k_forest_tile (rows resident, trees streamed) instead of k_forest_chunk.
-// rank = 1: k_forest_rank over the rank layout (4-byte nodes, u16 rank rows).
+// Kernel variants.  rank = 0: k_forest_chunk over the wide layout (float32 rows, 8-byte
+// nodes) -- forests the rank layout cannot hold or with more than 15 features; rank = 1:
+// k_forest_rank over the rank layout (4-byte nodes, u16 rank rows), block size BLOCK, one row
+// per lane, G trees walked at once per lane (G independent LDS dependency chains), the
+// software-pipelined walk with waits grouped by PIPE chains.  p16 = the rank node / plane
+// format: 0 = v1 (u32 planes), 2 = v2 (32 threshold slots over u16 planes), 3 = v2 nodes over
+// 16 u16 planes (forests whose every feature fits one slot).
 struct Variant {
-    int block, rows, group, tile, rank, p16 = 0, pipe = 0, occ = 1;
+    int block, rows, group, rank, p16, pipe;
 };
-constexpr int kDefaultRankVariant = 41;  // measured fastest on MI355X (r01: G=6 walks per lane, pipelined, paired waits)
 constexpr Variant kVariants[] = {
-    {512, 1, 4, 0, 0},  {1024, 1, 4, 0, 0}, {512, 2, 4, 0, 0},  {512, 2, 2, 0, 0},  {256, 2, 4, 0, 0},
-    {1024, 1, 3, 0, 0}, {512, 1, 3, 0, 0},  {768, 1, 3, 0, 0},  {768, 1, 4, 0, 0},  {1024, 1, 2, 0, 0},
-    {768, 1, 2, 0, 0},  {768, 2, 2, 0, 0},  {1024, 1, 2, 1, 0}, {512, 2, 1, 1, 0},  {512, 3, 1, 1, 0},
-    {768, 2, 1, 1, 0},
-    // rank layout (k_forest_rank): variants 16..
-    {1024, 1, 4, 0, 1}, {1024, 1, 2, 0, 1}, {512, 2, 2, 0, 1},  {512, 2, 4, 0, 1},  {1024, 1, 3, 0, 1},
-    {768, 1, 4, 0, 1},  {256, 4, 2, 0, 1},  {1024, 1, 6, 0, 1}, {1024, 1, 8, 0, 1}, {1024, 1, 5, 0, 1},
-    // rank layout, u16 row planes (2048 rows per tile in the same 64 KiB): variants 26..
-    {1024, 2, 3, 0, 1, 1}, {1024, 2, 4, 0, 1, 1}, {1024, 2, 5, 0, 1, 1}, {512, 4, 3, 0, 1, 1}, {1024, 2, 2, 0, 1, 1},
-    // + software-pipelined walk (each chain's next LDS read issued as soon as it can be): 31..
-    {1024, 2, 3, 0, 1, 1, 1}, {1024, 2, 4, 0, 1, 1, 1}, {1024, 2, 5, 0, 1, 1, 1}, {1024, 1, 6, 0, 1, 0, 1},
-    {1024, 1, 4, 0, 1, 1, 1},
-    // 36.. pipelined shape sweep
-    {1024, 1, 6, 0, 1, 1, 1}, {1024, 1, 5, 0, 1, 0, 1}, {768, 1, 6, 0, 1, 0, 1}, {512, 2, 6, 0, 1, 0, 1},
-    {512, 2, 4, 0, 1, 0, 1},
-    // 41.. grouped waits (pipe = group width)
-    {1024, 1, 6, 0, 1, 0, 2}, {1024, 1, 6, 0, 1, 0, 3}, {1024, 1, 6, 0, 1, 0, 6},
-    // 44..: rank layout v2 (32 threshold-rank slots, u16 planes of 1,024 rows; p16 = 2)
-    {1024, 1, 6, 0, 1, 2, 2}, {1024, 1, 4, 0, 1, 2, 2},
-    // 46..: v2 nodes over 16 slots of 1,024 u16 rows (32 KiB of planes; slot = feature, v1 rows)
-    {1024, 1, 6, 0, 1, 3, 2}, {1024, 1, 8, 0, 1, 3, 2},
-    // 48..: rank layout v3, sibling pairs (one LDS round trip per step; p16 = 4)
-    // (pipe = SEL of pair_walk: 0 compiler select, 1 v_bfi select, 2 grouped compares)
-    {1024, 1, 6, 0, 1, 4, 0}, {1024, 1, 6, 0, 1, 4, 1}, {1024, 1, 8, 0, 1, 4, 1}, {1024, 1, 6, 0, 1, 4, 2},
-    {1024, 1, 9, 0, 1, 4, 2}, {1024, 1, 4, 0, 1, 4, 1},
-    // 54..: compact v2 nodes, two 1,024-thread blocks per CU (8 waves per SIMD, <= 64 VGPRs)
-    {1024, 1, 4, 0, 1, 3, 2, 2}, {1024, 1, 6, 0, 1, 3, 2, 2}, {1024, 1, 3, 0, 1, 3, 2, 2}};
-constexpr int kDefaultRankV2Variant = 44;
-constexpr int kDefaultRankCompactVariant = 46;
+    {512, 1, 4, 0, 0, 0},   // 0: wide layout
+    {1024, 1, 6, 1, 0, 2},  // 1: rank layout v1 (the default; r01/r02 sweeps: fastest of 57 shapes)
+    {1024, 1, 6, 1, 2, 2},  // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
+    {1024, 1, 6, 1, 3, 2},  // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
+    {1024, 1, 8, 1, 0, 2},  // 4-6: v1 with 8 / 10 / 12 walk chains per lane (latency-hiding study)
+    {1024, 1, 10, 1, 0, 2},
+    {1024, 1, 12, 1, 0, 2},
+};
+constexpr int kDefaultRankVariant = 1;
+constexpr int kDefaultRankV2Variant = 2;
+constexpr int kDefaultRankCompactVariant = 3;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -963,101 +953,6 @@ __global__ void __launch_bounds__(BLOCK) k_forest_chunk(
     }
 }
 
-// Rows-resident traversal (tile variants): one block per CU keeps a tile of BLOCK*R rows'
-// scaled features in LDS for the WHOLE forest and streams the trees through the rest of LDS
-// chunk by chunk.  The chunks are read from L2 (the packed forest, a few MB, stays resident
-// in every XCD's 4 MiB L2 or the Infinity Cache), the running sums stay in registers, so a
-// row costs one 64-B read of z and one 8-B write of proba in HBM instead of 80 B per chunk
-// launch.  Tree order of the float64 sum is unchanged (chunks, then groups, in order).
-template <int FS, int BLOCK, int R, int G>
-__global__ void __launch_bounds__(BLOCK) k_forest_tile(
-    const uint64_t *__restrict__ nodes, const int32_t *__restrict__ chunk_t, const int64_t *__restrict__ chunk_base,
-    int32_t n_chunks, const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
-    const float *__restrict__ z, const int32_t *__restrict__ nan_flag, int64_t n, double *__restrict__ proba,
-    const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
-    int32_t n_trees) {
-    constexpr int kRowsPerBlock = BLOCK * R;
-    constexpr int kNodeCap = lds_node_bytes(FS, BLOCK, R) / 8;
-    constexpr int K = R * G;
-    __shared__ uint64_t s_nodes[kNodeCap];
-    __shared__ float s_x[FS][kRowsPerBlock];
-    const int tid = threadIdx.x;
-    const char *lbase = reinterpret_cast<const char *>(s_nodes);
-    const bool any_nan = *nan_flag != 0;
-    const float *xcol[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) xcol[k] = &s_x[0][(k / G) * BLOCK + tid];
-    for (int64_t base = (int64_t)blockIdx.x * kRowsPerBlock; base < n; base += (int64_t)gridDim.x * kRowsPerBlock) {
-        int64_t row[R];
-        bool ok[R];
-        double a[R];
-        __syncthreads();  // the previous tile is done with s_x
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            row[r] = base + r * BLOCK + tid;
-            ok[r] = row[r] < n;
-            const float4 *src = reinterpret_cast<const float4 *>(z + (ok[r] ? row[r] : 0) * FS);
-#pragma unroll
-            for (int q = 0; q < FS / 4; ++q) {
-                float4 v = src[q];
-                s_x[4 * q + 0][r * BLOCK + tid] = v.x;
-                s_x[4 * q + 1][r * BLOCK + tid] = v.y;
-                s_x[4 * q + 2][r * BLOCK + tid] = v.z;
-                s_x[4 * q + 3][r * BLOCK + tid] = v.w;
-            }
-            a[r] = 0.0;
-        }
-        for (int c = 0; c < n_chunks; ++c) {
-            const int32_t t0 = chunk_t[c], t1 = chunk_t[c + 1];
-            const int64_t nb0 = chunk_base[c];
-            const int32_t cn = (int32_t)(chunk_base[c + 1] - nb0);
-            __syncthreads();  // every wave is done with the previous chunk's nodes
-            for (int i = tid; i < cn; i += BLOCK) s_nodes[i] = nodes[nb0 + i];
-            __syncthreads();
-            for (int t = t0; t < t1; t += G) {
-                uint32_t p[K];
-                uint64_t nd[K];
-                int dmax = 0;
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const bool act = t + g < t1;
-                    const uint32_t p0 = act ? (uint32_t)(root[t + g] - nb0) * 8u : 0u;
-                    const uint64_t n0 = act ? node_at<true>(s_nodes, lbase, p0) : 0ull;
-                    dmax = act ? max(dmax, depth[t + g]) : dmax;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        p[r * G + g] = p0;
-                        nd[r * G + g] = n0;
-                    }
-                }
-                if (any_nan)
-                    walk_group<true, true, kRowsPerBlock, K>(s_nodes, lbase, xcol, p, nd, dmax);
-                else
-                    walk_group<false, true, kRowsPerBlock, K>(s_nodes, lbase, xcol, p, nd, dmax);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        if (t + g < t1) {
-                            a[r] += leaf_value(nd[r * G + g]);
-                            if (leaf_out && ok[r]) {
-                                const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
-                                if (dst >= 0) leaf_out[dst * n_trees + t + g] = orig[nb0 + (p[r * G + g] >> 3)];
-                            }
-                        }
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!ok[r]) continue;
-            const int64_t dst = out_perm ? (int64_t)out_perm[row[r]] : row[r];
-            if (dst >= 0) proba[dst] = a[r] / (double)n_trees;  // < 0: padding slot
-        }
-    }
-}
-
 // Rank-layout walk step (see "Rank layout"): 5 VALU + 2 LDS reads per chain.  pa = LDS byte
 // address of the chain's node, nd = that node.
 constexpr uint32_t kRankNodeB = kRankXWords * 4;  // byte offset of the node region in LDS
@@ -1075,8 +970,8 @@ __device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
 // steps exactly as in the 32-bit form (leaf: k = 0x7FFF vs sentinel 0x4000 -> d < 0, off 0;
 // jump: k = 0 -> d > 0); |d| < 2^31 because r, k <= 0x7FFF.
 // Node / plane formats (template parameter P16): 0 = u32 planes, 4-bit feature, 12-bit right
-// offset (rank layout v1); 1 = the same nodes over u16 planes; 2 = rank layout v2: u16 planes
-// of 1,024 rows, a 5-bit SLOT field and an 11-bit right offset (see build_rank_layout).
+// offset (rank layout v1); 2 = rank layout v2: u16 planes of 1,024 rows, a 5-bit SLOT field and
+// an 11-bit right offset (see build_rank_layout).
 template <int P16>
 constexpr uint32_t kSlotMask = (P16 == 2 || P16 == 3) ? 0xF800u : 0xF000u;
 template <int P16>
@@ -1181,165 +1076,6 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
     for (; d < depth; ++d) step();
 }
 
-__device__ __forceinline__ uint2 lds64(const char *lds, uint32_t byte_addr) {
-    return *reinterpret_cast<const uint2 *>(lds + byte_addr);
-}
-
-// Rank layout v3, the PAIR layout (P16 = 4): the two children of a node are adjacent words of
-// an 8-byte aligned pair, so one ds_read_b64 fetches both, issued together with the node's
-// feature-rank read: ONE dependent LDS round trip per step (the v1 step reads the rank, then
-// the next node: two).  Node word: [31:16] k+1 | [15:12] feature | [11:0] offset, in pairs,
-// of its children pair from the pair holding the node.  Row planes hold (r+1) << 16 (NaN:
-// 0xFFFFFFFF), so  r <= k  <=>  plane <= word  (one unsigned compare; the low 16 bits of the
-// word never decide it).  Ranks are capped at 32,766 (at most 32,766 thresholds per feature),
-// so planes and words stay below 2^31.  Leaves have offset 0, so their "children" pair is
-// their own pair, and are fixed points: a left leaf is 0x7FFF0000 (every plane value <=
-// 0x7FFF0000 compares <=, picks the left word = itself), a right leaf 0 (nothing compares
-// <=, picks itself).
-// Chain state: w = node word, q = LDS byte address of the pair holding it.  Step:
-//   c = q + (w & 0xFFF) * 8;  x = plane[(w & 0xF000) | lane];  pr = pair[c]
-//   w = x <= w ? pr.lo : pr.hi;  q = c                       (5 VALU, 1 b32 + 1 b64 read)
-// Software-pipelined: each chain's next two reads are issued right after its select, so
-// every chain of the wave has its reads in flight while the others wait / compute.
-// c = q + (w & 0xFFF) * 8 in 2 VALU (the compiler's form: shift, mask, add)
-__device__ __forceinline__ uint32_t pair_child(uint32_t w, uint32_t q) {
-    uint32_t c;
-    asm("v_and_b32 %0, 0xfff, %1\n\tv_lshl_add_u32 %0, %0, 3, %2" : "=&v"(c) : "v"(w), "v"(q));
-    return c;
-}
-
-// SEL = how a step selects the next word (same result):
-//   0  C: compare + v_cndmask (the compiler puts the gfx950 VCC wait, s_nop 1, between them)
-//   1  asm: d = w - x, m = d >> 31 (arithmetic), w = v_bfi(m, hi, lo) -- no lane mask, no
-//      wait states; needs w, x < 2^31 (v3 caps ranks at 32,766: x <= 0x7FFF0000)
-//   2  asm: chains in groups of 3, the 3 compares (to SGPR pairs) before the 3 selects, so
-//      every v_cndmask is 2 instructions after its compare (K a multiple of 3)
-// Every form then computes the next children-pair address and the rank address (3 VALU).
-template <int K, int SEL>
-__device__ __forceinline__ void pair_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&q)[K],
-                                          uint32_t (&w)[K], int depth) {
-    constexpr int S = (SEL == 2 && K % 3 != 0) ? 1 : SEL;  // tail groups of other widths: the bfi form
-    uint32_t x[K], c[K];
-    uint2 pr[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        c[k] = pair_child(w[k], q[k]);
-        pr[k] = lds64(lds, c[k]);
-        x[k] = lds32(lds, (w[k] & 0xF000u) | lane_base[k]);
-    }
-    auto reads = [&](int k, uint32_t xa) {
-        pr[k] = lds64(lds, c[k]);  // pair first: the wait for x (younger) covers both
-        x[k] = lds32(lds, xa);
-    };
-    // one asm block per step of a chain (or of 3 chains): the compiler pads the boundary
-    // between two asm blocks with an s_nop
-    auto step = [&]() {
-        if constexpr (S == 2) {
-#pragma unroll
-            for (int k = 0; k < K; k += 3) {
-                uint64_t m0, m1, m2;
-                uint32_t t0, t1, t2, a0, a1, a2;
-                asm("v_cmp_le_u32_e64 %[m0], %[x0], %[w0]\n\t"
-                    "v_cmp_le_u32_e64 %[m1], %[x1], %[w1]\n\t"
-                    "v_cmp_le_u32_e64 %[m2], %[x2], %[w2]\n\t"
-                    "v_cndmask_b32_e64 %[w0], %[h0], %[l0], %[m0]\n\t"
-                    "v_cndmask_b32_e64 %[w1], %[h1], %[l1], %[m1]\n\t"
-                    "v_cndmask_b32_e64 %[w2], %[h2], %[l2], %[m2]\n\t"
-                    "v_and_b32 %[t0], 0xfff, %[w0]\n\t"
-                    "v_and_b32 %[t1], 0xfff, %[w1]\n\t"
-                    "v_and_b32 %[t2], 0xfff, %[w2]\n\t"
-                    "v_lshl_add_u32 %[c0], %[t0], 3, %[c0]\n\t"
-                    "v_lshl_add_u32 %[c1], %[t1], 3, %[c1]\n\t"
-                    "v_lshl_add_u32 %[c2], %[t2], 3, %[c2]\n\t"
-                    "v_and_or_b32 %[a0], %[w0], %[fm], %[b0]\n\t"
-                    "v_and_or_b32 %[a1], %[w1], %[fm], %[b1]\n\t"
-                    "v_and_or_b32 %[a2], %[w2], %[fm], %[b2]"
-                    : [w0] "+v"(w[k]), [w1] "+v"(w[k + 1]), [w2] "+v"(w[k + 2]), [c0] "+v"(c[k]),
-                      [c1] "+v"(c[k + 1]), [c2] "+v"(c[k + 2]), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
-                      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2)
-                    : [x0] "v"(x[k]), [x1] "v"(x[k + 1]), [x2] "v"(x[k + 2]), [h0] "v"(pr[k].y),
-                      [l0] "v"(pr[k].x), [h1] "v"(pr[k + 1].y), [l1] "v"(pr[k + 1].x), [h2] "v"(pr[k + 2].y),
-                      [l2] "v"(pr[k + 2].x), [fm] "s"(0xF000u), [b0] "v"(lane_base[k]), [b1] "v"(lane_base[k + 1]),
-                      [b2] "v"(lane_base[k + 2]));
-                reads(k, a0);
-                reads(k + 1, a1);
-                reads(k + 2, a2);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if constexpr (S == 1) {
-                    uint32_t t, a;
-                    asm("v_sub_u32 %[t], %[w], %[x]\n\t"
-                        "v_ashrrev_i32 %[t], 31, %[t]\n\t"
-                        "v_bfi_b32 %[w], %[t], %[hi], %[lo]\n\t"
-                        "v_and_b32 %[t], 0xfff, %[w]\n\t"
-                        "v_lshl_add_u32 %[c], %[t], 3, %[c]\n\t"
-                        "v_and_or_b32 %[a], %[w], %[fm], %[b]"
-                        : [w] "+v"(w[k]), [c] "+v"(c[k]), [t] "=&v"(t), [a] "=&v"(a)
-                        : [x] "v"(x[k]), [hi] "v"(pr[k].y), [lo] "v"(pr[k].x), [fm] "s"(0xF000u),
-                          [b] "v"(lane_base[k]));
-                    reads(k, a);
-                } else {
-                    w[k] = x[k] <= w[k] ? pr[k].x : pr[k].y;
-                    c[k] = pair_child(w[k], c[k]);
-                    reads(k, (w[k] & 0xF000u) | lane_base[k]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    };
-    int d = 0;
-    bool done = false;
-    for (; d + kExitEvery <= depth; d += kExitEvery) {
-#pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) step();
-        uint32_t moving = 0;  // leaves (and only leaves) have offset 0
-#pragma unroll
-        for (int k = 0; k < K; ++k) moving |= w[k] & 0xFFFu;
-        if (!__any(moving != 0)) {
-            done = true;
-            break;
-        }
-    }
-    if (!done)
-        for (; d < depth; ++d) step();
-#pragma unroll
-    for (int k = 0; k < K; ++k) q[k] = c[k];  // every chain at a leaf: its "children" pair is its own
-}
-
-// The pair walk for batches with NaN features: a NaN rank (0xFFFFFFFF) takes the node's
-// missing_go_to_left (mleft by node position; p = byte address of the chain's node), and
-// leaves stay put.  Returns the leaf addresses in p.
-template <int K>
-__device__ __forceinline__ void pair_walk_nan(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&q)[K],
-                                              uint32_t (&w)[K], uint32_t (&p)[K], int depth,
-                                              const uint8_t *__restrict__ mleft) {
-    for (int d = 0; d < depth; ++d) {
-        uint32_t x[K], c[K];
-        uint2 pr[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            c[k] = q[k] + ((w[k] & 0xFFFu) << 3);
-            x[k] = lds32(lds, (w[k] & 0xF000u) | lane_base[k]);
-            pr[k] = lds64(lds, c[k]);
-        }
-        uint32_t moving = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            bool left = x[k] <= w[k];
-            if (x[k] == 0xFFFFFFFFu)
-                left = (w[k] & 0xFFFu) == 0 ? w[k] >= 0x10000u : mleft[(p[k] - kRankNodeB) >> 2] != 0;
-            w[k] = left ? pr[k].x : pr[k].y;
-            p[k] = c[k] + (left ? 0u : 4u);
-            q[k] = c[k];
-            moving |= w[k] & 0xFFFu;
-        }
-        if (!__any(moving != 0)) return;
-    }
-}
-
 template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
@@ -1360,25 +1096,10 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
             lane_base[r * GG + g] = lrow[r];
         }
     }
-    if constexpr (P16 == 4) {  // pair layout: pa (the root, a pair's left word) is q
-        uint32_t q[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) q[k] = pa[k];
-        if (any_nan) {
-            pair_walk_nan<K>(lds, lane_base, q, nd, pa, dmax, ml);
-        } else {
-            pair_walk<K, PIPE>(lds, lane_base, q, nd, dmax);
-#pragma unroll
-            for (int k = 0; k < K; ++k) pa[k] = q[k] + (nd[k] < 0x10000u ? 4u : 0u);  // right leaf: 2nd word
-        }
-        return;
-    }
     if (any_nan)
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
-    else if (PIPE)
-        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
     else
-        rank_walk<false, P16, K>(lds, lane_base, pa, nd, dmax, ml);
+        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
 }
 
 template <int K>
@@ -1447,15 +1168,8 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-// OCC = workgroups per CU: 2 halves the LDS budget (80 KiB: compact u16 planes + a smaller
-// node chunk) and caps the kernel at 64 VGPRs, so two 1,024-thread blocks -- 8 waves per SIMD
-// instead of 4 -- share a CU (more chunks, i.e. more row re-reads, for more issue-level
-// parallelism).
-template <int OCC>
-constexpr int kLdsBudget = OCC == 2 ? 80 * 1024 - 2048 : kLdsTotal;
-
-template <int BLOCK, int R, int G, int P16, int PIPE, int OCC = 1>
-__global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
+template <int BLOCK, int R, int G, int P16, int PIPE>
+__global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
     const int32_t *__restrict__ nan_flag, int64_t r0, int64_t r1, const double *__restrict__ lval,
@@ -1463,8 +1177,8 @@ __global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
     int32_t n_trees, int first, int last, const int32_t *__restrict__ chunk_t,
     const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n) {
-    // u32 planes: 1,024 rows x 16 slots; u16 planes: 2,048 rows x 16 slots; v2: 1,024 rows x 32 slots
-    constexpr int kPlaneRows = P16 == 1 ? 2 * kRankPlaneRows : kRankPlaneRows;
+    // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots
+    constexpr int kPlaneRows = kRankPlaneRows;
     constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
     constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS
     constexpr uint32_t kNB = kNodeB<P16>;
@@ -1480,30 +1194,26 @@ __global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
-    constexpr int kNodeWords = (kLdsBudget<OCC> - kXW * 4) / 4;
-    static_assert(OCC == 1 || P16 == 3, "two blocks per CU fit with the 32 KiB compact planes only");
+    constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
     __shared__ __align__(16) uint32_t s_mem[kXW + kNodeWords];
     uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
     const int tid = threadIdx.x;
     {
         const uint32_t *nb = nodes + node_base;
-        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = (P16 && P16 != 4) ? nb[i] ^ 0xFFFF0000u : nb[i];
+        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
     }
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
     for (int r = 0; r < R; ++r) {  // slot 15: the leaf / jump sentinel (v2 needs none)
-        if (P16 == 1)
-            s_x16[15 * kPlaneRows + r * BLOCK + tid] = (uint16_t)(kRankSentinel >> 16);
-        else if (P16 == 0)
-            s_x[15 * kRankPlaneRows + r * BLOCK + tid] = kRankSentinel;
+        if (P16 == 0) s_x[15 * kRankPlaneRows + r * BLOCK + tid] = kRankSentinel;
     }
     __syncthreads();
     const uint8_t *ml = mleft + node_base;
     const bool any_nan = *nan_flag != 0;  // uniform
     uint32_t lrow[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * ((P16 && P16 != 4) ? 2 : 4));
+    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * (P16 ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R], q2[R], q3[R];
@@ -1543,9 +1253,7 @@ __global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
 #pragma unroll
                 for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
                     const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                    if (P16 == 4)
-                        s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : (u + 1u) << 16;
-                    else if (P16)
+                    if (P16)
                         s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
                     else
                         s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
@@ -1588,6 +1296,10 @@ __global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
         FDX_RANK_TAIL(5)
         FDX_RANK_TAIL(6)
         FDX_RANK_TAIL(7)
+        FDX_RANK_TAIL(8)
+        FDX_RANK_TAIL(9)
+        FDX_RANK_TAIL(10)
+        FDX_RANK_TAIL(11)
 #undef FDX_RANK_TAIL
         if (pending) rank_accumulate<R, G>(a, pv);
         if (tv) continue;
@@ -1602,15 +1314,6 @@ __global__ void __launch_bounds__(BLOCK, OCC == 2 ? 8 : 1) k_forest_rank(
             }
         }
     }
-}
-
-int64_t forest_slab_rows() {
-    static int64_t v = [] {
-        const char *e = getenv("FDX_FOREST_SLAB_ROWS");
-        int64_t x = e ? atoll(e) : 0;
-        return x > 0 ? x : INT64_MAX;  // measured: slabbing for Infinity-Cache reuse did not pay (r01)
-    }();
-    return v;
 }
 
 float round_down_f32(double t) {
@@ -1751,7 +1454,7 @@ struct RankLayout {
 constexpr int64_t kSlotSpan = 32767;
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
-                      RankLayout &L, bool v2 = false, bool pair = false) {
+                      RankLayout &L, bool v2 = false) {
     if (!v2 && d->n_features > 15) {
         set_error("rank layout: %d features > 15", d->n_features);
         return FDX_E_UNSUPPORTED;
@@ -1777,10 +1480,6 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         auto &u = U[f];
         std::sort(u.begin(), u.end());
         u.erase(std::unique(u.begin(), u.end(), [](float a, float b) { return a == b; }), u.end());
-        if (pair && (int64_t)u.size() > kRankMaxRank) {
-            set_error("rank layout v3: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank);
-            return FDX_E_UNSUPPORTED;
-        }
         if (!v2 && (int64_t)u.size() > kRankMaxRank + 1) {
             set_error("rank layout: feature %d has %zu distinct thresholds > %d", f, u.size(), kRankMaxRank + 1);
             return FDX_E_UNSUPPORTED;
@@ -1855,65 +1554,6 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
         pend.pop_back();
         emit(w + (int64_t)((hi & 0xFFFFFFu) >> 3));
     };
-    if (pair) {
-        // v3 (see pair_walk): every tree is a run of 8-byte pairs, its root the left word of
-        // the first (the right word is never reached); pre-order over pairs, so a left child's
-        // children pair follows its own pair and the offsets are pair counts of left subtrees
-        int32_t dm = 0;
-        std::function<void(int64_t, int64_t, int32_t)> place = [&](int64_t w, int64_t pos, int32_t dep) {
-            const uint64_t nd = packed[(size_t)w];
-            if (!(nd >> 63)) {
-                double v;
-                memcpy(&v, &nd, 8);
-                L.nodes[(size_t)pos] = (pos & 1) ? 0u : 0x7FFF0000u;
-                L.orig[(size_t)pos] = worig[(size_t)w];
-                L.lval[(size_t)pos] = v;
-                dm = std::max(dm, dep);
-                return;
-            }
-            const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
-            const int f = (int)((hi >> 24) & 63);
-            float t;
-            memcpy(&t, &lo, 4);
-            const auto &u = U[f];
-            const int64_t k = std::lower_bound(u.begin(), u.end(), t) - u.begin();
-            const int64_t cp = (int64_t)L.nodes.size();
-            push(0u, -1, 0.0, 0);
-            push(0u, -1, 0.0, 0);
-            const int64_t off = cp / 2 - pos / 2;
-            if (off < 1 || off > 0xFFF) ok = false;
-            L.nodes[(size_t)pos] = ((uint32_t)(k + 1) << 16) | ((uint32_t)f << 12) | (uint32_t)(off & 0xFFF);
-            L.orig[(size_t)pos] = worig[(size_t)w];
-            L.ml[(size_t)pos] = (uint8_t)((hi >> 30) & 1);
-            place(w + 1, cp, dep + 1);
-            place(w + (int64_t)((hi & 0xFFFFFFu) >> 3), cp + 1, dep + 1);
-        };
-        for (int32_t tr = 0; tr < d->n_trees; ++tr) {
-            const int64_t tb = (int64_t)L.nodes.size();  // even: every tree is whole pairs
-            push(0u, -1, 0.0, 0);
-            push(0u, -1, 0.0, 0);
-            dm = 0;
-            place(d->node_offsets[tr], tb, 0);
-            if (!ok) {
-                set_error("rank layout v3: tree %d: a children pair is more than 4095 pairs away", tr);
-                return FDX_E_UNSUPPORTED;
-            }
-            const int64_t te = (int64_t)L.nodes.size();
-            if (te - tb > max_tree_nodes) {
-                set_error("rank layout v3: tree %d has %lld words > LDS budget %lld", tr, (long long)(te - tb),
-                          (long long)max_tree_nodes);
-                return FDX_E_UNSUPPORTED;
-            }
-            L.root.push_back((int32_t)tb);
-            L.depth.push_back(dm);
-            L.offsets.push_back(te);
-        }
-        if (L.nodes.size() >= (size_t(1) << 31)) {
-            set_error("rank layout: too many nodes");
-            return FDX_E_UNSUPPORTED;
-        }
-        return FDX_OK;
-    }
     for (int32_t tr = 0; tr < d->n_trees; ++tr) {
         const int64_t tb = (int64_t)L.nodes.size();
         margin = 2 * wdepth[(size_t)tr] + 16;
@@ -1961,15 +1601,14 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
 
 namespace fdx {
 namespace {
-int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair = false);
-// node format a variant runs on: 1 = rank layout v1, 2 = v2, 3 = v3 (sibling pairs)
-int variant_format(const Variant &v) { return v.p16 == 4 ? 3 : (v.p16 >= 2 ? 2 : 1); }
-int forest_format(const fdx_forest_s *F) { return F->rank_pair ? 3 : (F->rank_v2 ? 2 : 1); }
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
+// node format a variant runs on: 1 = rank layout v1, 2 = v2
+int variant_format(const Variant &v) { return v.p16 >= 2 ? 2 : 1; }
+int forest_format(const fdx_forest_s *F) { return F->rank_v2 ? 2 : 1; }
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
 constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
-constexpr int64_t kRankNodeCapHalf = (kLdsBudget<2> - kRankXWords * 2) / 4 - 1;  // 2 blocks per CU
 
 bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
 
@@ -1978,8 +1617,7 @@ bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; 
 // (wide layout only: a rank-layout forest has every tree within the budget by construction).
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
-    F->tile_ok = v.tile != 0;
-    const int64_t cap_nodes = v.rank ? (v.occ == 2 ? kRankNodeCapHalf : (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap))
+    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
                                      : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
@@ -1991,7 +1629,6 @@ void build_chunks(fdx_forest_s *F) {
         if (off[t + 1] - off[t] > cap_nodes) {
             c.t1 = t + 1;
             c.in_lds = false;
-            F->tile_ok = false;
         } else {
             int32_t u = t + 1;
             while (u < F->n_trees && off[u + 1] - c.node_base <= cap_nodes) ++u;
@@ -2004,7 +1641,7 @@ void build_chunks(fdx_forest_s *F) {
         t = c.t1;
     }
 }
-// Chunk table for the tile kernels (device copy; synchronous, off the hot path).
+// Chunk table for the all-chunks-at-once launch (device copy; synchronous, off the hot path).
 int upload_chunks(fdx_forest_s *F) {
     if (!F->chunk_t_d) return FDX_OK;
     std::vector<int32_t> ct(F->chunks.size() + 1);
@@ -2033,9 +1670,9 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     if (kVariants[variant].rank && variant_format(kVariants[variant]) != forest_format(F)) {
         // the variant runs on another node format: rebuild the rank layout in it
         const int want = variant_format(kVariants[variant]), had = forest_format(F);
-        int rc = install_rank_layout(F, want == 2, nullptr, want == 3);
+        int rc = install_rank_layout(F, want == 2, nullptr);
         if (rc) {
-            install_rank_layout(F, had == 2, nullptr, had == 3);  // restore the previous format
+            install_rank_layout(F, had == 2, nullptr);  // restore the previous format
             set_error("variant %d needs rank layout v%d, which this forest does not fit", variant, want);
             return FDX_E_UNSUPPORTED;
         }
@@ -2053,12 +1690,6 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
         F->variant = prev;
         build_chunks(F);
         set_error("variant %d: a tree does not fit its LDS node budget", variant);
-        return FDX_E_UNSUPPORTED;
-    }
-    if (kVariants[variant].tile && !F->tile_ok) {
-        F->variant = prev;
-        build_chunks(F);
-        set_error("variant %d: a tree does not fit the tile kernel's LDS node budget", variant);
         return FDX_E_UNSUPPORTED;
     }
     return upload_chunks(F);
@@ -2088,13 +1719,13 @@ static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL, int versio
     std::vector<int32_t> orig, root, depth;
     int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
-    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2, version == 3);
+    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2);
 }
 
 extern "C" int fdx_forest_rank_layout_size2(const fdx_forest_desc *d, int32_t version, int64_t *n_nodes,
                                             int32_t *n_thresholds, int32_t *n_slots) {
     FDX_REQUIRE(n_nodes && n_thresholds && n_slots, "null output");
-    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3");
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
     RankLayout RL;
     int rc = rank_layout_host(d, RL, version);
     if (rc) return rc;
@@ -2108,7 +1739,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
                                      int32_t *orig_out, double *leaf_value_out, uint8_t *missing_left_out,
                                      int32_t *root_out, int32_t *depth_out, float *thr_out, int32_t *thr_off_out,
                                      int32_t *slot_feat_out, int32_t *slot_base_out) {
-    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3");
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
     FDX_REQUIRE(nodes_out && orig_out && leaf_value_out && missing_left_out && root_out && depth_out && thr_off_out &&
                     slot_feat_out && slot_base_out,
                 "null output");
@@ -2134,7 +1765,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
 
 extern "C" int fdx_forest_layout(fdx_forest F, int32_t *layout, int32_t *n_slots) {
     FDX_REQUIRE(F && layout && n_slots, "null pointer");
-    *layout = !F->rank_ok ? 0 : (F->rank_pair ? 4 : (F->rank_v2 ? (F->rank_identity ? 3 : 2) : 1));
+    *layout = !F->rank_ok ? 0 : (F->rank_v2 ? (F->rank_identity ? 3 : 2) : 1);
     *n_slots = F->rank_v2 ? F->rn_slots : (F->rank_ok ? 16 : 0);
     return FDX_OK;
 }
@@ -2177,7 +1808,7 @@ namespace {
 void free_rank_buffers(fdx_forest_s *F) {
     void **bufs[] = {(void **)&F->rnodes_d, (void **)&F->rorig_d, (void **)&F->rlval_d, (void **)&F->rml_d,
                      (void **)&F->rroot_d, (void **)&F->rdepth_d, (void **)&F->rthr_d, (void **)&F->rseg_d,
-                     (void **)&F->ritab_d, (void **)&F->rrat_d, (void **)&F->rsmp_d};
+                     (void **)&F->ritab_d, (void **)&F->rrat_d, (void **)&F->rsmp_d, (void **)&F->retab_d};
     for (void **b : bufs) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
@@ -2187,20 +1818,19 @@ void free_rank_buffers(fdx_forest_s *F) {
 // Build the rank layout (v2 nodes when `v2`, else v1) from the host copy of the packed forest
 // and upload it with its search tables; synchronous (creation / set_variant, off the hot path).
 // On FDX_E_UNSUPPORTED the forest has no rank layout (rank_ok = false).
-int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair) {
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
     free_rank_buffers(F);
-    F->rank_ok = F->rank_v2 = F->rank_identity = F->rank_pair = false;
+    F->rank_ok = F->rank_v2 = F->rank_identity = false;
     fdx_forest_desc d{};
     d.n_trees = F->n_trees;
     d.n_features = F->n_features;
     d.node_offsets = F->node_offsets.data();
     RankLayout RL;
     if (v2 && F->zstride != 16) return FDX_E_UNSUPPORTED;
-    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2, pair && !v2);
+    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2);
     if (rc) return rc;
     F->rank_ok = true;
     F->rank_v2 = v2;
-    F->rank_pair = pair && !v2;
     if (v2) {
         bool ident = RL.n_slots <= 16 && RL.n_slots == F->n_features;
         for (int j = 0; j < RL.n_slots && ident; ++j) ident = RL.slot_feat[j] == j && RL.slot_base[j] == 0;
@@ -2237,6 +1867,34 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair) {
         for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
     }
     F->rnsmp = (int32_t)smp.size();
+    // Eytzinger tables of the searched features of k_zfill_grouped_w3 (15-feature forests with
+    // 16-float segments): samples padded with +inf to 2^L - 1, laid out in BFS order
+    std::vector<float> etab;
+    F->rnetab = 0;
+    if (F->n_features == 15 && seg == 16 && (!v2 || F->rank_identity)) {
+        for (int s = 0; s < 4; ++s) {
+            const int f = kW3Search[s];
+            const int32_t ns = F->rscnt[f];
+            int L = 0;
+            while (((int64_t)1 << L) - 1 < ns) ++L;
+            const int32_t m = (1 << L) - 1;
+            F->reoff[s] = (int32_t)etab.size();
+            F->relev[s] = L;
+            std::vector<float> e((size_t)m + 1, INFINITY);  // e[0] unused
+            int32_t i = 0;
+            std::function<void(int32_t)> fill = [&](int32_t k) {  // in-order walk = sorted order
+                if (k > m) return;
+                fill(2 * k);
+                e[(size_t)k] = i < ns ? smp[(size_t)(F->rsoff[f] + i)] : INFINITY;
+                ++i;
+                fill(2 * k + 1);
+            };
+            fill(1);
+            etab.insert(etab.end(), e.begin(), e.end());
+        }
+        if (etab.size() > (size_t)kMaxRankSamples) etab.clear();  // over the LDS budget: generic kernel
+        F->rnetab = (int32_t)etab.size();
+    }
     // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every
     // searched feature unconditionally (a feature without thresholds points here)
     for (int j = 0; j < 16; ++j) useg.push_back(INFINITY);
@@ -2280,6 +1938,10 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st, bool pair) {
     FDX_HIP(hipMemcpyAsync(F->rsmp_d, smp.data(), 4 * smp.size(), hipMemcpyHostToDevice, st));
     FDX_HIP(hipMemcpyAsync(F->ritab_d, itab.data(), 2 * itab.size(), hipMemcpyHostToDevice, st));
     FDX_HIP(hipMemcpyAsync(F->rrat_d, rat.data(), 2 * rat.size(), hipMemcpyHostToDevice, st));
+    if (!etab.empty()) {
+        FDX_HIP(hipMalloc(&F->retab_d, 4 * etab.size()));
+        FDX_HIP(hipMemcpyAsync(F->retab_d, etab.data(), 4 * etab.size(), hipMemcpyHostToDevice, st));
+    }
     FDX_HIP(hipMemcpyAsync(F->rnodes_d, RL.nodes.data(), 4 * rn, hipMemcpyHostToDevice, st));
     FDX_HIP(hipMemcpyAsync(F->rorig_d, RL.orig.data(), 4 * rn, hipMemcpyHostToDevice, st));
     FDX_HIP(hipMemcpyAsync(F->rlval_d, RL.lval.data(), 8 * rn, hipMemcpyHostToDevice, st));
@@ -2329,19 +1991,18 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     // Rank layout choice: v1 when the forest fits it (measured fastest on MI355X for the bench
     // model: 8.06 vs 8.68 ms for the compact v2 planes, profiles/r02_v6_ab_*.json); else v2 (more
     // than 4,096 nodes under one threshold rank or ranks past 12 bits -- the deployed model);
-    // else the wide 8-byte layout.  FDX_RANK_V2=1 tries v2 first (A/B; a v2 forest whose every
-    // feature needs one slot keeps v1's row format and runs on the compact 32 KiB planes).
-    static const bool prefer_v2 = getenv("FDX_RANK_V2") != nullptr;
-    rc = install_rank_layout(F, prefer_v2, st);
-    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, !prefer_v2, st);
+    // else the wide 8-byte layout.  (fdx_forest_set_variant switches an existing forest to the
+    // other rank format.)
+    rc = install_rank_layout(F, false, st);
+    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, true, st);
     if (rc == FDX_E_UNSUPPORTED) rc = FDX_OK;  // the wide layout serves it
     if (rc) {
         fdx_forest_destroy(F);
         return rc;
     }
     set_error("");
-    // default kernel: the rank layout when the forest fits it, else the wide 1024 x 1 x 4
-    F->variant = !F->rank_ok ? (F->zstride == 16 ? 1 : 0)
+    // default kernel: the rank layout when the forest fits it, else the wide layout
+    F->variant = !F->rank_ok ? 0
                              : (!F->rank_v2 ? kDefaultRankVariant
                                             : (F->rank_identity ? kDefaultRankCompactVariant : kDefaultRankV2Variant));
     build_chunks(F);
@@ -2390,17 +2051,7 @@ extern "C" int fdx_forest_destroy(fdx_forest F) {
     (void)hipFree(F->depth_d);
     (void)hipFree(F->chunk_t_d);
     (void)hipFree(F->chunk_base_d);
-    (void)hipFree(F->rnodes_d);
-    (void)hipFree(F->rorig_d);
-    (void)hipFree(F->rlval_d);
-    (void)hipFree(F->rml_d);
-    (void)hipFree(F->rroot_d);
-    (void)hipFree(F->rdepth_d);
-    (void)hipFree(F->rthr_d);
-    (void)hipFree(F->rseg_d);
-    (void)hipFree(F->ritab_d);
-    (void)hipFree(F->rrat_d);
-    (void)hipFree(F->rsmp_d);
+    free_rank_buffers(F);
     (void)hipFree(F->mean_d);
     (void)hipFree(F->scale_d);
     delete F;
@@ -2466,8 +2117,13 @@ static RankTab rank_tab(const fdx_forest_s *F) {
     rt.seg = F->rseg;
     rt.n_smp = F->rnsmp;
     rt.itab = F->ritab_d;
-    static const bool no_rat = getenv("FDX_PREP_NORAT") != nullptr;  // A/B switch: search the risks
-    rt.rat = no_rat ? nullptr : F->rrat_d;
+    rt.rat = F->rrat_d;
+    rt.etab = F->rnetab > 0 ? F->retab_d : nullptr;
+    rt.n_etab = F->rnetab;
+    for (int s = 0; s < 4; ++s) {
+        rt.eoff[s] = F->reoff[s];
+        rt.elev[s] = F->relev[s];
+    }
     return rt;
 }
 
@@ -2537,81 +2193,35 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
     int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
-    // Rows are processed in slabs small enough that the per-chunk re-reads of the scaled
-    // features and running sums stay in the 256 MiB Infinity Cache.
     if (rank_mode(F)) {
-        int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
         const size_t nc = F->chunks.size();
         const uint16_t *zr = reinterpret_cast<const uint16_t *>(z);
         // small batch: all chunks in one launch (grid.y = chunk) + k_tree_sum
         double *tv = nullptr;
-        if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n)) {
+        if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n))
             tv = reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + align_up(sizeof(double) * (size_t)n) + 256);
-            slab = n;
-        }
-        for (int64_t s0 = 0; s0 < n; s0 += slab) {
-            const int64_t s1 = std::min<int64_t>(n, s0 + slab);
-            for (size_t c = 0; c < (tv ? 1 : nc); ++c) {
-                const auto &ch = F->chunks[c];
-                const int first = c == 0, last = c + 1 == nc;
-#define FDX_LAUNCH_RANK2(B, R, G, P, PIPE, OCC)                                                               \
+        for (size_t c = 0; c < (tv ? 1 : nc); ++c) {
+            const auto &ch = F->chunks[c];
+            const int first = c == 0, last = c + 1 == nc;
+#define FDX_LAUNCH_RANK(B, R, G, P, PIPE)                                                                      \
     do {                                                                                                      \
-        const int64_t tiles_ = ceil_div(s1 - s0, (int64_t)(B) * (R));                                         \
-        const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu * (OCC)),         \
-                        tv ? (unsigned)nc : 1u);                                                              \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, OCC>), grid, dim3(B), 0, st, F->rnodes_d,         \
-                           ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, s0, \
-                           s1, F->rlval_d, F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees,  \
-                           first, last, F->chunk_t_d, F->chunk_base_d, tv, n);                                \
+        const int64_t tiles_ = ceil_div(n, (int64_t)(B) * (R));                                               \
+        const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu), tv ? (unsigned)nc : 1u); \
+        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,    \
+                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, (int64_t)0, n,       \
+                           F->rlval_d, F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first,  \
+                           last, F->chunk_t_d, F->chunk_base_d, tv, n);                                           \
     } while (0)
-#define FDX_LAUNCH_RANK(B, R, G, P, ...) FDX_LAUNCH_RANK2(B, R, G, P, __VA_ARGS__ + 0, 1)
-                switch (F->variant) {
-                    case 17: FDX_LAUNCH_RANK(1024, 1, 2, false); break;
-                    case 18: FDX_LAUNCH_RANK(512, 2, 2, false); break;
-                    case 19: FDX_LAUNCH_RANK(512, 2, 4, false); break;
-                    case 20: FDX_LAUNCH_RANK(1024, 1, 3, false); break;
-                    case 21: FDX_LAUNCH_RANK(768, 1, 4, false); break;
-                    case 22: FDX_LAUNCH_RANK(256, 4, 2, false); break;
-                    case 23: FDX_LAUNCH_RANK(1024, 1, 6, false); break;
-                    case 24: FDX_LAUNCH_RANK(1024, 1, 8, false); break;
-                    case 25: FDX_LAUNCH_RANK(1024, 1, 5, false); break;
-                    case 26: FDX_LAUNCH_RANK(1024, 2, 3, true); break;
-                    case 27: FDX_LAUNCH_RANK(1024, 2, 4, true); break;
-                    case 28: FDX_LAUNCH_RANK(1024, 2, 5, true); break;
-                    case 29: FDX_LAUNCH_RANK(512, 4, 3, true); break;
-                    case 30: FDX_LAUNCH_RANK(1024, 2, 2, true); break;
-                    case 31: FDX_LAUNCH_RANK(1024, 2, 3, true, 1); break;
-                    case 32: FDX_LAUNCH_RANK(1024, 2, 4, true, 1); break;
-                    case 33: FDX_LAUNCH_RANK(1024, 2, 5, true, 1); break;
-                    case 34: FDX_LAUNCH_RANK(1024, 1, 6, false, 1); break;
-                    case 35: FDX_LAUNCH_RANK(1024, 1, 4, true, 1); break;
-                    case 36: FDX_LAUNCH_RANK(1024, 1, 6, true, 1); break;
-                    case 37: FDX_LAUNCH_RANK(1024, 1, 5, false, 1); break;
-                    case 38: FDX_LAUNCH_RANK(768, 1, 6, false, 1); break;
-                    case 39: FDX_LAUNCH_RANK(512, 2, 6, false, 1); break;
-                    case 40: FDX_LAUNCH_RANK(512, 2, 4, false, 1); break;
-                    case 41: FDX_LAUNCH_RANK(1024, 1, 6, false, 2); break;
-                    case 42: FDX_LAUNCH_RANK(1024, 1, 6, false, 3); break;
-                    case 43: FDX_LAUNCH_RANK(1024, 1, 6, false, 6); break;
-                    case 44: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
-                    case 45: FDX_LAUNCH_RANK(1024, 1, 4, 2, 2); break;
-                    case 46: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
-                    case 47: FDX_LAUNCH_RANK(1024, 1, 8, 3, 2); break;
-                    case 48: FDX_LAUNCH_RANK(1024, 1, 6, 4, 0); break;
-                    case 49: FDX_LAUNCH_RANK(1024, 1, 6, 4, 1); break;
-                    case 50: FDX_LAUNCH_RANK(1024, 1, 8, 4, 1); break;
-                    case 51: FDX_LAUNCH_RANK(1024, 1, 6, 4, 2); break;
-                    case 52: FDX_LAUNCH_RANK(1024, 1, 9, 4, 2); break;
-                    case 53: FDX_LAUNCH_RANK(1024, 1, 4, 4, 1); break;
-                    case 54: FDX_LAUNCH_RANK2(1024, 1, 4, 3, 2, 2); break;
-                    case 55: FDX_LAUNCH_RANK2(1024, 1, 6, 3, 2, 2); break;
-                    case 56: FDX_LAUNCH_RANK2(1024, 1, 3, 3, 2, 2); break;
-                    default: FDX_LAUNCH_RANK(1024, 1, 4, false); break;
-                }
-#undef FDX_LAUNCH_RANK
-#undef FDX_LAUNCH_RANK2
-                FDX_LAUNCHED("k_forest_rank");
+            switch (F->variant) {
+                case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
+                case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
+                case 4: FDX_LAUNCH_RANK(1024, 1, 8, 0, 2); break;
+                case 5: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
+                case 6: FDX_LAUNCH_RANK(1024, 1, 12, 0, 2); break;
+                default: FDX_LAUNCH_RANK(1024, 1, 6, 0, 2); break;
             }
+#undef FDX_LAUNCH_RANK
+            FDX_LAUNCHED("k_forest_rank");
         }
         if (tv) {
             hipLaunchKernelGGL(k_tree_sum, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, st, tv, n, F->n_trees,
@@ -2620,60 +2230,23 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         }
         return FDX_OK;
     }
-    if (F->zstride == 16 && kVariants[F->variant].tile) {
-#define FDX_LAUNCH_TILE(B, R, G)                                                                            \
-    hipLaunchKernelGGL((k_forest_tile<16, B, R, G>), dim3((unsigned)std::min<int64_t>(ceil_div(n, (B) * (R)), 256)), \
-                       dim3(B), 0, st, F->nodes_d, F->chunk_t_d, F->chunk_base_d, (int32_t)F->chunks.size(),      \
-                       F->root_d, F->depth_d, z, flag, n, proba_d, out_perm_d, leaf_d, F->orig_d, F->n_trees)
-        switch (F->variant) {
-            case 12: FDX_LAUNCH_TILE(1024, 1, 2); break;
-            case 13: FDX_LAUNCH_TILE(512, 2, 1); break;
-            case 14: FDX_LAUNCH_TILE(512, 3, 1); break;
-            default: FDX_LAUNCH_TILE(768, 2, 1); break;
-        }
-#undef FDX_LAUNCH_TILE
-        FDX_LAUNCHED("k_forest_tile");
-        return FDX_OK;
-    }
-    const int64_t slab = F->slab_rows > 0 ? F->slab_rows : forest_slab_rows();
+    // wide layout: k_forest_chunk, one launch per chunk (an oversized tree runs from global memory)
     const size_t nc = F->chunks.size();
-    for (int64_t s0 = 0; s0 < n; s0 += slab) {
-        const int64_t s1 = std::min<int64_t>(n, s0 + slab);
-        for (size_t c = 0; c < nc; ++c) {
-            const auto &ch = F->chunks[c];
-            const int first = c == 0, last = c + 1 == nc;
-#define FDX_LAUNCH_CHUNK(FS, L, B, R, G)                                                                    \
-    do {                                                                                                    \
-        const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(s1 - s0, (int64_t)(B) * (R)), 256 * 4);    \
-        hipLaunchKernelGGL((k_forest_chunk<FS, L, B, R, G>), dim3(grid), dim3(B), 0, st, F->nodes_d,          \
-                           ch.node_base, (int32_t)ch.nodes, F->root_d, F->depth_d, ch.t0, ch.t1, z, flag, s0, s1, \
-                           acc, proba_d, out_perm_d, leaf_d, F->orig_d, F->n_trees, first, last);            \
-    } while (0)
-#define FDX_LAUNCH_VARIANT(L)                                                                               \
-    switch (F->zstride == 16 ? F->variant : -1) {                                                           \
-        case 0: FDX_LAUNCH_CHUNK(16, L, 512, 1, 4); break;                                                  \
-        case 1: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 4); break;                                                 \
-        case 2: FDX_LAUNCH_CHUNK(16, L, 512, 2, 4); break;                                                  \
-        case 3: FDX_LAUNCH_CHUNK(16, L, 512, 2, 2); break;                                                  \
-        case 4: FDX_LAUNCH_CHUNK(16, L, 256, 2, 4); break;                                                  \
-        case 5: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 3); break;                                                 \
-        case 6: FDX_LAUNCH_CHUNK(16, L, 512, 1, 3); break;                                                  \
-        case 7: FDX_LAUNCH_CHUNK(16, L, 768, 1, 3); break;                                                  \
-        case 8: FDX_LAUNCH_CHUNK(16, L, 768, 1, 4); break;                                                  \
-        case 9: FDX_LAUNCH_CHUNK(16, L, 1024, 1, 2); break;                                                 \
-        case 10: FDX_LAUNCH_CHUNK(16, L, 768, 1, 2); break;                                                 \
-        case 11: FDX_LAUNCH_CHUNK(16, L, 768, 2, 2); break;                                                 \
-        default: FDX_LAUNCH_CHUNK(32, L, 512, 1, 4); break;                                                 \
-    }
-            if (ch.in_lds) {
-                FDX_LAUNCH_VARIANT(true);
-            } else {
-                FDX_LAUNCH_VARIANT(false);
-            }
-#undef FDX_LAUNCH_VARIANT
-#undef FDX_LAUNCH_CHUNK
-            FDX_LAUNCHED("k_forest_chunk");
+    for (size_t c = 0; c < nc; ++c) {
+        const auto &ch = F->chunks[c];
+        const int first = c == 0, last = c + 1 == nc;
+#define FDX_LAUNCH_CHUNK(FS, L)                                                                              \
+    hipLaunchKernelGGL((k_forest_chunk<FS, L, 512, 1, 4>), dim3((unsigned)std::min<int64_t>(ceil_div(n, 512), 1024)), \
+                       dim3(512), 0, st, F->nodes_d, ch.node_base, (int32_t)ch.nodes, F->root_d, F->depth_d, ch.t0,  \
+                       ch.t1, z, flag, (int64_t)0, n, acc, proba_d, out_perm_d, leaf_d, F->orig_d, F->n_trees, first, \
+                       last)
+        if (F->zstride == 16) {
+            if (ch.in_lds) FDX_LAUNCH_CHUNK(16, true); else FDX_LAUNCH_CHUNK(16, false);
+        } else {
+            if (ch.in_lds) FDX_LAUNCH_CHUNK(32, true); else FDX_LAUNCH_CHUNK(32, false);
         }
+#undef FDX_LAUNCH_CHUNK
+        FDX_LAUNCHED("k_forest_chunk");
     }
     return FDX_OK;
 }
@@ -2764,13 +2337,6 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
     return FDX_OK;
 }
 
-extern "C" int fdx_forest_set_slab_rows(fdx_forest F, int64_t rows) {
-    FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(rows >= 0, "rows < 0");
-    F->slab_rows = rows;
-    return FDX_OK;
-}
-
 extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
                                           int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                           const int32_t *cust_nb_d, const double *cust_avg_d,
@@ -2785,6 +2351,7 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                 3 + 4 * n_windows);
     if (n == 0) return FDX_OK;
     FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && term_rec_d, "null pointer");
+    FDX_REQUIRE((cust_val_is_sum & ~5) == 0, "cust_val_is_sum: FDX_PREP_VAL_IS_SUM | FDX_PREP_TERM_COMPACT only");
     FDX_REQUIRE(!(cust_val_is_sum & 4) || (n_windows == 3 && ((uintptr_t)term_rec_d & 15) == 0),
                 "compact terminal records: W = 3 and a 16-byte aligned record array");
     float *z;
@@ -2795,9 +2362,8 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
-    static const bool generic = getenv("FDX_PREP_GENERIC") != nullptr;  // A/B switch
     const RankTab rt = rank_tab(F);
-    if (!generic && rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat) {
+    if (rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat && rt.etab) {
         hipLaunchKernelGGL(k_zfill_grouped_w3, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
                            cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,
                            F->mean_d, F->scale_d, (void *)z, flag, rt);

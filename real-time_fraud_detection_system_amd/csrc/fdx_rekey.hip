@@ -6,10 +6,10 @@
 // :2435-2436).  Because the input table is already in time order, a STABLE sort on the key
 // alone yields per-key time order, which is what the window kernels need.
 //
-// Per pass (8-bit digit): hist (per-tile digit counts, LDS atomics) -> device-wide
-// exclusive scan over the digit-major [256][tiles] table -> scatter (wave ballot
-// multisplit gives the stable in-tile rank; the tile is re-ordered in LDS so that the
-// global writes are runs of consecutive addresses).  All traffic is HBM-streaming.
+// Per pass (8- or 9-bit digit): hist (per-tile digit counts, wave-private counters fed by a
+// ballot multisplit) -> device-wide exclusive scan over the digit-major [bins][tiles] table ->
+// scatter (the same multisplit gives the stable in-tile rank; the tile is re-ordered in LDS
+// so that the global writes are runs of consecutive addresses).  All traffic is HBM-streaming.
 #include <algorithm>
 
 #include "fdx_internal.h"
@@ -127,69 +127,34 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
     return (uint32_t)(((k ^ flip) >> shift) & (K)((1 << BITS) - 1));
 }
 
+// Per-tile digit counts, in the scatter's blocked order (wave w counts the 1,024 consecutive
+// keys [w * 1024, (w + 1) * 1024) of the tile).  Each wave keeps its own LDS counters and, per
+// item, only the lowest lane of each group of equal digits (ballot multisplit) adds the
+// group's size: no two lanes of an instruction touch one counter, where one block-shared
+// atomicAdd per key spent ~70 % of its LDS cycles on same-address conflicts (r02 PMC).
 template <typename K, int BITS>
 __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ keys, int64_t n, int shift,
                                                        K flip, int64_t n_tiles,
                                                        uint32_t *__restrict__ hist) {
     constexpr int kBins = 1 << BITS;
-    __shared__ uint32_t s_h[kBins];
-    for (int d = threadIdx.x; d < kBins; d += kBlock) s_h[d] = 0;
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        int64_t i = base + (int64_t)k * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&s_h[digit_of<K, BITS>(keys[i], shift, flip)], 1u);
-    }
-    __syncthreads();
-    for (int d = threadIdx.x; d < kBins; d += kBlock) hist[(int64_t)d * n_tiles + blockIdx.x] = s_h[d];
-}
-
-// Stable scatter of one tile.  vals_in == nullptr means "the value is the row index" (with
-// bit 31 = flag_in[row] != 0 when flag_in is given: fdx_rekey_payload's packed flag).
-// PW > 0: PW 8-byte payload streams ride along.  After the keys are out, each stream is
-// loaded coalesced in input order, re-ordered through LDS (reusing the key/value buffers as
-// 4,096 8-byte slots) with the same tile permutation, and written to the destinations the key
-// pass computed: the same coalesced runs as the keys.  The grouped payload then reads
-// sequentially downstream, where gathering it through the permutation took a random HBM line
-// per 8-byte element (round-1 PMC: 3-6x the algorithmic bytes).
-template <typename K, int BITS, int PW>
-__global__ void __launch_bounds__(kBlock) k_radix_scatter(
-    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
-    int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
-    uint32_t *__restrict__ vals_out, const uint8_t *__restrict__ flag_in, const uint64_t *__restrict__ p0_in,
-    const uint64_t *__restrict__ p1_in, uint64_t *__restrict__ p0_out, uint64_t *__restrict__ p1_out) {
-    constexpr int kBins = 1 << BITS, kPer = kBins / kBlock;
-    static_assert(kBins % kBlock == 0, "digit bins must be a multiple of the block");
-    __shared__ uint32_t s_run[kBins];                  // digit counts of earlier rounds
-    __shared__ uint32_t s_wcnt[kWavesPerBlock][kBins]; // this round's per-wave counts
-    __shared__ uint32_t s_start[kBins];                // tile-local digit starts
-    // keys | values; later re-used as 4,096 8-byte payload slots (>= 8 bytes per element)
-    constexpr int kKeyWords = (int)(sizeof(K) / 4);
-    __shared__ __align__(16) uint32_t s_kv[(kKeyWords + 1) * kTile];
-    K *s_key = reinterpret_cast<K *>(s_kv);
-    uint32_t *s_val = s_kv + kKeyWords * kTile;
-
+    constexpr int kWaveSpan = kTile / kWavesPerBlock;
+    __shared__ uint32_t s_h[kWavesPerBlock][kBins];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    for (int d = tid; d < kBins; d += kBlock) {
-        s_run[d] = 0;
-#pragma unroll
-        for (int w = 0; w < kWavesPerBlock; ++w) s_wcnt[w][d] = 0;
-    }
+    for (int d = tid; d < kWavesPerBlock * kBins; d += kBlock) (&s_h[0][0])[d] = 0;
     __syncthreads();
-
-    K key[kItems];
-    uint32_t val[kItems], rank[kItems];
+    const int64_t wbase = (int64_t)blockIdx.x * kTile + (int64_t)wv * kWaveSpan + lane;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t *h = s_h[wv];
+    K key[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const int64_t i = base + (int64_t)r * kBlock + tid;
-        const bool valid = i < n;
-        key[r] = valid ? keys_in[i] : (K)0;
-        val[r] = valid ? (vals_in ? vals_in[i] : ((uint32_t)i | (flag_in && flag_in[i] ? 0x80000000u : 0u))) : 0u;
+        const int64_t i = wbase + (int64_t)r * kWave;
+        key[r] = i < n ? keys[i] : (K)0;
+    }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const bool valid = wbase + (int64_t)r * kWave < n;
         const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
-        // peers: lanes of this wave holding the same digit (wave multisplit by ballots)
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < BITS; ++b) {
@@ -197,106 +162,35 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
             const uint64_t bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t in_wave = (uint32_t)__popcll(peers & lt_mask);
-        if (valid && in_wave == 0) s_wcnt[wv][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pre = s_run[d];
-            for (int w = 0; w < wv; ++w) pre += s_wcnt[w][d];
-            rank[r] = pre + in_wave;
-        }
-        __syncthreads();
-        for (int dd = tid; dd < kBins; dd += kBlock) {
-            uint32_t s = 0;
-#pragma unroll
-            for (int w = 0; w < kWavesPerBlock; ++w) {
-                s += s_wcnt[w][dd];
-                s_wcnt[w][dd] = 0;
-            }
-            s_run[dd] += s;
-        }
-        __syncthreads();
-    }
-    // tile-local digit starts = exclusive scan of s_run over digits (kPer consecutive
-    // digits per thread)
-    {
-        uint32_t c[kPer], sum = 0;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            c[q] = s_run[tid * kPer + q];
-            sum += c[q];
-        }
-        uint32_t tot;
-        uint32_t ex = block_excl_scan(sum, &tot);
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            s_start[tid * kPer + q] = ex;
-            ex += c[q];
-        }
+        if (valid && (peers & lt_mask) == 0) h[d] += (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    uint32_t pos[kItems];  // tile position of each of this thread's items (payload re-order)
+    for (int d = tid; d < kBins; d += kBlock) {
+        uint32_t c = 0;
 #pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const int64_t i = base + (int64_t)r * kBlock + tid;
-        if (i < n) {
-            const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
-            const uint32_t p = s_start[d] + rank[r];
-            pos[r] = p;
-            s_key[p] = key[r];
-            s_val[p] = val[r];
-        }
-    }
-    __syncthreads();
-    const int64_t cnt = std::min<int64_t>(kTile, n - base);
-    int32_t dsts[kItems];  // destination of tile position tid + j * kBlock
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-        const int p = tid + j * kBlock;
-        if (p < cnt) {
-            const K k = s_key[p];
-            const uint32_t d = digit_of<K, BITS>(k, shift, flip);
-            const int64_t dst = (int64_t)offsets[(int64_t)d * n_tiles + blockIdx.x] + (p - s_start[d]);
-            dsts[j] = (int32_t)dst;
-            keys_out[dst] = k;
-            vals_out[dst] = s_val[p];
-        }
-    }
-    if constexpr (PW > 0) {
-        uint64_t *s_pay = reinterpret_cast<uint64_t *>(s_kv);
-#pragma unroll
-        for (int q = 0; q < PW; ++q) {
-            const uint64_t *pin = q == 0 ? p0_in : p1_in;
-            uint64_t *pout = q == 0 ? p0_out : p1_out;
-            uint64_t v[kItems];
-#pragma unroll
-            for (int r = 0; r < kItems; ++r) {  // coalesced, input order
-                const int64_t i = base + (int64_t)r * kBlock + tid;
-                v[r] = i < n ? pin[i] : 0ull;
-            }
-            __syncthreads();  // the previous contents of the LDS slots are consumed
-#pragma unroll
-            for (int r = 0; r < kItems; ++r)
-                if (base + (int64_t)r * kBlock + tid < n) s_pay[pos[r]] = v[r];
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < kItems; ++j) {
-                const int p = tid + j * kBlock;
-                if (p < cnt) pout[dsts[j]] = s_pay[p];
-            }
-        }
+        for (int w = 0; w < kWavesPerBlock; ++w) c += s_h[w][d];
+        hist[(int64_t)d * n_tiles + blockIdx.x] = c;
     }
 }
 
-// The same stable scatter with a BLOCKED tile: wave w owns the 1,024 consecutive input
-// positions [w * 1024, (w + 1) * 1024) of the tile (item r of lane l at w * 1024 + r * 64 + l,
-// still coalesced loads).  Input order inside the tile is then (wave, item, lane), so each
+// Stable scatter of one tile (BLOCKED: wave w owns the 1,024 consecutive input positions
+// [w * 1024, (w + 1) * 1024) of the tile, item r of lane l at w * 1024 + r * 64 + l -- still
+// coalesced loads).  vals_in == nullptr means "the value is the row index" (with bit 31 =
+// flag_in[row] != 0 when flag_in is given: fdx_rekey_payload's packed flag).  PW > 0: PW
+// 8-byte payload streams ride along: after the keys are out, each stream is loaded coalesced
+// in input order, re-ordered through LDS (reusing the key/value buffers as 4,096 8-byte slots)
+// with the same tile permutation, and written to the destinations the key pass computed --
+// the same coalesced runs as the keys, so the grouped payload reads sequentially downstream
+// (gathering it through the permutation took a random HBM line per 8-byte element: round-1
+// PMC 3-6x the algorithmic bytes).  Input order inside the tile is then (wave, item, lane), so each
 // wave ranks its 16 items against wave-private digit counters (ballot multisplit; the leader
 // lane of each digit group bumps the counter) with no block barrier, and one barrier later the
 // per-digit scan over the four waves' counts gives each wave its offset: 3 barriers per tile
-// instead of 3 per item.  The tile's global digit offsets are staged in LDS once.
+// instead of 3 per item (measured on MI355X at config 2: terminal re-key 0.686 -> 0.611 ms,
+// 64-bit argsort 2.43 -> 1.59 ms, customer re-key unchanged; bit-identical,
+// tools/radix_ab.py).  The tile's global digit offsets are staged in LDS once.
 template <typename K, int BITS, int PW>
-__global__ void __launch_bounds__(kBlock) k_radix_scatter_b(
+__global__ void __launch_bounds__(kBlock) k_radix_scatter(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, int64_t n, int shift, K flip,
     int64_t n_tiles, const uint32_t *__restrict__ offsets, K *__restrict__ keys_out,
     uint32_t *__restrict__ vals_out, const uint8_t *__restrict__ flag_in, const uint64_t *__restrict__ p0_in,
@@ -529,18 +423,8 @@ template <typename K, int BITS, int PW>
 void launch_scatter(const K *kin, const uint32_t *vin, int64_t n, int shift, K flip, int64_t tiles,
                     const uint32_t *hist, K *kout, uint32_t *vout, const uint8_t *flag_in, const uint64_t *const (&pin)[2],
                     uint64_t *const (&pout)[2], hipStream_t st) {
-    // A/B switch: FDX_RADIX_BLOCKED=1 selects the blocked-tile scatter (k_radix_scatter_b; not yet
-    // validated on the GPU -- the default stays the per-item-ranking kernel until it is)
-    static const bool blocked = [] {
-        const char *e = getenv("FDX_RADIX_BLOCKED");
-        return e && atoi(e) != 0;
-    }();
-    if (!blocked)
-        hipLaunchKernelGGL((k_radix_scatter<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
-                           shift, flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
-    else
-        hipLaunchKernelGGL((k_radix_scatter_b<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n,
-                           shift, flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
+    hipLaunchKernelGGL((k_radix_scatter<K, BITS, PW>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, vin, n, shift,
+                       flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
 }
 
 template <typename K>
@@ -549,8 +433,7 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
                const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr) {
     const int64_t tiles = ceil_div(n, kTile);
     // 9-bit digits when they need fewer passes than 8-bit ones (17- and 18-bit keys: 2, not 3)
-    static const bool only8 = getenv("FDX_RADIX_8BIT") != nullptr;  // A/B switch
-    const int dbits = (!only8 && (bits + 8) / 9 < (bits + kRadixBits - 1) / kRadixBits) ? 9 : kRadixBits;
+    const int dbits = ((bits + 8) / 9 < (bits + kRadixBits - 1) / kRadixBits) ? 9 : kRadixBits;
     const int passes = (bits + dbits - 1) / dbits;
     const K *kin = keys;
     const uint32_t *vin = nullptr;  // identity on the first pass

@@ -496,17 +496,3 @@ extern "C" int fdx_stream_status_async(fdx_stream s, int32_t *flags_pinned_h, vo
     return FDX_OK;
 }
 
-// A HIP stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask): the
-// scoring pipeline can run its two overlapped halves on disjoint CU sets.
-extern "C" int fdx_hip_stream_create_cu_mask(const uint32_t *cu_mask, int32_t n_words, void **stream_out) {
-    FDX_REQUIRE(cu_mask && stream_out && n_words > 0, "bad argument");
-    hipStream_t s = nullptr;
-    FDX_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, cu_mask));
-    *stream_out = s;
-    return FDX_OK;
-}
-
-extern "C" int fdx_hip_stream_destroy(void *stream) {
-    if (stream) FDX_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
-    return FDX_OK;
-}

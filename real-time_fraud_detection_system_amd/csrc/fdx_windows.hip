@@ -294,6 +294,9 @@ __global__ void __launch_bounds__(256) k_interleave(
 // leave the window are read from LDS.  A trailing row older than the ring (window
 // occupancy > kRing - kChunk rows) is copied from global memory instead (correct, slower).
 constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
+// walk length classes: groups whose longest segment has >= kWalkSplitRows rows use the 256-row
+// ring on the fork stream (fdx_customer_windows_walk)
+constexpr int kWalkSplitRows = 480;
 
 // kRing rows per segment stay in LDS.  Launched once per ring size over length classes of
 // groups (a block outside [lg_min, lg_max) exits at once): long segments belong to busy
@@ -446,75 +449,14 @@ __global__ void __launch_bounds__(64) k_customer_ring(
 }
 
 // ---------------------------------------------------- customer windows, two-pass form
-// Pass 1 (k_customer_starts, fully parallel): pandas' variable-window start of every row,
-//   start_w(t) = first row j of the segment with ts_j > ts_t - W_w   (closed='right'),
-// written into the nb output array (same [W][n_slots] int32 shape; pass 2 overwrites each
-// entry with the count after reading it).  One wave per 16 interleaved rows; each lane (one
-// segment x window) binary-searches its first row's start, then advances it row by row.
+// Pass 1 (k_interleave<true, ...>, in the layout kernel): pandas' variable-window start of
+//   every row, start_w(t) = first row j of the segment with ts_j > ts_t - W_w (closed='right').
 // Pass 2 (k_customer_walk): the exact Kahan add/remove recurrence, one lane per (segment,
-// window) -- the only sequential part -- now free of timestamp compares: per row it removes
+// window) -- the only sequential part -- free of timestamp compares: per row it removes
 // rows [start(t-1), start(t)) (or re-initialises when start(t) == t) and adds row t.  Only
 // the amounts ride in the LDS ring (8 B per row), so more waves fit per CU.
-__global__ void __launch_bounds__(256) k_customer_starts(
-    const int64_t *__restrict__ its, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
-    const uint32_t *__restrict__ goff, int64_t n_groups, int64_t n_seg, int32_t S, int64_t n_slots, WinArgs win,
-    int32_t n_win, int32_t *__restrict__ starts) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int64_t rho0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) * kChunk;
-    const int64_t n_rows = n_slots / S;
-    if (rho0 >= n_rows) return;
-    const int l = lane / n_win, wi = lane - l * n_win;
-    if (l >= S) return;
-    int64_t W = win.w[0];
-#pragma unroll
-    for (int i = 1; i < FDX_MAX_WINDOWS; ++i) W = wi == i ? win.w[i] : W;
-    // group of row rho0: the last g with goff[g] <= rho0 * S
-    int64_t lo = 0, hi = n_groups;
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)goff[mid] <= rho0 * S) lo = mid; else hi = mid;
-    }
-    int64_t g = lo;
-    int64_t gbase = goff[g], grows = ((int64_t)goff[g + 1] - gbase) / S;
-    auto seg_len = [&](int64_t gg) -> int32_t {
-        const int64_t si = gg * S + l;
-        if (si >= n_seg) return 0;
-        const int64_t sg = sorder[si];
-        return (int32_t)(seg_off[sg + 1] - seg_off[sg]);
-    };
-    int32_t L = seg_len(g);
-    int32_t t = (int32_t)(rho0 - gbase / S);
-    int32_t st = -1;  // start of the previous row of this lane (-1: not known yet)
-    for (int j = 0; j < kChunk && rho0 + j < n_rows; ++j) {
-        if (t == grows) {  // next group
-            ++g;
-            gbase = goff[g];
-            grows = ((int64_t)goff[g + 1] - gbase) / S;
-            L = seg_len(g);
-            t = 0;
-            st = -1;
-        }
-        if (t < L) {
-            const int64_t *ts = its + gbase + l;  // row k of this lane's segment: ts[k * S]
-            const int64_t bound = ts[(int64_t)t * S] - W;
-            if (st < 0) {
-                int32_t a = 0, b = t;  // first k in [0, t] with ts[k] > bound (k = t qualifies)
-                while (a < b) {
-                    const int32_t m = (a + b) >> 1;
-                    if (ts[(int64_t)m * S] > bound) b = m; else a = m + 1;
-                }
-                st = a;
-            } else {
-                while (ts[(int64_t)st * S] <= bound) ++st;
-            }
-            starts[(int64_t)wi * n_slots + gbase + (int64_t)t * S + l] = st;
-        }
-        ++t;
-    }
-}
-
-// starts == nullptr: the starts are in nb_out (k_customer_starts, slot layout) and are
-// overwritten by the counts; else segment-contiguous (k_interleave<true>).
+// starts: segment-contiguous (k_interleave<true>); nullptr = in nb_out, slot layout, overwritten
+// by the counts.
 template <int S_MAX, int kRing>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
@@ -895,8 +837,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
     int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out,
-    int32_t *__restrict__ scratch, const int32_t *__restrict__ dmap, int64_t len_lo, int64_t len_hi,
-    int64_t compact_n) {
+    int32_t *__restrict__ scratch, int64_t len_lo, int64_t len_hi, int64_t compact_n) {
     static_assert(LR % kWave == 0 && LR <= 32768, "the merge packs a staging index in 15 bits");
     constexpr int kMaxRunsLong = 2 * LR - 1;  // a long segment's run list in the stage's ts words
     __shared__ int64_t s_ts[kTermWaves][LR];
@@ -911,10 +852,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
     int64_t *lts = s_ts[wv];
     int32_t *lf = s_f[wv];
     auto fraud_of = [&](int64_t q) -> int { return gfraud ? (gfraud[q] != 0) : (int)((uint32_t)rows[q] >> 31); };
-    auto dest_of = [&](int64_t q) -> int64_t {
-        const int64_t r = rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q;
-        return dmap ? (int64_t)dmap[r] : r;  // dmap: row -> record position (e.g. its scoring slot)
-    };
+    auto dest_of = [&](int64_t q) -> int64_t { return rows ? (int64_t)(rows[q] & 0x7FFFFFFF) : q; };
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1208,86 +1146,38 @@ extern "C" int fdx_customer_windows(const int64_t *ts_ns_d, const double *amount
 
 // Every terminal-window launch: the short-segment pass (<= kTermShortRows rows, small LDS
 // stage, more resident waves) then the long pass (the 1,024-row stage, global memory beyond);
-// each skips the other's segments.  FDX_TERM_SPLIT=0: one launch with the 1,024-row stage.
+// each skips the other's segments.
 static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, const int32_t *rows,
                             const int64_t *seg_off, int64_t n_seg, int64_t n, int64_t delay_ns, const WinArgs &wa,
                             int32_t n_windows, int32_t *nb_d, double *risk_d, int64_t *rec_d, int32_t *scratch,
-                            const int32_t *dmap, hipStream_t st, int64_t compact_n = 0) {
-    static const bool split = [] {
-        const char *e = getenv("FDX_TERM_SPLIT");
-        return !(e && atoi(e) == 0);
-    }();
+                            hipStream_t st, int64_t compact_n = 0) {
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n_seg, kTermWaves), 256 * 16);
-    const int64_t lo = split ? kTermShortRows : 0, inf = INT64_MAX;
+    const int64_t lo = kTermShortRows, inf = INT64_MAX;
 #define FDX_TERM_LAUNCH(R, LRV, A, B)                                                                           \
     hipLaunchKernelGGL((k_terminal_g<R, LRV>), dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off, n_seg, \
-                       n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, dmap, (int64_t)(A), (int64_t)(B), \
+                       n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch, (int64_t)(A), (int64_t)(B), \
                        compact_n)
     if (runs) {
-        if (split) FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
+        FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
     } else {
-        if (split) FDX_TERM_LAUNCH(false, kTermShortRows, 0, kTermShortRows);
+        FDX_TERM_LAUNCH(false, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(false, kTermLdsRows, lo, inf);
     }
 #undef FDX_TERM_LAUNCH
 }
 
-// The input-order entry points (round 1's interface: ts / fraud in input order, segments
-// through the re-key perm) run the grouped kernel: a gather puts ts / fraud / destination in
-// grouped order first (stream-ordered temporaries), so every terminal kernel is k_terminal_g.
-__global__ void k_term_gather(const int64_t *__restrict__ ts, const uint8_t *__restrict__ fraud,
-                              const int32_t *__restrict__ rows, const int32_t *__restrict__ dest, int64_t n,
-                              int64_t *__restrict__ gts, uint8_t *__restrict__ gfr, int32_t *__restrict__ grow) {
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t src = rows ? rows[q] : q;
-        gts[q] = ts[src];
-        gfr[q] = fraud[src];
-        grow[q] = dest ? dest[src] : (int32_t)src;
-    }
+extern "C" size_t fdx_terminal_windows_workspace_size(int64_t n) {
+    return round_up((size_t)(n > 0 ? n : 0) * 4, 256) + 256;
 }
 
-static int terminal_input_order(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
-                                const int32_t *dest_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
-                                int64_t delay_ns, const WinArgs &wa, int32_t n_windows, bool runs, int32_t *nb_d,
-                                double *risk_d, int64_t *rec_d, hipStream_t st) {
-    const bool gather = row_d || dest_d;
-    const size_t b_ts = gather ? round_up((size_t)n * 8, 256) : 0;
-    const size_t b_fr = gather ? round_up((size_t)n, 256) : 0;
-    const size_t b_row = gather ? round_up((size_t)n * 4, 256) : 0;
-    const size_t bytes = b_ts + b_fr + b_row + round_up((size_t)n * 4, 256);
-    char *tmp = nullptr;
-    hipError_t e = hipMallocAsync((void **)&tmp, bytes, st);
-    if (e != hipSuccess) {
-        set_error("hipMallocAsync(%zu) failed: %s", bytes, hipGetErrorString(e));
-        return FDX_E_HIP;
-    }
-    const int64_t *gts = ts_ns_d;
-    const uint8_t *gfr = fraud_d;
-    const int32_t *grow = nullptr;
-    if (gather) {
-        hipLaunchKernelGGL(k_term_gather, dim3(stream_grid(n, 256)), dim3(256), 0, st, ts_ns_d, fraud_d, row_d,
-                           dest_d, n, (int64_t *)tmp, (uint8_t *)(tmp + b_ts), (int32_t *)(tmp + b_ts + b_fr));
-        gts = (const int64_t *)tmp;
-        gfr = (const uint8_t *)(tmp + b_ts);
-        grow = (const int32_t *)(tmp + b_ts + b_fr);
-    }
-    int32_t *scratch = (int32_t *)(tmp + b_ts + b_fr + b_row);
-    terminal_launch(runs, gts, gfr, grow, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, scratch,
-                    nullptr, st);
-    e = hipGetLastError();
-    (void)hipFreeAsync(tmp, st);
-    if (e != hipSuccess) {
-        set_error("k_terminal_g launch failed: %s", hipGetErrorString(e));
-        return FDX_E_HIP;
-    }
-    return FDX_OK;
-}
-
+// Grouped rows (time order inside each segment): the grouped kernel, its long-segment prefix
+// counts in the caller's workspace.
 extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud_d,
                                     const int64_t *seg_off_d, int64_t n_seg, int64_t n,
                                     int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
-                                    int32_t *nb_d, double *risk_d, void *stream) {
+                                    int32_t *nb_d, double *risk_d, void *workspace_d, size_t workspace_bytes,
+                                    void *stream) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -1295,75 +1185,21 @@ extern "C" int fdx_terminal_windows(const int64_t *ts_ns_d, const uint8_t *fraud
     FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
     if (n_seg == 0 || n == 0) return FDX_OK;
     FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && nb_d && risk_d, "null pointer");
-    return terminal_input_order(ts_ns_d, fraud_d, nullptr, nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows,
-                                false, nb_d, risk_d, nullptr, as_stream(stream));
-}
-
-static int terminal_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d, const int32_t *row_d,
-                           const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                           const int64_t *window_ns, int32_t n_windows, int64_t *rec_d, bool sort, void *stream,
-                           const int32_t *dest_d = nullptr) {
-    WinArgs wa;
-    int rc = check_windows(window_ns, n_windows, &wa);
-    if (rc) return rc;
-    FDX_REQUIRE(delay_ns > 0, "delay must be > 0 ns");
-    FDX_REQUIRE(n_seg >= 0 && n >= 0, "negative size");
-    if (n_seg == 0 || n == 0) return FDX_OK;
-    FDX_REQUIRE(ts_ns_d && fraud_d && seg_off_d && rec_d, "null pointer");
-    return terminal_input_order(ts_ns_d, fraud_d, row_d, dest_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, sort,
-                                nullptr, nullptr, rec_d, as_stream(stream));
-}
-
-extern "C" int fdx_terminal_windows_packed(const int64_t *ts_ns_d, const uint8_t *fraud_d,
-                                           const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg, int64_t n,
-                                           int64_t delay_ns, const int64_t *window_ns, int32_t n_windows,
-                                           int64_t *rec_d, void *stream) {
-    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
-                           false, stream);
-}
-
-extern "C" int fdx_terminal_windows_packed_dest(const int64_t *ts_ns_d, const uint8_t *fraud_d,
-                                                const int32_t *row_d, const int32_t *dest_d, const int64_t *seg_off_d,
-                                                int64_t n_seg, int64_t n, int64_t delay_ns, const int64_t *window_ns,
-                                                int32_t n_windows, int64_t *rec_d, void *stream) {
-    FDX_REQUIRE(dest_d, "null dest");
-    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
-                           false, stream, dest_d);
-}
-
-__global__ void k_invert_slots(const int32_t *__restrict__ irow, int64_t n_slots, int32_t *__restrict__ slot_of,
-                               int64_t n_rows) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_slots;
-         s += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t r = irow[s];
-        if (r >= 0 && r < n_rows) slot_of[r] = (int32_t)s;
+    const size_t need = fdx_terminal_windows_workspace_size(n);
+    if (!workspace_d || workspace_bytes < need) {
+        set_error("terminal windows workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
     }
-}
-
-extern "C" int fdx_invert_slots(const int32_t *irow_d, int64_t n_slots, int32_t *slot_of_d, int64_t n_rows,
-                                void *stream) {
-    FDX_REQUIRE(n_slots >= 0 && n_rows >= 0, "negative size");
-    if (n_slots == 0) return FDX_OK;
-    FDX_REQUIRE(irow_d && slot_of_d, "null pointer");
-    hipLaunchKernelGGL(k_invert_slots, dim3(stream_grid(n_slots, 256)), dim3(256), 0, as_stream(stream), irow_d,
-                       n_slots, slot_of_d, n_rows);
-    FDX_LAUNCHED("k_invert_slots");
+    terminal_launch(false, ts_ns_d, fraud_d, nullptr, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d,
+                    nullptr, reinterpret_cast<int32_t *>(workspace_d), as_stream(stream));
+    FDX_LAUNCHED("k_terminal_g");
     return FDX_OK;
-}
-
-extern "C" int fdx_terminal_windows_packed_unsorted(const int64_t *ts_ns_d, const uint8_t *fraud_d,
-                                                    const int32_t *row_d, const int64_t *seg_off_d, int64_t n_seg,
-                                                    int64_t n, int64_t delay_ns, const int64_t *window_ns,
-                                                    int32_t n_windows, int64_t *rec_d, void *stream) {
-    return terminal_packed(ts_ns_d, fraud_d, row_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, rec_d,
-                           true, stream);
 }
 
 static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const int32_t *rows_d,
                             const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
                             const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d, double *risk_d,
-                            int64_t *rec_d, int32_t *scratch_d, const int32_t *dest_map_d, void *stream,
-                            bool compact = false) {
+                            int64_t *rec_d, int32_t *scratch_d, void *stream, bool compact = false) {
     WinArgs wa;
     int rc = check_windows(window_ns, n_windows, &wa);
     if (rc) return rc;
@@ -1373,11 +1209,10 @@ static int terminal_grouped(const int64_t *gts_d, const uint8_t *gfraud_d, const
     FDX_REQUIRE(gts_d && seg_off_d && scratch_d, "null pointer");
     FDX_REQUIRE(gfraud_d || rows_d, "fraud comes from gfraud_d or bit 31 of rows_d");
     FDX_REQUIRE(rec_d || (nb_d && risk_d), "no output");
-    FDX_REQUIRE(!dest_map_d || rec_d, "dest_map_d places count records");
-    FDX_REQUIRE(!compact || (rec_d && n_windows == 3 && !dest_map_d && ((uintptr_t)rec_d & 15) == 0),
-                "compact records: W = 3, a 16-byte aligned record array, records by row");
+    FDX_REQUIRE(!compact || (rec_d && n_windows == 3 && ((uintptr_t)rec_d & 15) == 0),
+                "compact records: W = 3, a 16-byte aligned record array");
     terminal_launch(runs != 0, gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d,
-                    rec_d, scratch_d, dest_map_d, as_stream(stream), compact ? n : 0);
+                    rec_d, scratch_d, as_stream(stream), compact ? n : 0);
     FDX_LAUNCHED("k_terminal_g");
     return FDX_OK;
 }
@@ -1387,7 +1222,7 @@ extern "C" int fdx_terminal_windows_grouped(const int64_t *gts_d, const uint8_t 
                                             const int64_t *window_ns, int32_t n_windows, int32_t runs, int32_t *nb_d,
                                             double *risk_d, int64_t *rec_d, int32_t *scratch_d, void *stream) {
     return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs, nb_d,
-                            risk_d, rec_d, scratch_d, nullptr, stream);
+                            risk_d, rec_d, scratch_d, stream);
 }
 
 extern "C" int fdx_terminal_windows_grouped_compact(const int64_t *gts_d, const uint8_t *gfraud_d,
@@ -1396,17 +1231,7 @@ extern "C" int fdx_terminal_windows_grouped_compact(const int64_t *gts_d, const 
                                                     int32_t n_windows, int32_t runs, int64_t *rec_d,
                                                     int32_t *scratch_d, void *stream) {
     return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs,
-                            nullptr, nullptr, rec_d, scratch_d, nullptr, stream, true);
-}
-
-extern "C" int fdx_terminal_windows_grouped_dest(const int64_t *gts_d, const uint8_t *gfraud_d,
-                                                 const int32_t *rows_d, const int32_t *dest_map_d,
-                                                 const int64_t *seg_off_d, int64_t n_seg, int64_t n, int64_t delay_ns,
-                                                 const int64_t *window_ns, int32_t n_windows, int32_t runs,
-                                                 int64_t *rec_d, int32_t *scratch_d, void *stream) {
-    FDX_REQUIRE(dest_map_d, "null dest_map_d");
-    return terminal_grouped(gts_d, gfraud_d, rows_d, seg_off_d, n_seg, n, delay_ns, window_ns, n_windows, runs,
-                            nullptr, nullptr, rec_d, scratch_d, dest_map_d, stream);
+                            nullptr, nullptr, rec_d, scratch_d, stream, true);
 }
 
 extern "C" int fdx_assemble_features(int64_t n, int32_t n_windows, const double *amount_d,
@@ -1590,7 +1415,7 @@ extern "C" int fdx_customer_windows_scan(const int64_t *gts_d, const double *gam
 // Created at the HIGH priority level: HIP gives each priority level its own pool of
 // GPU_MAX_HW_QUEUES hardware queues, and a normal-priority stream created after torch's and
 // RCCL's was measured on the caller's own hardware queue (rocprofv3 Queue_Id) -- the two
-// walks then ran back to back.  FDX_FORK_PRIORITY=0 restores the normal level (A/B runs).
+// walks then ran back to back.
 struct ForkStream {
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -1604,9 +1429,8 @@ static int fork_stream(ForkStream **out) {
     if (!f.side) {
         int least = 0, greatest = 0;
         FDX_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        const char *e = getenv("FDX_FORK_PRIORITY");
-        const int prio = (e && atoi(e) == 0) ? 0 : greatest;
-        FDX_HIP(hipStreamCreateWithPriority(&f.side, hipStreamNonBlocking, prio));
+        (void)least;
+        FDX_HIP(hipStreamCreateWithPriority(&f.side, hipStreamNonBlocking, greatest));
         FDX_HIP(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming));
         FDX_HIP(hipEventCreateWithFlags(&f.join, hipEventDisableTiming));
     }
@@ -1629,17 +1453,8 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     // longest window holds more rows than the 128-row ring minus a chunk, so nearly every
     // removal would miss the ring and wait on a dependent global load) walk with a 256-row
     // ring on a forked stream, concurrently with the rest on the 128-row ring (twice the
-    // blocks per CU).  FDX_CUSTOMER_WALK_SPLIT = the class boundary in rows (0 = one launch).
-    static const int split = [] {
-        const char *e = getenv("FDX_CUSTOMER_WALK_SPLIT");
-        return e ? atoi(e) : 480;
-    }();
-    if (split <= 0) {
-        hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d, seg_off_d,
-                           sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, 0, INT32_MAX);
-        FDX_LAUNCHED("k_customer_walk");
-        return FDX_OK;
-    }
+    // blocks per CU); the class boundary is kWalkSplitRows.
+    constexpr int split = kWalkSplitRows;
     ForkStream *f;
     int rc = fork_stream(&f);
     if (rc) return rc;
@@ -1669,57 +1484,21 @@ extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const doub
     FDX_REQUIRE(its_d && iamt_d && seg_off_d && sorder_d && goff_d && nb_d && avg_d, "null pointer");
     const int32_t S = kWave / n_windows;
     const int64_t n_groups = ceil_div(n_seg, S);
-    // Length classes (segment rows Lg of a group's longest segment): groups with Lg >= split
-    // get a 192-row ring (2 waves per CU, no ring misses at config 2), the rest a 96-row ring
-    // (4 per CU).  Measured (r01, config 2): occupancy wins -- all groups on the 96-row ring
-    // 1.74 ms, split at 320 rows 2.48 ms, all on 192 rows 2.33 ms -- so the default sends
-    // every group to the 96-row ring (FDX_CUSTOMER_RING_SPLIT overrides).
-    static const int split_env = [] {
-        const char *e = getenv("FDX_CUSTOMER_RING_SPLIT");
-        return e ? atoi(e) : INT32_MAX;
-    }();
+    // One pass per group (the ring kernel: window starts found in the walk itself) -- the form
+    // for any window count; the scoring pipeline's 3-window layouts use the two-kernel
+    // layout-starts + fdx_customer_windows_walk instead.  Ring rows: measured (r01, config 2)
+    // 96 rows for every group 1.74 ms (occupancy wins), a 192-row ring for the longest groups
+    // 2.33-2.48 ms.
     hipStream_t st = as_stream(stream);
-    static const int walk_env = [] {  // FDX_CUSTOMER_WALK=0: the one-pass ring kernel instead
-        const char *e = getenv("FDX_CUSTOMER_WALK");
-        return e ? atoi(e) : 1;
-    }();
-    if (walk_env && S <= 21) {
-        const int64_t n_rows = n_slots / S;
-        const int64_t waves = ceil_div(n_rows, (int64_t)kChunk);
-        hipLaunchKernelGGL(k_customer_starts, dim3((unsigned)ceil_div(waves * kWave, (int64_t)256)), dim3(256), 0, st,
-                           its_d, seg_off_d, sorder_d, goff_d, n_groups, n_seg, S, n_slots, wa, n_windows, nb_d);
-        FDX_LAUNCHED("k_customer_starts");
-        if (walk_env == 256)
-            hipLaunchKernelGGL((k_customer_walk<21, 256>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
-                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d,
-                               (const int32_t *)nullptr);
-        else
-            hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d,
-                               seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, avg_d,
-                               (const int32_t *)nullptr);
-        FDX_LAUNCHED("k_customer_walk");
-        return FDX_OK;
-    }
-#define FDX_RING(SM, RG, LO, HI)                                                                          \
+#define FDX_RING(SM, RG)                                                                                   \
     hipLaunchKernelGGL((k_customer_ring<SM, RG>), dim3((unsigned)n_groups), dim3(64), 0, st, its_d, iamt_d, seg_off_d, \
-                       sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d, (int32_t)(LO), (int32_t)(HI))
-    if (S <= 21) {
-        static const int small_env = [] {  // FDX_CUSTOMER_RING: rows of the small ring (64 / 96 / 128)
-            const char *e = getenv("FDX_CUSTOMER_RING");
-            return e ? atoi(e) : 96;
-        }();
-        if (split_env < INT32_MAX) FDX_RING(21, 192, split_env, INT32_MAX);
-        if (small_env == 64)
-            FDX_RING(21, 64, 0, split_env);
-        else if (small_env == 128)
-            FDX_RING(21, 128, 0, split_env);
-        else
-            FDX_RING(21, 96, 0, split_env);
-    } else if (S <= 32) {
-        FDX_RING(32, 192, 0, INT32_MAX);
-    } else {
-        FDX_RING(64, 96, 0, INT32_MAX);
-    }
+                       sorder_d, goff_d, n_seg, S, n_slots, wa, n_windows, nb_d, avg_d, 0, INT32_MAX)
+    if (S <= 21)
+        FDX_RING(21, 96);
+    else if (S <= 32)
+        FDX_RING(32, 192);
+    else
+        FDX_RING(64, 96);
 #undef FDX_RING
     FDX_LAUNCHED("k_customer_ring");
     return FDX_OK;

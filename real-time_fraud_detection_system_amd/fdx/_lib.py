@@ -57,7 +57,8 @@ SIGNATURES = {
     "fdx_abi_version": (ctypes.c_int, []),
     "fdx_time_flags": (ctypes.c_int, [P, c_i64, c_i32, P, P, P]),
     "fdx_customer_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
-    "fdx_terminal_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P, P]),
+    "fdx_terminal_windows_workspace_size": (c_sz, [c_i64]),
+    "fdx_terminal_windows": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P, P, c_sz, P]),
     "fdx_assemble_features": (ctypes.c_int, [c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_i64, P]),
     "fdx_customer_layout_workspace_size": (c_sz, [c_i64]),
     "fdx_customer_layout": (ctypes.c_int, [P, c_i64, P, P, P, c_i32, P, P, P, P, P, c_i64, P, P, c_sz, P]),
@@ -67,14 +68,13 @@ SIGNATURES = {
     "fdx_customer_windows_interleaved": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_exclusive_scan_u32_workspace_size": (c_sz, [c_i64]),
     "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),
-    "fdx_terminal_windows_packed": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
-    "fdx_terminal_windows_packed_unsorted": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
-    "fdx_terminal_windows_packed_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, P, P]),
-    "fdx_invert_slots": (ctypes.c_int, [P, c_i64, P, c_i64, P]),
     "fdx_segment_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
     "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
     "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),
-    "fdx_dedup_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
+    "fdx_dedup_latest_workspace_size": (c_sz, [c_i64]),
+    "fdx_dedup_latest": (ctypes.c_int, [P, P, c_i64, P, P, P, c_sz, P]),
+    "fdx_cdc_compact_workspace_size": (c_sz, [c_i64]),
+    "fdx_cdc_compact": (ctypes.c_int, [P, c_i64, P, P, P, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_stream_create": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, c_i32, P, c_i64, c_i32, c_i64, P, P]),
     "fdx_stream_reset": (ctypes.c_int, [P, P]),
     "fdx_stream_memory": (ctypes.c_int, [P, P]),
@@ -82,8 +82,6 @@ SIGNATURES = {
     "fdx_stream_status": (ctypes.c_int, [P, P, P]),
     "fdx_stream_status_async": (ctypes.c_int, [P, P, P]),
     "fdx_stream_destroy": (ctypes.c_int, [P]),
-    "fdx_hip_stream_create_cu_mask": (ctypes.c_int, [P, c_i32, ctypes.POINTER(P)]),
-    "fdx_hip_stream_destroy": (ctypes.c_int, [P]),
     "fdx_train_test_split": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, c_i64, c_i64, c_i32, c_i32, c_i32, P, P, P,
                                             c_sz, P, P]),
     "fdx_card_precision_workspace_size": (ctypes.c_size_t, [c_i32]),
@@ -95,8 +93,6 @@ SIGNATURES = {
     "fdx_rekey_payload_workspace_size": (c_sz, [c_i64, c_i32, c_i32]),
     "fdx_rekey_payload": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_terminal_windows_grouped": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P, P, P, P]),
-    "fdx_terminal_windows_grouped_dest": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
-                                                         P]),
     "fdx_terminal_windows_grouped_compact": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
                                                             P]),
     "fdx_customer_layout_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, P, P, P, P, c_i64, P, P,
@@ -137,7 +133,6 @@ SIGNATURES = {
     "fdx_forest_prepare_features": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_forest_prepare_grouped": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
-    "fdx_forest_set_slab_rows": (ctypes.c_int, [P, c_i64]),
     "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
     "fdx_forest_get_variant": (ctypes.c_int, [P, P]),
     "fdx_forest_prepare_reply": (ctypes.c_int, [P, P, P, c_i64, c_i32, c_i32, P, c_sz, P]),
@@ -158,7 +153,7 @@ def load():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.fdx_abi_version() != 1:
+        if L.fdx_abi_version() != 2:
             raise FdxError("libfdx ABI version mismatch")
         _lib = L
     return _lib

@@ -132,10 +132,14 @@ class KeyRangeCheck:
 
     def __init__(self, keys: torch.Tensor, n_keys: int, what: str = "keys", stream=None):
         self.what, self.n_keys = what, int(n_keys)
+        st = stream or torch.cuda.current_stream()
         self._host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-        self._host.copy_(count_out_of_range(keys, 0, n_keys, stream), non_blocking=True)
-        self._ev = torch.cuda.Event()
-        self._ev.record(stream or torch.cuda.current_stream())
+        # count, copy and event all on `st` (the copy must follow the count kernel, and the
+        # event must follow the copy), whatever torch's current stream is
+        with torch.cuda.stream(st):
+            self._host.copy_(count_out_of_range(keys, 0, n_keys, st), non_blocking=True)
+            self._ev = torch.cuda.Event()
+            self._ev.record(st)
 
     def check(self) -> None:
         self._ev.synchronize()
@@ -203,15 +207,18 @@ def customer_windows(ts_ns, amount, seg_off, windows_days=(1, 7, 30), stream=Non
 
 
 def terminal_windows(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), stream=None):
-    """Grouped rows -> (nb int32 [W, n], risk float64 [W, n])."""
+    """Grouped rows -> (nb int32 [W, n], risk float64 [W, n]); the kernel's scratch is a caller
+    workspace (fdx_terminal_windows_workspace_size)."""
     _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
     n = ts_ns.numel()
     W = len(windows_days)
     nb = torch.empty((W, n), dtype=torch.int32, device=ts_ns.device)
     risk = torch.empty((W, n), dtype=torch.float64, device=ts_ns.device)
-    check(_lib.load().fdx_terminal_windows(_ptr(ts_ns), _ptr(fraud), _ptr(seg_off), seg_off.numel() - 1, n,
-                                           int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W, _ptr(nb),
-                                           _ptr(risk), _s(stream)), "fdx_terminal_windows")
+    L = _lib.load()
+    ws = workspace(L.fdx_terminal_windows_workspace_size(n), ts_ns.device)
+    check(L.fdx_terminal_windows(_ptr(ts_ns), _ptr(fraud), _ptr(seg_off), seg_off.numel() - 1, n,
+                                 int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W, _ptr(nb), _ptr(risk),
+                                 _ptr(ws), ws.numel(), _s(stream)), "fdx_terminal_windows")
     return nb, risk
 
 
@@ -343,49 +350,6 @@ def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 
     return nb, avg
 
 
-def terminal_windows_packed(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), rows=None,
-                            stream=None):
-    """Terminal windows as count records int64 [ts rows, W] (word = NB | FRAUD << 32).
-    rows=None: ts/fraud are grouped (time-sorted within terminal) and record q belongs to
-    grouped row q.  rows = the re-key perm (grouped position -> input row): ts/fraud are the
-    caller's arrays, read through the perm inside the kernel, and record r belongs to input
-    row r."""
-    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
-    if rows is not None:
-        _dev(rows, torch.int32, "rows")
-        if rows.numel() != ts_ns.numel():
-            raise ValueError("rows must have one entry per transaction")
-    n = ts_ns.numel()
-    W = len(windows_days)
-    rec = torch.empty((n, W), dtype=torch.int64, device=ts_ns.device)
-    check(_lib.load().fdx_terminal_windows_packed(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(seg_off),
-                                                  seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
-                                                  _win_ns(windows_days), W, _ptr(rec), _s(stream)),
-          "fdx_terminal_windows_packed")
-    return rec
-
-
-def terminal_windows_grouped_dest(gts, seg_off, rows, dest_map, n_out: int, gfraud=None, delay_days=7,
-                                  windows_days=(1, 7, 30), runs: bool = False, stream=None):
-    """terminal_windows_grouped's count records written at dest_map[row] of an [n_out, W]
-    int64 array (e.g. the rows' scoring slots: invert_slots); positions no row maps to are
-    left unwritten."""
-    _dev(gts, torch.int64, "gts"); _dev(seg_off, torch.int64, "seg_off"); _dev(rows, torch.int32, "rows")
-    _dev(dest_map, torch.int32, "dest_map")
-    if gfraud is not None:
-        _dev(gfraud, torch.uint8, "gfraud")
-    n = gts.numel()
-    W = len(windows_days)
-    rec = torch.empty((int(n_out), W), dtype=torch.int64, device=gts.device)
-    scratch = torch.empty(max(n, 1), dtype=torch.int32, device=gts.device)
-    check(_lib.load().fdx_terminal_windows_grouped_dest(_ptr(gts), _ptr(gfraud), _ptr(rows), _ptr(dest_map),
-                                                        _ptr(seg_off), seg_off.numel() - 1, n,
-                                                        int(delay_days) * NS_PER_DAY, _win_ns(windows_days), W,
-                                                        int(bool(runs)), _ptr(rec), _ptr(scratch), _s(stream)),
-          "fdx_terminal_windows_grouped_dest")
-    return rec
-
-
 def terminal_windows_compact(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
                              runs: bool = False, stream=None):
     """terminal_windows_grouped's count records by row in the COMPACT format (3 windows): an
@@ -456,53 +420,6 @@ def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7,
     check(L.fdx_terminal_windows_grouped(*args, _ptr(nb), _ptr(risk), None, _ptr(scratch), _s(stream)),
           "fdx_terminal_windows_grouped")
     return nb, risk
-
-
-def terminal_windows_packed_dest(ts_ns, fraud, seg_off, rows, dest, n_out: int, delay_days=7,
-                                 windows_days=(1, 7, 30), stream=None):
-    """terminal_windows_packed with the record of input row r written at dest[r] (e.g. its
-    scoring slot: dest = invert_slots(layout.irow, n, layout.n_slots)); returns rec [n_out, W]."""
-    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
-    _dev(rows, torch.int32, "rows"); _dev(dest, torch.int32, "dest")
-    n = ts_ns.numel()
-    W = len(windows_days)
-    rec = torch.empty((int(n_out), W), dtype=torch.int64, device=ts_ns.device)
-    check(_lib.load().fdx_terminal_windows_packed_dest(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(dest), _ptr(seg_off),
-                                                       seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
-                                                       _win_ns(windows_days), W, _ptr(rec), _s(stream)),
-          "fdx_terminal_windows_packed_dest")
-    return rec
-
-
-def invert_slots(irow, n_rows: int, n_slots: int, stream=None):
-    """slot_of[irow[s]] = s for the interleaved layout's non-padding slots s < n_slots
-    (irow may be longer: the layout buffers are sized for the worst case)."""
-    _dev(irow, torch.int32, "irow")
-    if not 0 <= int(n_slots) <= irow.numel():
-        raise FdxError("n_slots out of range")
-    out = torch.empty(int(n_rows), dtype=torch.int32, device=irow.device)
-    check(_lib.load().fdx_invert_slots(_ptr(irow), int(n_slots), _ptr(out), int(n_rows), _s(stream)),
-          "fdx_invert_slots")
-    return out
-
-
-def terminal_windows_packed_unsorted(ts_ns, fraud, seg_off, delay_days=7, windows_days=(1, 7, 30), rows=None,
-                                     stream=None):
-    """terminal_windows_packed for segments that are not in time order (each is sorted in
-    the kernel): the multi-GPU owner side, whose segments are concatenated per-rank runs."""
-    _dev(ts_ns, torch.int64, "ts_ns"); _dev(fraud, torch.uint8, "fraud"); _dev(seg_off, torch.int64, "seg_off")
-    if rows is not None:
-        _dev(rows, torch.int32, "rows")
-        if rows.numel() != ts_ns.numel():
-            raise ValueError("rows must have one entry per transaction")
-    n = ts_ns.numel()
-    W = len(windows_days)
-    rec = torch.empty((n, W), dtype=torch.int64, device=ts_ns.device)
-    check(_lib.load().fdx_terminal_windows_packed_unsorted(_ptr(ts_ns), _ptr(fraud), _ptr(rows), _ptr(seg_off),
-                                                           seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
-                                                           _win_ns(windows_days), W, _ptr(rec), _s(stream)),
-          "fdx_terminal_windows_packed_unsorted")
-    return rec
 
 
 def unpack_term_records(rec: torch.Tensor):
@@ -585,10 +502,6 @@ class Forest:
         self.n_chunks = nc.value
         self.variant = int(variant)
 
-    def set_slab_rows(self, rows: int) -> None:
-        check(_lib.load().fdx_forest_set_slab_rows(self._h, int(rows)), "fdx_forest_set_slab_rows")
-        self.slab_rows = int(rows)
-
     def workspace_size(self, n: int) -> int:
         return int(_lib.load().fdx_forest_workspace_size(self._h, int(n)))
 
@@ -640,14 +553,12 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_by_slot: bool = False,
-                           term_compact: bool = False):
+                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_compact: bool = False):
     """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
-    term_by_slot: term_rec[i] is scoring row i's record (terminal_windows_packed_dest);
     term_compact: term_rec is terminal_windows_compact's array."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
-    opts = (1 if val_is_sum else 0) | (2 if term_by_slot else 0) | (4 if term_compact else 0)
+    opts = (1 if val_is_sum else 0) | (4 if term_compact else 0)
     check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
                                                  _ptr(camt), _ptr(cnb),
                                                  _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),

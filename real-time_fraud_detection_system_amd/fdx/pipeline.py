@@ -14,7 +14,6 @@ sorts them on the GPU.  All outputs are returned in input row order.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -39,36 +38,6 @@ class Features:
     X: Optional[torch.Tensor] = None  # float64 [n, ld] input_features in row order
 
 
-# A/B switches for measurements (bench / profiling runs); the defaults are the measured-best forms
-_OVERLAP = os.environ.get("FDX_OVERLAP", "1") != "0"            # terminal half on a side stream
-_CUST_PAYLOAD = os.environ.get("FDX_CUSTOMER_PAYLOAD", "1") != "0"  # re-key carries ts / amount
-_TERM_PAYLOAD = os.environ.get("FDX_TERMINAL_PAYLOAD", "1") != "0"  # re-key carries ts + fraud bit
-_SIDE_PRIORITY = int(os.environ.get("FDX_SIDE_PRIORITY", "0"))        # side stream priority (-1 = high)
-_SCAN_DIRECT = os.environ.get("FDX_SCAN_DIRECT", "0") != "0"  # scan mode: one kernel with its own start searches
-_CU_SPLIT = os.environ.get("FDX_CU_SPLIT", "")  # "k/8": side stream on the CUs with index % 8 < k
-# terminal records written at their scoring slots (the row assembly then reads them in slot
-# order); the terminal windows wait for the customer layout
-_TERM_SLOTS = os.environ.get("FDX_TERM_SLOTS", "0") != "0"
-# terminal count records in the compact 16-byte format (one aligned store / load per row);
-# opt-in until it is measured and validated on the GPU
-_TERM_COMPACT = os.environ.get("FDX_TERM_COMPACT", "0") != "0"
-
-
-def _masked_stream(device, eighths: int):
-    """A torch stream over the HIP stream limited to the CUs with index % 8 < eighths."""
-    import ctypes
-
-    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-    words = [0] * ((n_cu + 31) // 32)
-    for i in range(n_cu):
-        if i % 8 < eighths:
-            words[i // 32] |= 1 << (i % 32)
-    arr = (ctypes.c_uint32 * len(words))(*words)
-    h = ctypes.c_void_p()
-    check(_lib.load().fdx_hip_stream_create_cu_mask(arr, len(words), ctypes.byref(h)), "fdx_hip_stream_create_cu_mask")
-    return torch.cuda.ExternalStream(h.value, device=device)
-
-
 class FraudPipeline:
     """avg_mode: "exact" -- the customer averages bit for bit as pandas' roll_sum (the
     sequential Kahan add/remove recurrence, k_customer_walk) -- or "scan" -- float64 prefix
@@ -77,10 +46,12 @@ class FraudPipeline:
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
-                 avg_mode: str = "exact"):
+                 avg_mode: str = "exact", compact_records: bool = False):
         if avg_mode not in ("exact", "scan"):
             raise ValueError("avg_mode must be 'exact' or 'scan'")
         self.avg_mode = avg_mode
+        # the scoring path's terminal count records in the 16-byte compact form (3 windows)
+        self.compact_records = bool(compact_records)
         self.windows_days = tuple(int(w) for w in windows_days)
         self.delay_days = int(delay_days)
         self.flags_mode = flags_mode
@@ -148,7 +119,7 @@ class FraudPipeline:
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
                   proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, mark=None,
-                  validate: bool = True, overlap: Optional[bool] = None):
+                  validate: bool = True, overlap: bool = True):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
@@ -162,88 +133,63 @@ class FraudPipeline:
         on its stream (bench.py records a HIP event there).  validate: the customer / terminal
         ids must lie in [0, n_customers) / [0, n_terminals) (counted on the device, read at
         the layout's host sync -- no extra stall).  overlap=False runs the terminal half on the
-        caller's stream too (None: FDX_OVERLAP, default on)."""
+        caller's stream too (bench.py's isolated per-stage timings)."""
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         main = stream or torch.cuda.current_stream()
         if ts_ns.numel() == 0:  # an empty table: nothing to score
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
-            self._side = (_masked_stream(ts_ns.device, int(_CU_SPLIT.split("/")[0])) if _CU_SPLIT else
-                          torch.cuda.Stream(device=ts_ns.device, priority=_SIDE_PRIORITY))
-        side = self._side
+            self._side = torch.cuda.Stream(device=ts_ns.device)
+        side = self._side if overlap else main
         mk("start", main)
         if validate:
             rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
                   ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
-        if not (_OVERLAP if overlap is None else overlap):
-            side = main
         side.wait_stream(main)
         # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
         # perm); the records come out in input row order, read by the row assembly through irow.
         # Allocated under the side stream's context, so that the caching allocator hands
         # these buffers to nothing on the main stream while the side stream still uses them.
-        by_slot = _TERM_SLOTS and _TERM_PAYLOAD
-        compact = _TERM_COMPACT and _TERM_PAYLOAD and not by_slot and W == 3
+        compact = self.compact_records and W == 3
         with torch.cuda.stream(side):
             mk("start", side)
-            if by_slot:  # the windows come after the customer layout (below)
-                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
-                mk("rekey_terminal", side)
-            elif _TERM_PAYLOAD:
-                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
-                mk("rekey_terminal", side)
-                if compact:
-                    trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                        windows_days=self.windows_days, stream=side)
-                else:
-                    trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                        windows_days=self.windows_days, stream=side)
-            else:  # round-1 form: plain re-key, the kernel gathers ts / fraud through the perm
-                tperm, tseg, _ = ops.rekey(terminal, n_terminals, side)
-                mk("rekey_terminal", side)
-                trec = ops.terminal_windows_packed(ts_ns, fraud, tseg, self.delay_days, self.windows_days,
-                                                   rows=tperm, stream=side)
-            if not by_slot:
-                mk("terminal_windows", side)
+            tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+            mk("rekey_terminal", side)
+            if compact:
+                trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                    windows_days=self.windows_days, stream=side)
+            else:
+                trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                    windows_days=self.windows_days, stream=side)
+            mk("terminal_windows", side)
         for t in (ts_ns, terminal, fraud):
             t.record_stream(side)  # inputs in use on the side stream
         # customer half (caller's stream): the re-key carries ts and amount into grouped order
         scan = self.avg_mode == "scan"
-        if _CUST_PAYLOAD or scan:
-            cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
-            mk("rekey_customer", main)
-            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
-                                      None if (scan and _SCAN_DIRECT) else self.windows_days, grouped=True)
-        else:  # round-1 form: plain re-key, the layout gathers ts / amount through the perm
-            cperm, cseg, _ = ops.rekey(customer, n_customers, main)
-            mk("rekey_customer", main)
-            lay = ops.customer_layout(cseg, cperm, ts_ns, amount, W, main, self._slots_hint, self.windows_days)
+        walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
+        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
+        mk("rekey_customer", main)
+        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
+                                  self.windows_days if walk else None, grouped=True)
         mk("customer_layout", main)
         if validate:
             for c in rc:
                 c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
-        if by_slot:
-            slot_of = ops.invert_slots(lay.irow, ts_ns.numel(), lay.n_slots, main)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                trec = ops.terminal_windows_grouped_dest(tgts, tseg, tperm, slot_of, lay.n_slots,
-                                                         delay_days=self.delay_days,
-                                                         windows_days=self.windows_days, stream=side)
-                mk("terminal_windows", side)
         if scan:  # the windows straight from the grouped rows into the layout's slots
             inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
-        else:
+        elif walk:
             inb, isum = ops.customer_windows_walk(lay, cseg, main)
+        else:
+            inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, main)
         mk("customer_walk", main)
         main.wait_stream(side)
         trec.record_stream(main)
         ws = self._forest_ws(lay.n_slots, ws, amount.device)
         ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                   ws, main, n=lay.n_slots, val_is_sum=True, term_by_slot=by_slot,
-                                   term_compact=compact)
+                                   ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact)
         mk("assemble_rows", main)
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
         mk("forest_traverse", main)

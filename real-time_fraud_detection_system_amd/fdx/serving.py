@@ -72,13 +72,21 @@ def cdc_decode(amount_bytes: torch.Tensor | None, offsets: torch.Tensor | None, 
     return uns, amt, tsn
 
 
-def dedup_latest(key: torch.Tensor, kafka_ts: torch.Tensor, stream=None) -> torch.Tensor:
-    """uint8 keep mask: the record with the largest Kafka timestamp per key (ties: last)."""
+def dedup_latest(key: torch.Tensor, kafka_ts: torch.Tensor, bad: torch.Tensor | None = None, stream=None):
+    """uint8 keep mask: the record with the largest Kafka timestamp per key (ties: last).
+    bad (int32 device scalar, optional): set to 1 if a key is -1 (the hash table's empty key)."""
     ops._dev(key, torch.int64, "key"); ops._dev(kafka_ts, torch.int64, "kafka_ts")
-    perm = ops.argsort_i64(key, stream)
-    keep = torch.empty(key.numel(), dtype=torch.uint8, device=key.device)
-    check(_lib.load().fdx_dedup_latest(ops._ptr(key), ops._ptr(kafka_ts), ops._ptr(perm), key.numel(),
-                                       ops._ptr(keep), ops._s(stream)), "fdx_dedup_latest")
+    n = key.numel()
+    keep = torch.empty(n, dtype=torch.uint8, device=key.device)
+    L = _lib.load()
+    ws = ops.workspace(L.fdx_dedup_latest_workspace_size(n), key.device)
+    own = bad is None
+    if own:
+        bad = torch.zeros(1, dtype=torch.int32, device=key.device)
+    check(L.fdx_dedup_latest(ops._ptr(key), ops._ptr(kafka_ts), n, ops._ptr(keep), ops._ptr(bad), ops._ptr(ws),
+                             ws.numel(), ops._s(stream)), "fdx_dedup_latest")
+    if own and n and int(bad.item()):
+        raise _lib.FdxUnsupported("tx_id -1 is reserved (the dedup table's empty key)")
     return keep
 
 

@@ -180,6 +180,66 @@ class StreamScorer:
         """Wait for the last batch's status bits and raise if it reported a problem."""
         self.state.poll(block=True)
 
+    def score_cdc(self, tx_id, customer_id, terminal_id, amount_bytes, amount_offsets, tx_datetime_us, kafka_ts,
+                  fraud=None):
+        """One Debezium micro-batch scored from its wire columns, device-resident end to end --
+        the reference's sink (pyspark/scripts/kafka_s3_sink_transactions.py) decodes tx_amount
+        DECIMAL(10,2) bytes (:64-71), truncates tx_datetime microseconds to seconds (:167) and
+        keeps the latest record per tx_id by Kafka timestamp (:180); then the scoring job scores
+        the rows (fraud_detection.py:183-201).  Here: fdx_cdc_decode -> fdx_dedup_latest ->
+        fdx_cdc_compact (kept records, batch order) -> score().  Inputs are device tensors:
+        tx_id / customer_id / terminal_id / tx_datetime_us / kafka_ts int64 [n], amount_bytes
+        uint8 (the records' bytes back to back), amount_offsets int64 [n + 1], fraud uint8 [n]
+        or None (the CDC topic carries no label: zeros).  One host read per batch (the kept
+        count).  -> (proba [m] device view, rows int32 [m] = batch position of each kept record)."""
+        L = _lib.load()
+        n = tx_id.numel()
+        dev = tx_id.device
+        for t, nm in ((tx_id, "tx_id"), (customer_id, "customer_id"), (terminal_id, "terminal_id"),
+                      (tx_datetime_us, "tx_datetime_us"), (kafka_ts, "kafka_ts")):
+            ops._dev(t, torch.int64, nm)
+            if t.numel() != n:
+                raise FdxError(f"{nm} has {t.numel()} rows, tx_id has {n}")
+        ops._dev(amount_bytes, torch.uint8, "amount_bytes")
+        ops._dev(amount_offsets, torch.int64, "amount_offsets")
+        if amount_offsets.numel() != n + 1:
+            raise FdxError("amount_offsets needs n + 1 entries")
+        if fraud is not None:
+            ops._dev(fraud, torch.uint8, "fraud")
+        if n > self.state.max_batch:
+            raise FdxError(f"batch of {n} records > max_batch {self.state.max_batch}")
+        c = getattr(self, "_cdc", None)
+        if c is None:  # per-scorer buffers for max_batch records
+            m = self.state.max_batch
+            c = self._cdc = dict(
+                amt=torch.empty(m, dtype=torch.float64, device=dev), ts=torch.empty(m, dtype=torch.int64, device=dev),
+                keep=torch.empty(m, dtype=torch.uint8, device=dev), cust=torch.empty(m, dtype=torch.int32, device=dev),
+                term=torch.empty(m, dtype=torch.int32, device=dev), ts_k=torch.empty(m, dtype=torch.int64, device=dev),
+                amt_k=torch.empty(m, dtype=torch.float64, device=dev), fr_k=torch.empty(m, dtype=torch.uint8, device=dev),
+                rows=torch.empty(m, dtype=torch.int32, device=dev),
+                status=torch.zeros(2, dtype=torch.int64, device=dev),  # [count, bad]
+                ws=ops.workspace(max(L.fdx_dedup_latest_workspace_size(m), L.fdx_cdc_compact_workspace_size(m)), dev),
+                host=torch.zeros(2, dtype=torch.int64, pin_memory=True))
+        st = torch.cuda.current_stream()
+        P, S = ops._ptr, ops._s()
+        bad = c["status"][1:].view(torch.int32)[:1]  # low word of status[1]
+        c["status"].zero_()
+        if n:
+            check(L.fdx_cdc_decode(P(amount_bytes), P(amount_offsets), P(tx_datetime_us), n, None, P(c["amt"]),
+                                   P(c["ts"]), P(bad), S), "fdx_cdc_decode")
+            check(L.fdx_dedup_latest(P(tx_id), P(kafka_ts), n, P(c["keep"]), P(bad), P(c["ws"]), c["ws"].numel(), S),
+                  "fdx_dedup_latest")
+        check(L.fdx_cdc_compact(P(c["keep"]), n, P(customer_id), P(terminal_id), P(c["ts"]), P(c["amt"]), P(fraud),
+                                P(c["cust"]), P(c["term"]), P(c["ts_k"]), P(c["amt_k"]), P(c["fr_k"]), P(c["rows"]),
+                                P(c["status"]), P(c["ws"]), c["ws"].numel(), S), "fdx_cdc_compact")
+        c["host"].copy_(c["status"], non_blocking=True)
+        st.synchronize()
+        m, b = int(c["host"][0]), int(c["host"][1])
+        if b:
+            raise FdxUnsupported("CDC batch: a tx_amount field of 0 or > 8 bytes, or tx_id -1 (reserved)")
+        out = self.score(c["ts_k"][:m], c["cust"][:m], c["amt_k"][:m], c["term"][:m], c["fr_k"][:m])
+        return out, c["rows"][:m]
+
 
 def stream_terminal_exchange(K, records, ts, terminal, fraud, world, n_terminals_total, windows_days=(1, 7, 30),
                              delay_days=7, group=None):

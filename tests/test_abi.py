@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(L, name), name
     assert set(_lib.SIGNATURES) == set(declared_functions())
-    assert L.fdx_abi_version() == 1
+    assert L.fdx_abi_version() == 2
 
 
 def test_error_path_without_gpu():

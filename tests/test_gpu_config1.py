@@ -1,0 +1,120 @@
+"""BASELINE.json configs[0] on the GPU: the handbook-default set (5k customers / 10k terminals /
+183 days, ~1.75M tx) + DecisionTree(max_depth=2) scoring (model_training.ipynb:1276-1280), and
+the reference's own config-1 rows behind the values its notebook printed.
+
+  * notebook known answers: the reference generator's rows behind the values printed in
+    feature_transformation.ipynb (:1414-1440 tx 2051326, :1798-1863 tx 3527 / 9583 / row
+    10355, :3013-3031 latest terminal rows, ...), featurized by FraudPipeline.featurize and by
+    the pandas drop-ins (driven like the notebook, :1092-1093 / :2435-2436), every printed
+    value to its printed decimals -- the same check tests/test_oracle_golden.py applies to the
+    CPU oracle;
+  * a 5k / 10k / 183-day synthetic set (the handbook distributions, fdx.synth.generate_device):
+    every feature of every row equal to the C oracle; the fused scoring path's
+    probabilities equal to the float64 path's on every row and to the oracle forest on the
+    oracle's features, for DT(depth 2) (configs[0]'s model) and the RF(100, depth 20) bench
+    model.
+"""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import fdx
+import oracle
+from fdx import ops, synth
+from fdx.pipeline import FraudPipeline
+from kat_check import check_notebook_kat
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FEATS = oracle.INPUT_FEATURES
+
+
+def T(a, dt, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+
+
+def test_notebook_known_answers_pipeline(dev):
+    """FraudPipeline.featurize (re-keys, customer / terminal windows, flags, assembly)."""
+    pipe = FraudPipeline()
+
+    def featurize(ts, c, t, a, fr, tids):
+        f = pipe.featurize(T(ts, torch.int64, dev), T(c, torch.int32, dev), T(t, torch.int32, dev),
+                           T(a, torch.float64, dev), T(fr, torch.uint8, dev), int(c.max()) + 1, int(t.max()) + 1)
+        X = f.X.cpu().numpy()
+        assert np.array_equal(X[:, 0], a)
+        return {name: X[:, j] for j, name in enumerate(FEATS)}
+
+    assert check_notebook_kat(featurize) >= 500
+
+
+def test_notebook_known_answers_dropins(dev):
+    """The pandas drop-ins driven exactly like the notebook: groupby-free whole-frame calls,
+    sort_values('TX_DATETIME') between them (:1093, :2436), flags by is_weekend / is_night."""
+
+    def featurize(ts, c, t, a, fr, tids):
+        df = pd.DataFrame({"TRANSACTION_ID": tids, "TX_DATETIME": pd.to_datetime(ts, unit="ns"),
+                           "CUSTOMER_ID": c, "TERMINAL_ID": t, "TX_AMOUNT": a, "TX_FRAUD": fr})
+        df["TX_DURING_WEEKEND"] = fdx.is_weekend(df.TX_DATETIME)
+        df["TX_DURING_NIGHT"] = fdx.is_night(df.TX_DATETIME)
+        out = fdx.get_customer_spending_behaviour_features(df, windows_size_in_days=[1, 7, 30])
+        out = out.sort_values("TX_DATETIME", kind="stable").reset_index(drop=True)
+        out = fdx.get_count_risk_rolling_window(out, delay_period=7, windows_size_in_days=[1, 7, 30],
+                                                feature="TERMINAL_ID")
+        out = out.sort_values("TX_DATETIME", kind="stable").reset_index(drop=True)
+        out = out.set_index("TRANSACTION_ID").loc[tids]
+        return {name: out[name].values for name in FEATS[1:]}
+
+    assert check_notebook_kat(featurize) >= 500
+
+
+@pytest.fixture(scope="module")
+def config1(dev):
+    g = synth.generate_device(5_000, 10_000, 183, seed=20240601, device=dev)
+    d = {k: g[k].cpu().numpy() for k in ("ts", "customer", "terminal", "amount", "fraud")}
+    assert 1_500_000 < len(d["ts"]) < 2_100_000
+    ref = oracle.featurize_arrays(d["ts"], d["customer"], d["terminal"], d["amount"], d["fraud"])
+    Xo = np.column_stack([d["amount"]] + [ref[c] for c in FEATS[1:]])
+    return g, d, Xo
+
+
+def test_config1_every_feature_of_every_row(dev, config1):
+    g, d, Xo = config1
+    pipe = FraudPipeline()
+    X = pipe.featurize(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 5_000, 10_000).X.cpu().numpy()
+    for j, c in enumerate(FEATS):
+        np.testing.assert_array_equal(X[:, j], Xo[:, j], err_msg=c)
+
+
+def _load(name):
+    if name == "dt2":
+        z = np.load(os.path.join(ROOT, "tests", "golden", "forest_dt2.npz"))
+    else:
+        z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    return arrays, z["mean"], z["scale"]
+
+
+@pytest.mark.parametrize("model", ["dt2", "rf100_d20"])
+def test_config1_scoring_fused_vs_f64_vs_oracle(dev, config1, model):
+    """configs[0]'s DecisionTree(max_depth=2) and the bench RF: fused path == float64 path on
+    every row; == the oracle forest on the oracle's features (every row for DT2, 200k sampled
+    rows for the RF)."""
+    g, d, Xo = config1
+    arrays, mean, scale = _load(model)
+    forest = ops.Forest(arrays, 15, mean, scale)
+    pipe = FraudPipeline(forest=forest)
+    n = len(d["ts"])
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 5_000, 10_000)
+    fused = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, fused)
+    _, p64 = pipe.run(*args)
+    fused, p64 = fused.cpu().numpy(), p64.cpu().numpy()
+    np.testing.assert_array_equal(fused, p64)
+    sel = np.arange(n) if model == "dt2" else np.random.default_rng(3).choice(n, 200_000, replace=False)
+    np.testing.assert_array_equal(fused[sel], oracle.forest_predict(Xo[sel], arrays, mean, scale))
+    if model == "dt2":  # a depth-2 tree has 4 leaves: every one of them must be reached
+        assert len(np.unique(fused)) >= 3

@@ -80,21 +80,21 @@ def test_fused_scoring_paths_agree(dev, golden):
 def test_terminal_records_unsorted_runs(dev, parts):
     """The owner side of the exchange: rows arrive as one time-sorted run per source rank,
     so a stable re-key by terminal yields segments of concatenated runs.  The records of
-    fdx_terminal_windows_packed_unsorted must equal those of the time-sorted input row by
-    row -- for 1 run (sorted), a few runs, and more runs than the per-run search handles
+    fdx_terminal_windows_grouped(runs = 1) over them must equal those of the time-sorted input
+    row by row -- for 1 run (sorted), a few runs, and more runs than the per-run search handles
     (100 > kMaxRuns: direct counts)."""
     d = synth.generate(n_customers=600, n_terminals=300, nb_days=80, r=30, seed=5)
     T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
     n = len(d["ts"])
     ts, term, fr = T(d["ts"], torch.int64), T(d["terminal"], torch.int32), T(d["fraud"], torch.uint8)
-    tperm, tseg, _ = ops.rekey(term, 300)
-    ref = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()   # by input row
+    tperm, tseg, tgts, _ = ops.rekey_payload(term, 300, ts, flag=fr)
+    ref = ops.terminal_windows_grouped(tgts, tseg, rows=tperm).cpu().numpy()   # by input row
     # "receive buffer": rows grouped by source part (customer % parts), time order inside
     order = np.argsort(d["customer"] % parts, kind="stable")
     rts, rterm, rfr = T(d["ts"][order], torch.int64), T(d["terminal"][order], torch.int32), \
         T(d["fraud"][order], torch.uint8)
-    gperm, gseg, _ = ops.rekey(rterm, 300)
-    got = ops.terminal_windows_packed_unsorted(rts, rfr, gseg, rows=gperm).cpu().numpy()  # by receive index
+    gperm, gseg, gts, _ = ops.rekey_payload(rterm, 300, rts, flag=rfr)
+    got = ops.terminal_windows_grouped(gts, gseg, rows=gperm, runs=True).cpu().numpy()  # by receive index
     np.testing.assert_array_equal(got, ref[order])
     assert n > 0
 
@@ -112,8 +112,8 @@ def test_terminal_records_hot_terminals_long_segments(dev, parts):
     n = len(d["ts"])
     assert np.bincount(d["terminal"]).max() > 4 * 1024
     ts, term, fr = T(d["ts"], torch.int64), T(d["terminal"], torch.int32), T(d["fraud"], torch.uint8)
-    tperm, tseg, _ = ops.rekey(term, 8)
-    ref = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()   # by input row
+    tperm, tseg, tgts, _ = ops.rekey_payload(term, 8, ts, flag=fr)
+    ref = ops.terminal_windows_grouped(tgts, tseg, rows=tperm).cpu().numpy()   # by input row
     m = d["terminal"] == 3
     f = oracle.featurize_arrays(d["ts"][m], d["customer"][m], d["terminal"][m], d["amount"][m], d["fraud"][m])
     w = ref[m]
@@ -125,10 +125,7 @@ def test_terminal_records_hot_terminals_long_segments(dev, parts):
     order = np.argsort(d["customer"] % parts, kind="stable")
     rts, rterm, rfr = T(d["ts"][order], torch.int64), T(d["terminal"][order], torch.int32), \
         T(d["fraud"][order], torch.uint8)
-    gperm, gseg, _ = ops.rekey(rterm, 8)
-    got = ops.terminal_windows_packed_unsorted(rts, rfr, gseg, rows=gperm).cpu().numpy()  # by receive index
-    np.testing.assert_array_equal(got, ref[order])
-    # the owner side's own path: payload re-key (fraud in bit 31 of the perm), grouped runs
+    # the owner side's path: payload re-key (fraud in bit 31 of the perm), grouped runs
     perm, seg, gts, _ = ops.rekey_payload(rterm, 8, rts, flag=rfr)
     got = ops.terminal_windows_grouped(gts, seg, rows=perm, runs=True).cpu().numpy()
     np.testing.assert_array_equal(got, ref[order])

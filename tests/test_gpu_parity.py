@@ -147,18 +147,16 @@ def test_windows_random_edge_cases(dev, max_len):
         onb, orisk = oracle.terminal_windows(ts, fr, seg, 7, windows)
         np.testing.assert_array_equal(nb, onb)
         np.testing.assert_array_equal(risk, orisk)
-        rec = ops.terminal_windows_packed(T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev),
-                                          7, windows)
+        gts, gfr, gseg = T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev)
+        rec = ops.terminal_windows_grouped(gts, gseg, gfraud=gfr, delay_days=7, windows_days=windows)
         W = len(windows)
         rnb, rrisk = ops.unpack_term_records(rec)
         np.testing.assert_array_equal(rnb.cpu().numpy(), onb)
         np.testing.assert_array_equal(rrisk.cpu().numpy(), orisk)
-        # rows=perm: inputs read through the perm, records land at the input row
+        # rows=perm: the record of grouped position q lands at row perm[q]
         perm = np.random.default_rng(W).permutation(len(ts)).astype(np.int32)
-        ts_in = np.empty_like(ts); ts_in[perm] = ts
-        fr_in = np.empty_like(fr); fr_in[perm] = fr
-        rec2 = ops.terminal_windows_packed(T(ts_in, torch.int64, dev), T(fr_in, torch.uint8, dev),
-                                           T(seg, torch.int64, dev), 7, windows, rows=T(perm, torch.int32, dev))
+        rec2 = ops.terminal_windows_grouped(gts, gseg, rows=T(perm, torch.int32, dev), gfraud=gfr, delay_days=7,
+                                            windows_days=windows)
         np.testing.assert_array_equal(rec2.cpu().numpy()[perm], rec.cpu().numpy())
         inv = ops.invert_perm(T(perm, torch.int32, dev)).cpu().numpy()
         np.testing.assert_array_equal(inv[perm], np.arange(len(ts)))
@@ -216,7 +214,7 @@ def test_forest_chunks_and_global_path(dev, n_trees, depth):
     X[rng.random(X.shape) < 0.01] = np.nan
     mean, scale = rng.normal(size=15) * 0.1, rng.uniform(0.5, 2.0, size=15)
     op, ol = oracle.forest_predict(X, arr, mean, scale, want_leaves=True)
-    for variant in (None, 1):  # default (rank layout) and the wide layout, whose trees spill
+    for variant in (None, 0):  # default (rank layout) and the wide layout, whose trees spill
         f = ops.Forest(arr, 15, mean, scale)
         if variant is not None:
             f.set_variant(variant)
@@ -307,7 +305,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(57)))
+@pytest.mark.parametrize("variant", list(range(7)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")
@@ -326,30 +324,6 @@ def test_forest_variants_bit_identical(dev, golden, variant):
     op, ol = oracle.forest_predict(Xr, arr, want_leaves=True)
     np.testing.assert_array_equal(l.cpu().numpy(), ol)
     np.testing.assert_array_equal(p.cpu().numpy(), op)
-
-
-def test_terminal_records_at_slots(dev):
-    """fdx_invert_slots + fdx_terminal_windows_packed_dest (records at scoring slots) equal the
-    row-order records gathered through the layout, and FDX_PREP_TERM_BY_SLOT scores the
-    same as the row-order path."""
-    from fdx import synth
-    from fdx.pipeline import FraudPipeline
-
-    d = synth.generate(n_customers=700, n_terminals=900, nb_days=70, seed=21)
-    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
-    ts, cust, term = T(d["ts"], torch.int64), T(d["customer"], torch.int32), T(d["terminal"], torch.int32)
-    amt, fr = T(d["amount"], torch.float64), T(d["fraud"], torch.uint8)
-    n = ts.numel()
-    cperm, cseg, _ = ops.rekey(cust, 700)
-    lay = ops.customer_layout(cseg, cperm, ts, amt, 3)
-    tperm, tseg, _ = ops.rekey(term, 900)
-    by_row = ops.terminal_windows_packed(ts, fr, tseg, rows=tperm).cpu().numpy()
-    slot_of = ops.invert_slots(lay.irow, n, lay.n_slots)
-    by_slot = ops.terminal_windows_packed_dest(ts, fr, tseg, tperm, slot_of, lay.n_slots).cpu().numpy()
-    irow = lay.irow[: lay.n_slots].cpu().numpy()
-    valid = irow >= 0
-    np.testing.assert_array_equal(by_slot[valid], by_row[irow[valid]])
-    assert sorted(slot_of.cpu().numpy().tolist()) == sorted(np.nonzero(valid)[0].tolist())
 
 
 def test_layout_starts_walk_equals_interleaved(dev):
@@ -408,11 +382,11 @@ def test_fused_scoring_rank_table_overflows(dev):
     np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
 
 
-@pytest.mark.parametrize("variant", [41, 46, 48, 49, 51, 52, 54, 55])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6])
 def test_fused_scoring_every_rank_format(dev, golden, variant):
-    """The fused scoring path (rank rows prepared in-pipeline) on each rank node format --
-    v1 (41), v2 compact (46), v3 sibling pairs (48, 50) -- equals featurize + float64 X +
-    predict on the wide layout (variant 1)."""
+    """The fused scoring path (rank rows prepared in-pipeline) on each rank node format and
+    walk shape -- v1 (1, 4-6: 6 / 8 / 10 / 12 trees per lane), v2 compact (3) -- equals
+    featurize + float64 X + predict on the wide layout (variant 0)."""
     from fdx import synth
     from fdx.pipeline import FraudPipeline
 
@@ -423,9 +397,41 @@ def test_fused_scoring_every_rank_format(dev, golden, variant):
             T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
     n = len(d["ts"])
     pipe = FraudPipeline(forest=f)
-    f.set_variant(1)
+    f.set_variant(0)
     _, p_ref = pipe.run(*args, 1500, 3000)
     f.set_variant(variant)
     p = torch.empty(n, dtype=torch.float64, device=dev)
     pipe.run_fused(*args, 1500, 3000, p, ops.workspace(f.workspace_size(n * 2), dev))
     np.testing.assert_array_equal(p.cpu().numpy(), p_ref.cpu().numpy())
+
+
+def test_terminal_windows_caller_workspace_abi(dev):
+    """fdx_terminal_windows through ctypes with a caller workspace (the call allocates
+    nothing): a workspace below fdx_terminal_windows_workspace_size(n) is refused with
+    FDX_E_WORKSPACE, the sized one gives the oracle's windows -- incl. a segment longer than
+    the kernel's 1,024-row LDS stage (its prefix counts live in the workspace)."""
+    import ctypes
+
+    from fdx import _lib
+
+    rng = np.random.default_rng(77)
+    ts, _, fr, seg = _edge_segments(rng, 30, 2500)
+    assert np.diff(seg).max() > 1024
+    n, W = len(ts), 3
+    L = _lib.load()
+    need = L.fdx_terminal_windows_workspace_size(n)
+    assert need >= 4 * n
+    win = (ctypes.c_int64 * W)(*[d * 86_400 * 10**9 for d in (1, 7, 30)])
+    tsd, frd, segd = T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev)
+    nb = torch.empty((W, n), dtype=torch.int32, device=dev)
+    risk = torch.empty((W, n), dtype=torch.float64, device=dev)
+    small = torch.empty(need - 256, dtype=torch.uint8, device=dev)
+    args = lambda ws: (ops._ptr(tsd), ops._ptr(frd), ops._ptr(segd), len(seg) - 1, n, 7 * 86_400 * 10**9, win, W,  # noqa: E731
+                       ops._ptr(nb), ops._ptr(risk), ops._ptr(ws), ws.numel(), ops._s())
+    assert L.fdx_terminal_windows(*args(small)) == -4  # FDX_E_WORKSPACE
+    assert b"workspace" in L.fdx_last_error()
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    assert L.fdx_terminal_windows(*args(ws)) == 0
+    onb, orisk = oracle.terminal_windows(ts, fr, seg, 7, (1, 7, 30))
+    np.testing.assert_array_equal(nb.cpu().numpy(), onb)
+    np.testing.assert_array_equal(risk.cpu().numpy(), orisk)

@@ -144,31 +144,6 @@ def test_fused_pipeline_hot_terminal_matches_oracle(dev, golden):
         np.testing.assert_array_equal(X[:, 3 + j], ref[c], err_msg=c)
 
 
-def test_terminal_records_at_scoring_slots(dev, monkeypatch):
-    """FDX_TERM_SLOTS form of run_fused: the terminal records written at the rows' scoring
-    slots (fdx_terminal_windows_grouped_dest over fdx_invert_slots), read in slot order by
-    the row assembly -- the same probabilities as the by-row records, every row."""
-    import os
-
-    from fdx import pipeline
-
-    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench_assets",
-                             "rf100_d20.npz"))
-    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
-              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
-    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
-    g = synth.generate_device(3000, 6000, 90, seed=5, device=dev)
-    n = g["ts"].numel()
-    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
-    ws = ops.workspace(forest.workspace_size(n * 2), dev)
-    p_row = torch.empty(n, dtype=torch.float64, device=dev)
-    FraudPipeline(forest=forest).run_fused(*args, 3000, 6000, p_row, ws)
-    monkeypatch.setattr(pipeline, "_TERM_SLOTS", True)
-    p_slot = torch.empty(n, dtype=torch.float64, device=dev)
-    FraudPipeline(forest=forest).run_fused(*args, 3000, 6000, p_slot, ws)
-    assert torch.equal(p_row, p_slot)
-
-
 def test_compact_records_equal_full_records(dev):
     """fdx_terminal_windows_grouped_compact: the 16-byte records unpack to the full count
     records (oracle), for the sorted single-run form and the multi-run owner form."""
@@ -189,7 +164,7 @@ def test_compact_records_equal_full_records(dev):
     np.testing.assert_array_equal(ops.compact_records_unpack(rec, len(ts)).cpu().numpy(), ref[order])
 
 
-def test_compact_records_overflow_rows(dev, golden, monkeypatch):
+def test_compact_records_overflow_rows(dev, golden):
     """Window counts above 2^21 - 1 (one terminal with 2.2M rows in one day, then later rows
     whose delayed windows hold all of them): those rows escape to full records in the overflow
     area -- exact; the run_fused row assembly reads both kinds."""
@@ -217,9 +192,6 @@ def test_compact_records_overflow_rows(dev, golden, monkeypatch):
     amt = T(np.round(rng.uniform(1, 300, n), 2), torch.float64, dev)
     pipe = FraudPipeline(forest=forest)
     _, p64 = pipe.run(tsd, cust, termd, amt, frd, 100, 2)
-    from fdx import pipeline
-
-    monkeypatch.setattr(pipeline, "_TERM_COMPACT", True)  # the fused path on compact records
-    proba = torch.empty(n, dtype=torch.float64, device=dev)
-    pipe.run_fused(tsd, cust, termd, amt, frd, 100, 2, proba)
+    proba = torch.empty(n, dtype=torch.float64, device=dev)  # the fused path on compact records
+    FraudPipeline(forest=forest, compact_records=True).run_fused(tsd, cust, termd, amt, frd, 100, 2, proba)
     assert torch.equal(proba, p64)

@@ -57,44 +57,9 @@ def test_oracle_ties(golden):
 
 
 def test_oracle_notebook_known_answers():
-    kat = json.load(open(os.path.join(GOLDEN, "notebook_kat.json")))
-    z = np.load(os.path.join(GOLDEN, "notebook_kat_inputs.npz"))
-    days = z["TX_TIME_DAYS"]
-    runs = {}
-    for name, mask in (("2024", days < 214), ("2025", days >= 214)):  # the notebook's two loads
-        f = oracle.featurize_arrays(z["TX_DATETIME"][mask], z["CUSTOMER_ID"][mask], z["TERMINAL_ID"][mask],
-                                    z["TX_AMOUNT"][mask], z["TX_FRAUD"][mask])
-        runs[name] = (z["TRANSACTION_ID"][mask], z["CUSTOMER_ID"][mask], z["TERMINAL_ID"][mask],
-                      z["TX_DATETIME"][mask], f)
-    customers = set(z["customers"].tolist())
-    rows = {}
-    for r in kat:
-        rows.setdefault((r["cell"], r["row"]), {})[r["column"].upper()] = r["value"]
-    checked = 0
-    for (cell, label), rec in rows.items():
-        tids, c, t, ts, f = runs["2025" if cell in (43, 51, 54) else "2024"]
-        if cell == 36:  # latest row per terminal (groupby.idxmax)
-            m = np.flatnonzero(t == int(rec["TERMINAL_ID"]))
-            i = m[np.argmax(ts[m])]
-        elif "TRANSACTION_ID" in rec:
-            hit = np.flatnonzero(tids == int(rec["TRANSACTION_ID"]))
-            assert len(hit) == 1, (cell, label)
-            i = hit[0]
-        else:
-            # cells 51/54 print the January frame's row position (TRANSACTION_ID 2051331 is
-            # position 0; the notebook's unstable time sort can shift tied rows by a few places)
-            m = np.flatnonzero(c == int(rec["CUSTOMER_ID"]))
-            i = m[np.argmin(np.abs(tids[m] - (2051331 + int(label))))]
-            assert abs(int(tids[i]) - (2051331 + int(label))) <= 3, (cell, label)
-        for col, s in rec.items():
-            if not (col.startswith("CUSTOMER_ID_") or col.startswith("TERMINAL_ID_") or col.startswith("TX_DURING")):
-                continue
-            if col.startswith("CUSTOMER_ID_") and c[i] not in customers:
-                continue
-            dec = len(s.split(".")[1]) if "." in s else 0
-            assert "%.*f" % (dec, f[col][i]) == s, (cell, label, col, f[col][i], s)
-            checked += 1
-    assert checked >= 500, checked
+    from kat_check import check_notebook_kat
+
+    check_notebook_kat(lambda ts, c, t, a, fr, tids: oracle.featurize_arrays(ts, c, t, a, fr))
 
 
 @pytest.mark.parametrize("name", ["forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"])

@@ -270,78 +270,3 @@ def test_rank_layout_v2_deployed_model():
     sel = np.arange(0, len(z["test_X"]), 16)
     proba, _ = walk_rank_v2(R, _z32(z["test_X"][sel], z["mean"], z["scale"]))
     np.testing.assert_array_equal(proba, z["test_proba1"][sel])
-
-
-def walk_rank_v3(R, z32):
-    """numpy model of k_forest_rank<.., P16 = 4> (pair_walk / pair_walk_nan): planes hold
-    (r + 1) << 16 (NaN 0xFFFFFFFF); node word [31:16] k+1 | [15:12] feature | [11:0] offset
-    of the children pair (in pairs) from the pair q holding the node; c = q + off * 8 bytes;
-    next = x <= word ? pair[c].lo : pair[c].hi; NaN: missing_go_to_left, leaves stay."""
-    n = z32.shape[0]
-    xs = np.zeros((n, 16), np.int64)
-    for f in range(min(z32.shape[1], 15)):
-        u = R["thr"][R["thr_off"][f]:R["thr_off"][f + 1]]
-        r = np.searchsorted(u, z32[:, f], side="left").astype(np.int64)
-        xs[:, f] = np.where(np.isnan(z32[:, f]), 0xFFFFFFFF, (r + 1) << 16)
-    nodes = R["nodes"].astype(np.int64)
-    assert len(nodes) % 2 == 0 and (R["root"] % 2 == 0).all()
-    acc = np.zeros(n)
-    rows = np.arange(n)
-    nt = len(R["root"])
-    leaves = np.zeros((n, nt), np.int32)
-    for t in range(nt):
-        p = np.full(n, R["root"][t], np.int64)          # word index of the chain's node
-        w = nodes[p]
-        for _ in range(int(R["depth"][t])):
-            q = p & ~1                                   # its pair
-            c = q + 2 * (w & 0xFFF)                      # children pair (word index)
-            x = xs[rows, (w >> 12) & 15]
-            left = x <= w
-            nan = x == 0xFFFFFFFF
-            leaf = (w & 0xFFF) == 0
-            left = np.where(nan, np.where(leaf, w >= 0x10000, R["ml"][p] != 0), left)
-            p = c + np.where(left, 0, 1)
-            w = nodes[p]
-        assert ((w & 0xFFF) == 0).all(), "walk did not end on leaves within depth"
-        acc = acc + R["lval"][p]
-        leaves[:, t] = R["orig"][p]
-    return acc / nt, leaves
-
-
-def test_rank_layout_v3_pairs_reproduce_sklearn(golden):
-    """v3 (sibling pairs, one LDS round trip per step): sklearn's leaves and proba on the
-    golden forests, NaN rows included in rf3's test rows."""
-    for name in ("forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"):
-        z = golden(name)
-        R = pack_rank2(z, version=3)
-        assert R is not None
-        proba, leaves = walk_rank_v3(R, _z32(z["X"], z["mean"], z["scale"]))
-        np.testing.assert_array_equal(leaves, z["leaves"])
-        np.testing.assert_array_equal(proba, z["proba"])
-
-
-def test_rank_layout_v3_bench_model_and_random_forests():
-    """The config-3 model fits v3 (every children pair within 4,095 pairs) and reproduces
-    sklearn; random deep trees with NaN rows reproduce the oracle; a tree whose right subtree
-    starts more than 4,095 pairs away is rejected (v1 / v2 serve it)."""
-    import os
-
-    from conftest import ROOT
-
-    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
-    R = pack_rank2(z, version=3)
-    assert R is not None
-    proba, _ = walk_rank_v3(R, _z32(z["check_X"], z["mean"], z["scale"]))
-    np.testing.assert_array_equal(proba, z["check_proba"])
-    rng = np.random.default_rng(31)
-    a = random_forest(rng, 4, 11, p_leaf=0.05)
-    R = pack_rank2(a, version=3)
-    assert R is not None
-    X = rng.normal(size=(3000, 15))
-    X[rng.random(X.shape) < 0.05] = np.nan
-    op, ol = oracle.forest_predict(X, a, want_leaves=True)
-    proba, leaves = walk_rank_v3(R, X.astype(np.float32))
-    np.testing.assert_array_equal(leaves, ol)
-    np.testing.assert_array_equal(proba, op)
-    big = random_forest(rng, 1, 14, p_leaf=0.0)
-    assert pack_rank2(big, version=3) is None

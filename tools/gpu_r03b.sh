@@ -1,0 +1,15 @@
+# Round 3, GPU call b: the whole GPU suite (incl. configs[0] / configs[4] tests), smoke, bench
+# default + compact records + the forest walk-shape sweep.
+set -eu
+O=gpurun_out/r03b
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+cat $O/smoke.log
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --sweep-variant 1,3,4,5,6 > $O/bench_base.json 2> $O/bench_base.err
+grep variant_sweep $O/bench_base.err || true
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --compact-records > $O/bench_compact.json 2> $O/bench_compact.err
+for f in base compact; do python3 -c "import json; d=json.load(open('$O/bench_$f.json')); print('$f', d['ms_per_step'], [(r['stage'], r['ms_in_step'], r.get('ms_isolated')) for r in d['kernels']['per_stage']])"; done
+echo r03b done
