@@ -57,6 +57,16 @@ STAGES = [
     ("assemble_rows", "K3", [("k_zfill_grouped_w3", 1)]),
     ("forest_traverse", "K3", [("k_forest_rank", "chunks")]),
 ]
+# N > 1 (ShardedPipeline): the terminal half is the exchange on the side stream instead
+EXCHANGE_STAGES = [
+    ("exchange_splits", "xGMI", [("k_key_map", 1), ("k_radix_hist", 1), ("k_radix_scatter", 1)]),
+    ("exchange_pack", "xGMI", [("k_exchange_pack", 1)]),
+    ("exchange_rows", "xGMI", []),
+    ("owner_windows", "K1-term", [("k_exchange_unpack", 1), ("k_radix_scatter<unsigned int, 9, 1>", 2),
+                                  ("k_terminal_g<true>", 1)]),
+    ("exchange_back", "xGMI", []),
+]
+XGMI_LINK_GBS = 153.0  # per point-to-point xGMI link and direction (7 links per GPU)
 
 
 def walk_steps_per_row(arrays):
@@ -321,8 +331,25 @@ def main():
     pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode, compact_records=args.compact_records)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
-    marks_all = []   # per timed step: [(stage, event), ...]
+    marks_all = []   # per timed step: {stage: (start event, end event)}
     trav = []        # per timed step: (start, end) of the forest traversal
+    shard_stats = {}  # the exchange's split sizes / bytes per peer (N > 1)
+
+    def make_mark(record):
+        """mark(stage, stream): a HIP event on the stage's stream, paired with the previous
+        event on that stream ("start" opens a stream); marks[stage] = (start, end)."""
+        marks, last = {}, {}
+
+        def mark(name, st):
+            if record:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(st)
+                if name == "start":
+                    marks.setdefault("_starts", []).append(e)
+                else:
+                    marks[name] = (last[id(st)], e)
+                last[id(st)] = e
+        return mark, marks
 
     if world > 1 or args.sharded:
         from fdx.distributed import ShardedPipeline
@@ -331,23 +358,16 @@ def main():
                              n_customers_local=args.customers)
 
         def step(record):
-            sp.run(ts, cust, term, amt, fr, proba, ws, trav if record else None)
+            mark, marks = make_mark(record)
+            sp.run(ts, cust, term, amt, fr, proba, ws, mark=mark, stats=shard_stats)
+            if record:
+                marks_all.append(marks)
+                trav.append(marks["forest_traverse"])
     else:
         lcust = cust  # rank 0 of a 1-GPU run: base 0
 
         def step(record, overlap=True, into=None):
-            marks = {}   # stage -> (start event, end event) on the stage's own stream
-
-            last = {}
-
-            def mark(name, st):
-                if record:
-                    e = torch.cuda.Event(enable_timing=True)
-                    e.record(st)
-                    if name != "start":
-                        marks[name] = (last[id(st)], e)
-                    last[id(st)] = e
-
+            mark, marks = make_mark(record)
             pipe.run_fused(ts, lcust, term, amt, fr, args.customers, args.terminals, proba, ws, mark=mark,
                            overlap=overlap)
             if record and into is not None:
@@ -381,7 +401,7 @@ def main():
         n_total = n_local
 
     iso_all = []  # per-kernel times: every stage alone on the GPU (after the timed region)
-    if marks_all and args.isolated_steps > 0:
+    if marks_all and args.isolated_steps > 0 and not (world > 1 or args.sharded):
         for _ in range(args.isolated_steps):
             step(True, overlap=False, into=iso_all)
         torch.cuda.synchronize()
@@ -445,8 +465,9 @@ def main():
                                                    "ds_read_b32, 32 independent reads in flight per lane"}
     if marks_all:
         table = []
-        names = [s for s, _, _ in STAGES]
-        for name, unit, kernels in STAGES:
+        for name, unit, kernels in STAGES + EXCHANGE_STAGES:
+            if name not in marks_all[0]:
+                continue
             ms = [mk[name][0].elapsed_time(mk[name][1]) for mk in marks_all]
             t_ms = sum(ms) / len(ms)
             row = {"stage": name, "unit": unit, "ms_in_step": round(t_ms, 4)}
@@ -459,6 +480,8 @@ def main():
         # §8(d) units: K1-cust = layout + walk, K3 = assemble + traverse
         units = {}
         for row in table:
+            if row["unit"] == "xGMI":
+                continue
             u = units.setdefault(row["unit"] + ("" if row["unit"] != "K2" else ":" + row["stage"]),
                                  {"ms": 0.0, "stages": [], "pmc": 0.0, "pmc_ok": True})
             u["ms"] += row["ms"]
@@ -490,6 +513,52 @@ def main():
                           "note": "ms_in_step = HIP events around each stage on its stream, mean over the timed steps; "
                                   "alg bytes = SURVEY.md §8(d) per tx x tx; pmc = rocprofv3 FETCH/WRITE per "
                                   "dispatch x dispatches (profiles/pmc_kernels.json)"}
+    if marks_all and (world > 1 or args.sharded):
+        # the exchange against the xGMI link roofline, and how much of it the customer half hides
+        def span(mk, a, b):  # ms from event a to event b
+            return a.elapsed_time(b)
+
+        ex_ms, link_ms, hidden_ms = [], [], []
+        for mk in marks_all:
+            t0m = mk["_starts"][0]                      # main stream start
+            ex_a, ex_b = mk["exchange_splits"][0], mk["exchange_back"][1]
+            cu_b = mk["customer_walk"][1]
+            a, b = span(mk, t0m, ex_a), span(mk, t0m, ex_b)
+            c = span(mk, t0m, cu_b)
+            ex_ms.append(b - a)
+            hidden_ms.append(max(0.0, min(b, c) - max(a, 0.0)))
+            link_ms.append(span(mk, *mk["exchange_rows"]) + span(mk, *mk["exchange_back"]))
+        mean = lambda v: sum(v) / len(v)  # noqa: E731
+        loc = torch.tensor([float(n_local), float(shard_stats.get("bytes_to_peers", 0)), mean(ex_ms), mean(link_ms),
+                            mean(hidden_ms)], dtype=torch.float64, device=dev)
+        if world > 1:
+            allr = [torch.empty_like(loc) for _ in range(world)]
+            dist.all_gather(allr, loc)
+            allr = torch.stack(allr).cpu().numpy()
+        else:
+            allr = loc.cpu().numpy()[None, :]
+        peers = max(world - 1, 1)
+        link_peak = min(peers, 7) * XGMI_LINK_GBS
+        per_rank = []
+        for r_ in range(world):
+            n_r, b_r, e_r, l_r, h_r = allr[r_]
+            per_rank.append({"rank": r_, "tx": int(n_r), "bytes_to_peers": int(b_r), "exchange_ms": round(e_r, 4),
+                             "link_ms": round(l_r, 4),
+                             "achieved_egress_GBs": round(b_r / (l_r * 1e-3) / 1e9, 1) if l_r > 0 else None,
+                             "hidden_share": round(h_r / e_r, 3) if e_r > 0 else None})
+        me = per_rank[rank]
+        out["exchange"] = {
+            "world": world, "per_rank": per_rank,
+            "send_rows_per_peer": shard_stats.get("send_rows"), "recv_rows_per_peer": shard_stats.get("recv_rows"),
+            "bytes_per_row": {"rows": shard_stats.get("row_bytes"), "reply": shard_stats.get("reply_bytes")},
+            "link_roofline": {"bound": "xgmi", "peers": world - 1, "peak_GBs": link_peak,
+                              "achieved_GBs": me["achieved_egress_GBs"],
+                              "frac": round(me["achieved_egress_GBs"] / link_peak, 4)
+                              if me["achieved_egress_GBs"] and world > 1 else None},
+            "note": "exchange_ms = side-stream span from the owner-key re-key to the reply all-to-all; link_ms = "
+                    "the two all-to-all phases (rows 16 B/row out, count records 24 B/row back); achieved = bytes "
+                    "this rank sends to its peers / link_ms against min(world-1, 7) x 153 GB/s; hidden_share = "
+                    "part of exchange_ms that overlaps the customer half (main-stream start to customer_walk end)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         data = {k: g[k].cpu().numpy() for k in ("ts", "customer", "terminal", "amount", "fraud")}
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, check_X, check_proba, args.cpu_score_rows)

@@ -798,13 +798,17 @@ struct Variant {
     int block, rows, group, rank, p16, pipe;
 };
 constexpr Variant kVariants[] = {
-    {512, 1, 4, 0, 0, 0},   // 0: wide layout
-    {1024, 1, 6, 1, 0, 2},  // 1: rank layout v1 (the default; r01/r02 sweeps: fastest of 57 shapes)
-    {1024, 1, 6, 1, 2, 2},  // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
-    {1024, 1, 6, 1, 3, 2},  // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
-    {1024, 1, 8, 1, 0, 2},  // 4-6: v1 with 8 / 10 / 12 walk chains per lane (latency-hiding study)
-    {1024, 1, 10, 1, 0, 2},
-    {1024, 1, 12, 1, 0, 2},
+    {512, 1, 4, 0, 0, 0},    // 0: wide layout
+    {1024, 1, 10, 1, 0, 2},  // 1: rank layout v1, 10 chains per lane (the default: r03 sweep, 7.63 vs
+                             //    8.43 ms for 6 chains at config 2; 12 chains spill, 11.7 ms)
+    {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
+    {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
+    {1024, 1, 6, 1, 0, 2},   // 4: v1, 6 chains (the r01/r02 default, fastest of 57 shapes then)
+    {1024, 1, 8, 1, 0, 2},   // 5-7: v1 chain / wait-group study
+    {1024, 1, 10, 1, 0, 5},
+    {1024, 1, 9, 1, 0, 3},
+    {1024, 1, 10, 1, 2, 2},  // 8: v2, 10 chains
+    {1024, 1, 10, 1, 3, 2},  // 9: compact v2, 10 chains
 };
 constexpr int kDefaultRankVariant = 1;
 constexpr int kDefaultRankV2Variant = 2;
@@ -2215,10 +2219,13 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             switch (F->variant) {
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
-                case 4: FDX_LAUNCH_RANK(1024, 1, 8, 0, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
-                case 6: FDX_LAUNCH_RANK(1024, 1, 12, 0, 2); break;
-                default: FDX_LAUNCH_RANK(1024, 1, 6, 0, 2); break;
+                case 4: FDX_LAUNCH_RANK(1024, 1, 6, 0, 2); break;
+                case 5: FDX_LAUNCH_RANK(1024, 1, 8, 0, 2); break;
+                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 0, 5); break;
+                case 7: FDX_LAUNCH_RANK(1024, 1, 9, 0, 3); break;
+                case 8: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
+                case 9: FDX_LAUNCH_RANK(1024, 1, 10, 3, 2); break;
+                default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
             }
 #undef FDX_LAUNCH_RANK
             FDX_LAUNCHED("k_forest_rank");

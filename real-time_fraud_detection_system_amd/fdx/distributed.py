@@ -135,29 +135,43 @@ def exchange_begin(K, term, world, group=None):
 
 
 def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30), delay_days=7,
-                    group=None, records=None):
+                    group=None, records=None, mark=None, stats=None):
     """Phase 2: all-to-all of the rows, owner-side terminal records, all-to-all back.
     Returns (reply [n_local, W] count records in send order, send_perm).
     records(rts, rterm_local, rfraud) -> [m, W] count records by receive position replaces
-    the owner-side batch windows (the streaming engine passes its incremental update)."""
+    the owner-side batch windows (the streaming engine passes its incremental update).
+    mark(name) is called after each phase is enqueued on the current stream (bench.py records
+    HIP events there); stats (a dict) receives the split sizes and bytes per peer."""
+    mk = mark or (lambda _name: None)
     send_perm, send_counts, recv_counts = state
     sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
     rec = K.exchange_pack(ts, term, fraud, send_perm)
     recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
+    mk("exchange_pack")
     alltoallv(recv, rec, rc, sc, group)
+    mk("exchange_rows")
     rts, rterm, rfr = K.exchange_unpack(recv, world)
     if records is not None:
         reply = records(rts, rterm, rfr)
-        back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
-        alltoallv(back, reply, sc, rc, group)
-        return back, send_perm
-    n_local_terms = (n_terminals_total + world - 1) // world
-    # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
-    # the records kernel handles such segments itself (no global time sort of the receive buffer)
-    reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days,
-                                     runs=world > 1)  # by receive index
+    else:
+        n_local_terms = (n_terminals_total + world - 1) // world
+        # stable re-key by local terminal id: a segment is one time-sorted run per source rank;
+        # the records kernel handles such segments itself (no global time sort of the receive buffer)
+        reply = K.terminal_records_rekey(rts, rterm, rfr, n_local_terms, delay_days, windows_days,
+                                         runs=world > 1)  # by receive index
+    mk("owner_windows")
     back = torch.empty((sum(sc), reply.shape[1]), dtype=torch.int64, device=reply.device)
     alltoallv(back, reply, sc, rc, group)
+    mk("exchange_back")
+    if stats is not None:
+        me = dist.get_rank(group)
+        row_b, rep_b = rec.element_size() * 2, reply.element_size() * reply.shape[1]
+        stats.update(send_rows=sc, recv_rows=rc,
+                     bytes_to_peers=sum(c for p, c in enumerate(sc) if p != me) * row_b
+                     + sum(c for p, c in enumerate(rc) if p != me) * rep_b,
+                     bytes_from_peers=sum(c for p, c in enumerate(rc) if p != me) * row_b
+                     + sum(c for p, c in enumerate(sc) if p != me) * rep_b,
+                     row_bytes=row_b, reply_bytes=rep_b)
     return back, send_perm
 
 
@@ -242,10 +256,15 @@ class ShardedPipeline:
         rc.check()
         return X[:, : p.n_features]
 
-    def run(self, ts, customer, terminal, amount, fraud, proba, ws, events=None, n_customers_local: int | None = None):
+    def run(self, ts, customer, terminal, amount, fraud, proba, ws, events=None, n_customers_local: int | None = None,
+            mark=None, stats=None):
         """featurize + score this rank's rows: the single-GPU scoring path (interleaved
         customer layout, FraudPipeline.run_fused) for the customer half; the terminal half
-        comes back from the owners as packed count records in send order."""
+        comes back from the owners as packed count records in send order.  mark(stage, stream)
+        after each stage is enqueued on its stream (bench.py's HIP events: the customer stages
+        on the caller's stream, the exchange phases on the side stream); stats: the split sizes
+        and bytes per peer of this step's exchange (exchange_finish)."""
+        mk = mark or (lambda _name, _st: None)
         p = self.pipe
         W = len(p.windows_days)
         base, n_local = self._range(n_customers_local)
@@ -256,23 +275,29 @@ class ShardedPipeline:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=ts.device, priority=_SHARD_SIDE_PRIORITY)
         side = self._side
+        mk("start", main)
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            mk("start", side)
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
+            mk("exchange_splits", side)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
         cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        mk("rekey_customer", main)
         # the exchange's split-size sync waits only for the (short) owner re-key on the side
         # stream; enqueueing the whole exchange before the layout's host sync keeps the side
         # stream busy while the customer re-key runs
         with torch.cuda.stream(side):
             back, send_perm = exchange_finish(GpuKernels, state, ts, terminal, fraud, self.world,
-                                              self.n_terminals_total, p.windows_days, p.delay_days, self.group)
+                                              self.n_terminals_total, p.windows_days, p.delay_days, self.group,
+                                              mark=lambda name: mk(name, side), stats=stats)
             sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
         scan = p.avg_mode == "scan"
         walk = W >= 3
         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, p.windows_days if walk else None,
                                   grouped=True)  # (host sync on main)
+        mk("customer_layout", main)
         rc.check()
         p._slots_hint = lay.its.numel()
         if scan:
@@ -281,16 +306,19 @@ class ShardedPipeline:
             inb, isum = ops.customer_windows_walk(lay, cseg)
         else:
             inb, isum = ops.customer_windows_interleaved(lay, cseg, p.windows_days)
+        mk("customer_walk", main)
         main.wait_stream(side)
         back.record_stream(main)
         sinv.record_stream(main)
         ws = p._forest_ws(lay.n_slots, ws, ts.device)
         ops.forest_prepare_grouped(p.forest, p.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, sinv, back, ws,
                                    n=lay.n_slots, val_is_sum=True)
+        mk("assemble_rows", main)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
         ops.forest_traverse_perm(p.forest, lay.n_slots, ws, proba, lay.irow)
+        mk("forest_traverse", main)
         if events is not None:
             b.record()
             events.append((a, b))

@@ -16,4 +16,6 @@ timeout -k 10 400 python3 bench_stream.py > $O/stream.json 2> $O/stream.err
 cat $O/stream.json
 timeout -k 10 400 python3 bench_stream.py --cdc > $O/stream_cdc.json 2> $O/stream_cdc.err
 cat $O/stream_cdc.json
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 6 --warmup 2 --sharded > $O/bench_sharded.json 2> $O/bench_sharded.err
+python3 -c "import json; d=json.load(open('$O/bench_sharded.json')); print('sharded', d['ms_per_step'], json.dumps(d.get('exchange')))"
 echo r03c done
