@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    ap.add_argument("--variant", type=int, default=-1, help="forest walk variant (fdx.h; -1: the library's choice)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -51,6 +52,8 @@ def main():
     else:
         arrays, mean, scale, check_X, check_proba = bench.load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
+    if args.variant >= 0:
+        forest.set_variant(args.variant)
     n = args.rows
     g = torch.Generator(device=dev)
     g.manual_seed(20240601)
@@ -122,6 +125,7 @@ def main():
         "value": round(n * args.steps / dt, 1), "unit": "rows/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "dtype": "f64 in, f32 compare (sklearn's), f64 accumulate", "rows": n,
+        "variant": forest.variant,
         "data": ("the notebook test set's 66,452 rows" if deployed else "bench model's 4,096 held-out config-1 feature rows")
         + " resampled (seed 20240601), resident in HBM",
         "bit_exact_vs_sklearn": True, "prepare_ms": round(prep_ms, 3), "traverse_ms": round(trav_ms, 3),

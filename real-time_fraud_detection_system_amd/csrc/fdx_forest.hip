@@ -793,7 +793,8 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 // per lane, G trees walked at once per lane (G independent LDS dependency chains), the
 // software-pipelined walk with waits grouped by PIPE chains.  p16 = the rank node / plane
 // format: 0 = v1 (u32 planes), 2 = v2 (32 threshold slots over u16 planes), 3 = v2 nodes over
-// 16 u16 planes (forests whose every feature fits one slot).
+// 16 u16 planes (forests whose every feature fits one slot), 4 = v1 nodes, no planes: the
+// lane's rank row stays in VGPRs (see reg_rank).
 struct Variant {
     int block, rows, group, rank, p16, pipe;
 };
@@ -809,6 +810,9 @@ constexpr Variant kVariants[] = {
     {1024, 1, 9, 1, 0, 3},
     {1024, 1, 10, 1, 2, 2},  // 8: v2, 10 chains
     {1024, 1, 10, 1, 3, 2},  // 9: compact v2, 10 chains
+    {1024, 1, 8, 1, 4, 2},   // 10: v1 nodes, register ranks (one ds_read per step, 10 LDS chunks instead of
+                             //     18): bit-exact, 16.3 vs 7.6 ms at config 2 (r03f; 6 and 9 chains the
+                             //     same, 10 spill) -- the 11-VALU feature select outweighs the LDS read
 };
 constexpr int kDefaultRankVariant = 1;
 constexpr int kDefaultRankV2Variant = 2;
@@ -983,17 +987,46 @@ constexpr uint32_t kOffMask = (P16 == 2 || P16 == 3) ? 0x7FFu : 0xFFFu;
 // 3 = the v2 node format over 16 u16 planes of 1,024 rows (32 KiB): forests whose every feature
 // fits one slot (slot = feature, the v1 row format); the node region starts at 32 KiB, so a
 // chunk holds a third more nodes than with 64 KiB of planes (fewer chunk launches per batch)
+// 4 = register ranks: no planes, the node region is the whole LDS
 template <int P16>
-constexpr uint32_t kNodeB = P16 == 3 ? 32768u : kRankNodeB;
+constexpr uint32_t kNodeB = P16 == 3 ? 32768u : P16 == 4 ? 0u : kRankNodeB;
+
+// P16 == 4: the lane's rank row -- 16 u16 ranks in 8 VGPRs, slot 15 = the v1 sentinel 0x4000 --
+// replaces the LDS row planes, so a step reads only its node.  The node's feature f (bits
+// [15:12] of s, the XORed node) is selected in registers: v_perm_b32 takes u16 f & 3 out of
+// each of the four VGPR pairs (selector bytes 2j, 2j + 1; the high bytes 0x0C give zeros),
+// then two v_bfi_b32 levels pick the pair by f >> 2 (masks = bits 14 and 15 of s
+// sign-extended).  11 VALU in place of one ds_read_b32 and its address op.
+__device__ __forceinline__ uint32_t reg_rank(const uint32_t (&w)[8], uint32_t s) {
+    const uint32_t sel = __builtin_amdgcn_ubfe(s, 12, 2) * 0x0202u + 0x0C0C0100u;
+    const uint32_t p0 = __builtin_amdgcn_perm(w[1], w[0], sel);
+    const uint32_t p1 = __builtin_amdgcn_perm(w[3], w[2], sel);
+    const uint32_t p2 = __builtin_amdgcn_perm(w[5], w[4], sel);
+    const uint32_t p3 = __builtin_amdgcn_perm(w[7], w[6], sel);
+    // one asm block: in C the compiler turns the 0 / -1 masks into v_cmp + v_cndmask through
+    // VCC (two more VALU and an s_nop per level), and around separate asm statements it pads
+    // with s_nop
+    uint32_t m, a, b, x;
+    asm("v_bfe_i32 %[m], %[s], 14, 1\n\t"
+        "v_bfi_b32 %[a], %[m], %[p1], %[p0]\n\t"
+        "v_bfi_b32 %[b], %[m], %[p3], %[p2]\n\t"
+        "v_bfe_i32 %[m], %[s], 15, 1\n\t"
+        "v_bfi_b32 %[x], %[m], %[b], %[a]"
+        : [m] "=&v"(m), [a] "=&v"(a), [b] "=&v"(b), [x] "=&v"(x)
+        : [s] "v"(s), [p0] "v"(p0), [p1] "v"(p1), [p2] "v"(p2), [p3] "v"(p3));
+    return x;
+}
 
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                          uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
+                                          uint32_t (&nd)[K], const uint8_t *__restrict__ mleft,
+                                          const uint32_t (&w)[8]) {
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        x[k] = P16 ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
-                   : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+        x[k] = P16 == 4 ? reg_rank(w, nd[k])
+               : P16    ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
+                        : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint32_t st;
@@ -1011,17 +1044,18 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
 
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                          uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft) {
+                                          uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft,
+                                          const uint32_t (&w)[8]) {
     int d = 0;
     for (; d + kExitEvery <= depth; d += kExitEvery) {
 #pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
+        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft, w);
         uint32_t moving = 0;  // leaves (and only leaves) have right offset 0
 #pragma unroll
         for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
         if (!__any(moving != 0)) return;
     }
-    for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
+    for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft, w);
 }
 
 // Walk trees [t, t+GG) for the R rows of this lane (chain k = r*GG + g); pa = final leaves.
@@ -1040,10 +1074,11 @@ __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
 // return in order): fewer issue slots per step.
 template <int P16, int K, int PW>
 __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                               uint32_t (&nd)[K], int depth) {
+                                               uint32_t (&nd)[K], int depth, const uint32_t (&w)[8]) {
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+    for (int k = 0; k < K; ++k)
+        x[k] = P16 == 4 ? reg_rank(w, nd[k]) : rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
     auto step = [&]() {
 #pragma unroll
         for (int g = 0; g < K; g += PW) {
@@ -1064,8 +1099,12 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (P16 == 4) {
+                x[k] = reg_rank(w, nd[k]);
+            } else {
+                x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     };
     int d = 0;
@@ -1084,7 +1123,7 @@ template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
                                            int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
-                                           uint32_t (&pa)[R * GG]) {
+                                           uint32_t (&pa)[R * GG], const uint32_t (&w)[8]) {
     constexpr int K = R * GG;
     uint32_t lane_base[K], nd[K];
     int dmax = 0;
@@ -1101,9 +1140,9 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
         }
     }
     if (any_nan)
-        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml, w);
     else
-        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
+        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w);
 }
 
 template <int K>
@@ -1184,7 +1223,8 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots
     constexpr int kPlaneRows = kRankPlaneRows;
     constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
-    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS
+    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : P16 == 4 ? 0 : kRankXWords;  // row-plane words in LDS
+    static_assert(P16 != 4 || R == 1, "register ranks: one row per lane");
     constexpr uint32_t kNB = kNodeB<P16>;
     if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
         const int c = blockIdx.y;
@@ -1195,7 +1235,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         first = 1;
         last = 0;
     }
-    static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
+    static_assert(P16 == 4 || BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
@@ -1242,11 +1282,16 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         int64_t row[R];
         bool ok[R];
         double a[R];
+        uint32_t w[8];  // P16 == 4: the lane's rank row, slot 15 = the sentinel
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             row[r] = base + r * BLOCK + tid;
             ok[r] = row[r] < r1;
-            if constexpr (P16 == 2) {
+            if constexpr (P16 == 4) {
+                w[0] = q0[r].x; w[1] = q0[r].y; w[2] = q0[r].z; w[3] = q0[r].w;
+                w[4] = q1[r].x; w[5] = q1[r].y; w[6] = q1[r].z;
+                w[7] = (q1[r].w & 0xFFFFu) | (kRankSentinel & 0xFFFF0000u);
+            } else if constexpr (P16 == 2) {
                 const uint32_t w[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                         q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
@@ -1271,7 +1316,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         int t = t0;
         for (; t + G <= t1; t += G) {
             uint32_t pa[K];
-            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
+            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa, w);
             if (pending) rank_accumulate<R, G>(a, pv);
             rank_leaf_values<K>(pa, node_base, lval, pv, kNB);
             if (tv) rank_tree_values<R, G>(pv, t, row, ok, tv, tv_n);
@@ -1284,7 +1329,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         if (nt == NT) {                                                                                    \
             uint32_t pt[R * NT];                                                                           \
             double vt[R * NT];                                                                             \
-            rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);           \
+            rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt, w);        \
             if (pending) rank_accumulate<R, G>(a, pv);                                                     \
             pending = false;                                                                               \
             rank_leaf_values<R * NT>(pt, node_base, lval, vt, kNB);                                        \
@@ -1607,12 +1652,13 @@ namespace fdx {
 namespace {
 int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
 // node format a variant runs on: 1 = rank layout v1, 2 = v2
-int variant_format(const Variant &v) { return v.p16 >= 2 ? 2 : 1; }
+int variant_format(const Variant &v) { return v.p16 == 2 || v.p16 == 3 ? 2 : 1; }
 int forest_format(const fdx_forest_s *F) { return F->rank_v2 ? 2 : 1; }
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
 constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
+constexpr int64_t kRankNodeCapReg = kLdsTotal / 4 - 1;  // register ranks: no planes
 
 bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
 
@@ -1621,7 +1667,7 @@ bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; 
 // (wide layout only: a rank-layout forest has every tree within the budget by construction).
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
-    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
+    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : v.p16 == 4 ? kRankNodeCapReg : kRankNodeCap)
                                      : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
@@ -2225,6 +2271,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 7: FDX_LAUNCH_RANK(1024, 1, 9, 0, 3); break;
                 case 8: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
                 case 9: FDX_LAUNCH_RANK(1024, 1, 10, 3, 2); break;
+                case 10: FDX_LAUNCH_RANK(1024, 1, 8, 4, 2); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
             }
 #undef FDX_LAUNCH_RANK

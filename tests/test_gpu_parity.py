@@ -305,7 +305,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(10)))
+@pytest.mark.parametrize("variant", list(range(11)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")
@@ -382,10 +382,11 @@ def test_fused_scoring_rank_table_overflows(dev):
     np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6, 7, 9])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6, 7, 9, 10])
 def test_fused_scoring_every_rank_format(dev, golden, variant):
     """The fused scoring path (rank rows prepared in-pipeline) on each rank node format and
-    walk shape -- v1 (1, 4-6: 6 / 8 / 10 / 12 trees per lane), v2 compact (3) -- equals
+    walk shape -- v1 (1, 4-7: 10 / 6 / 8 / 10 / 9 trees per lane), v2 compact (3, 9), v1 nodes
+    with register ranks (10) -- equals
     featurize + float64 X + predict on the wide layout (variant 0)."""
     from fdx import synth
     from fdx.pipeline import FraudPipeline
