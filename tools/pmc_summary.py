@@ -5,20 +5,31 @@ reads half the bytes of wide coalesced streaming reads, so traffic = 2*FETCH + W
 (upper estimate for the read side; ratios between variants are unaffected).
 
 usage: python tools/pmc_summary.py gpurun_out/pmc_r7 [kernel-substring ...]
+       python tools/pmc_summary.py profiles/r03e_pmc_raw k_forest   (the committed raw passes)
        python tools/pmc_summary.py --json out.json gpurun_out/pmc_r7   (per-kernel means)
 (reads <prefix>a ... <prefix>d directories)
 """
 import collections
 import csv
 import glob
+import gzip
+import os
 import sys
+
+
+def _passes(prefix):
+    """the passes' counter CSVs: rocprofv3 output dirs <prefix>a.. <prefix>d, or a committed
+    directory of gzipped passes (profiles/<tag>_pmc_raw/pass_*.csv.gz)"""
+    if os.path.isdir(prefix) and glob.glob(os.path.join(prefix, "pass_*.csv.gz")):
+        return [gzip.open(f, "rt") for f in sorted(glob.glob(os.path.join(prefix, "pass_*.csv.gz")))]
+    return [open(f) for d in sorted(glob.glob(prefix + "*")) for f in glob.glob(d + "/*/*counter_collection.csv")]
 
 
 def load(prefix):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
-    for d in sorted(glob.glob(prefix + "*")):
-        for f in glob.glob(d + "/*/*counter_collection.csv"):
-            rows = list(csv.DictReader(open(f)))
+    for fh in _passes(prefix):
+        with fh:
+            rows = list(csv.DictReader(fh))
             big = collections.defaultdict(int)
             for r in rows:
                 big[r["Kernel_Name"]] = max(big[r["Kernel_Name"]], int(r["Grid_Size"]))
