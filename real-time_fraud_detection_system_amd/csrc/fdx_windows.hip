@@ -267,21 +267,32 @@ __global__ void __launch_bounds__(256) k_interleave(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            int32_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound (starts rise)
-            for (int64_t t = lane; t < L; t += kWave) {
-                const int64_t tv = in_lds ? lts[t] : __builtin_nontemporal_load(gts + t * gstride);
-                for (int w = 0; w < n_win; ++w) {
-                    const int64_t bound = tv - win.w[w];
-                    int64_t a = prev[w], e = t;  // first k in [prev, t] with ts_k > bound (k = t qualifies)
-                    while (a < e) {
-                        const int64_t m = (a + e) >> 1;
-                        const int64_t x = in_lds ? lts[m] : __builtin_nontemporal_load(gts + m * gstride);
-                        if (x > bound) e = m; else a = m + 1;
+            // one loop per memory space (a load through `in_lds ? lds : global` compiles to a
+            // flat load, which takes the vector-memory path even for LDS addresses), windows
+            // unrolled (a runtime-indexed prev[] became a chain of v_cndmask per access)
+            auto search = [&](auto T) {
+                int32_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound (starts rise)
+                for (int64_t t = lane; t < L; t += kWave) {
+                    const int64_t tv = T(t);
+#pragma unroll
+                    for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                        if (w < n_win) {
+                            const int64_t bound = tv - win.w[w];
+                            int64_t a = prev[w], e = t;  // first k in [prev, t] with ts_k > bound (k = t qualifies)
+                            while (a < e) {
+                                const int64_t m = (a + e) >> 1;
+                                if (T(m) > bound) e = m; else a = m + 1;
+                            }
+                            prev[w] = (int32_t)a;
+                            starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = (int32_t)a;
+                        }
                     }
-                    prev[w] = (int32_t)a;
-                    starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = (int32_t)a;
                 }
-            }
+            };
+            if (in_lds)
+                search([&](int64_t j) { return lts[j]; });
+            else
+                search([&](int64_t j) { return __builtin_nontemporal_load(gts + j * gstride); });
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -296,7 +307,19 @@ __global__ void __launch_bounds__(256) k_interleave(
 constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
 // walk length classes: groups whose longest segment has >= kWalkSplitRows rows use the 256-row
 // ring on the fork stream (fdx_customer_windows_walk)
-constexpr int kWalkSplitRows = 480;
+#ifndef FDX_WALK_SPLIT  // walk launch shape: compile-time A/B only (tools/build_ab.sh, tools/walk_ab.py)
+#define FDX_WALK_SPLIT 480
+#endif
+#ifndef FDX_WALK_LP  // waves per group, long class
+#define FDX_WALK_LP 2
+#endif
+#ifndef FDX_WALK_SP  // waves per group, short class
+#define FDX_WALK_SP 1
+#endif
+#ifndef FDX_WALK_SINGLE  // one launch (256-row ring, FDX_WALK_LP waves per group) for every group
+#define FDX_WALK_SINGLE 0
+#endif
+constexpr int kWalkSplitRows = FDX_WALK_SPLIT;
 
 // kRing rows per segment stay in LDS.  Launched once per ring size over length classes of
 // groups (a block outside [lg_min, lg_max) exits at once): long segments belong to busy
@@ -457,7 +480,7 @@ __global__ void __launch_bounds__(64) k_customer_ring(
 // the amounts ride in the LDS ring (8 B per row), so more waves fit per CU.
 // starts: segment-contiguous (k_interleave<true>); nullptr = in nb_out, slot layout, overwritten
 // by the counts.
-template <int S_MAX, int kRing>
+template <int S_MAX, int kRing, int P>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
@@ -468,31 +491,48 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     constexpr int kRingEl = kRing * S_MAX + kWave;             // + one miss slot per lane
     __shared__ double r_amt[kRingEl];
     const int lane = threadIdx.x;
-    const int64_t g = blockIdx.x;
+    // P waves per group: wave h walks the group's segments [seg0, seg0 + Sw) (sorted by
+    // decreasing length, so its first is its longest, Lw rows); the length class is the group's
+    const int64_t g = blockIdx.x / P;
+    const int h = (int)(blockIdx.x % P);
+    const int Sh = (S + P - 1) / P, seg0 = h * Sh;
     const int64_t s0 = sorder[g * S];
     const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
     if (Lg < lg_min || Lg >= lg_max) return;  // another launch's length class
+    if (seg0 >= S || g * S + seg0 >= n_seg) return;
+    const int Sw = min(Sh, (int)min<int64_t>(S - seg0, n_seg - g * S - seg0));
+    const int64_t sw0 = sorder[g * S + seg0];
+    const int32_t Lw = (int32_t)(seg_off[sw0 + 1] - seg_off[sw0]);
     const int l = lane / n_win, wi = lane - l * n_win;
-    const int64_t si = g * S + l;
-    const bool active = l < S && si < n_seg;
-    const int64_t s = active ? sorder[si] : 0;
+    const bool active = l < Sw;
+    const int64_t s = active ? sorder[g * S + seg0 + l] : 0;
     const int32_t L = active ? (int32_t)(seg_off[s + 1] - seg_off[s]) : 0;
     const int64_t gbase = goff[g];
-    const double *g_amt = iamt + gbase + l;  // row t of this lane's segment: g_amt[t * S]
-    int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + l;
-    double *sm = sum_out + (int64_t)wi * n_slots + gbase + l;
+    const double *g_amt = iamt + gbase + seg0 + l;  // row t of this lane's segment: g_amt[t * S]
+    int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + seg0 + l;
+    double *sm = sum_out + (int64_t)wi * n_slots + gbase + seg0 + l;
+    // chunk element e = lane + j * 64 of this wave's Sw segments: row e / Sw, segment e % Sw --
+    // the same for every chunk, so its slot offset and ring position are computed once
+    int32_t e_src[kPer], e_ring[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int e = lane + j * kWave;
+        const int tt = e / Sw, ll = e - tt * Sw;
+        e_src[j] = tt * S + ll;
+        e_ring[j] = tt * S_MAX + ll;
+    }
     double pam[kPer];
     int32_t pst[kChunk];
     auto fetch = [&](int32_t t0) {
-        const int n_el = min(kChunk, Lg - t0) * S;
-        const int64_t src0 = gbase + (int64_t)t0 * S;
+        const int n_el = min(kChunk, Lw - t0) * Sw;
+        const int64_t src0 = gbase + (int64_t)t0 * S + seg0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int e = lane + j * kWave;
-            if (e < n_el) pam[j] = iamt[src0 + e];
+            if (e < n_el) pam[j] = iamt[src0 + e_src[j]];
         }
         if (starts) {
-            const int32_t *sp = starts + (int64_t)wi * n_slots + gbase + (int64_t)l * Lg + t0;
+            const int32_t *sp = starts + (int64_t)wi * n_slots + gbase + (int64_t)(seg0 + l) * Lg + t0;
 #pragma unroll
             for (int j = 0; j < kChunk; ++j)
                 if (t0 + j < L) pst[j] = sp[j];
@@ -503,15 +543,12 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         }
     };
     auto commit = [&](int32_t t0) {
-        const int n_el = min(kChunk, Lg - t0) * S;
-        const int ring0 = t0 & (kRing - 1);
+        const int n_el = min(kChunk, Lw - t0) * Sw;
+        const int ring0 = (t0 & (kRing - 1)) * S_MAX;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
             const int e = lane + j * kWave;
-            if (e < n_el) {
-                const int tt = e / S, ll = e - tt * S;
-                r_amt[(ring0 + tt) * S_MAX + ll] = pam[j];
-            }
+            if (e < n_el) r_amt[ring0 + e_ring[j]] = pam[j];
         }
     };
     double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
@@ -524,7 +561,7 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (t0 + kChunk < Lg) fetch(t0 + kChunk);  // in flight while this chunk is walked
+        if (t0 + kChunk < Lw) fetch(t0 + kChunk);  // in flight while this chunk is walked
         const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -578,10 +615,10 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     };
     int32_t nb_a[kChunk], nb_b[kChunk];
     double val_a[kChunk], val_b[kChunk];
-    if (Lg > 0) fetch(0);
-    for (int32_t t0 = 0; t0 < Lg; t0 += 2 * kChunk) {
+    if (Lw > 0) fetch(0);
+    for (int32_t t0 = 0; t0 < Lw; t0 += 2 * kChunk) {
         chunk(t0, nb_a, val_a);
-        if (t0 + kChunk < Lg) chunk(t0 + kChunk, nb_b, val_b);
+        if (t0 + kChunk < Lw) chunk(t0 + kChunk, nb_b, val_b);
     }
 }
 
@@ -618,70 +655,78 @@ __global__ void __launch_bounds__(64) k_customer_scan(
         const int64_t b = seg_off[s], L = seg_off[s + 1] - b;
         if (L <= 0) continue;
         const bool in_lds = L <= kScanLds;
-        double *E = in_lds ? s_e : ge + b + s;  // L + 1 entries
-        int32_t *C = in_lds ? s_c : gc + b + s;
         const int64_t *T = gts + b;
         const int64_t obase = sorder ? (int64_t)goff[si / S] + si % S : b;
         const int64_t ostride = sorder ? S : 1;
-        if (lane == 0) {
-            E[0] = 0.0;
-            C[0] = 0;
-        }
-        double carry = 0.0;
-        int32_t ccarry = 0;
-        for (int64_t t0 = 0; t0 < L; t0 += kWave) {
-            const int64_t t = t0 + lane;
-            double v = 0.0;
-            int32_t c = 0;
-            if (t < L) {
-                const double a = gamt[b + t];
-                if (in_lds) s_ts[t] = T[t];
-                if (a == a) {
-                    v = a;
-                    c = 1;
-                }
+        // E / C: L + 1 entries in LDS or in the segment's scratch range; the body is expanded once
+        // per memory space (through a runtime-selected pointer every access is a flat one)
+        auto body = [&](double *E, int32_t *C, auto ts_at) {
+            if (lane == 0) {
+                E[0] = 0.0;
+                C[0] = 0;
             }
+            double carry = 0.0;
+            int32_t ccarry = 0;
+            for (int64_t t0 = 0; t0 < L; t0 += kWave) {
+                const int64_t t = t0 + lane;
+                double v = 0.0;
+                int32_t c = 0;
+                if (t < L) {
+                    const double a = gamt[b + t];
+                    if (in_lds) s_ts[t] = T[t];
+                    if (a == a) {
+                        v = a;
+                        c = 1;
+                    }
+                }
 #pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const double u = __shfl_up(v, d, kWave);
-                const int32_t uc = __shfl_up(c, d, kWave);
-                if (lane >= d) {
-                    v += u;
-                    c += uc;
+                for (int d = 1; d < kWave; d <<= 1) {
+                    const double u = __shfl_up(v, d, kWave);
+                    const int32_t uc = __shfl_up(c, d, kWave);
+                    if (lane >= d) {
+                        v += u;
+                        c += uc;
+                    }
+                }
+                const double e = carry + v;
+                const int32_t cc = ccarry + c;
+                if (t < L) {
+                    E[t + 1] = e;
+                    C[t + 1] = cc;
+                }
+                carry = __shfl(e, kWave - 1, kWave);
+                ccarry = __shfl(cc, kWave - 1, kWave);
+            }
+            if (!in_lds) __threadfence();  // this wave's scratch writes before its reads below
+            wave_sync();
+            int64_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound
+            for (int64_t t = lane; t < L; t += kWave) {
+                const int64_t tv = ts_at(t);
+                const double et = E[t + 1];
+                const int32_t ct = C[t + 1];
+#pragma unroll
+                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                    if (w < n_win) {
+                        const int64_t bound = tv - win.w[w];
+                        int64_t a = prev[w], e = t;  // first j in [prev, t] with ts_j > bound (j = t qualifies)
+                        while (a < e) {
+                            const int64_t m = (a + e) >> 1;
+                            if (ts_at(m) > bound) e = m; else a = m + 1;
+                        }
+                        prev[w] = a;
+                        const int32_t nb = ct - C[a];
+                        const double sum = nb > 0 ? et - E[a] : __builtin_nan("");
+                        const int64_t o = (int64_t)w * n_out + obase + t * ostride;
+                        nb_out[o] = nb;
+                        val_out[o] = val_is_sum ? sum : sum / (double)nb;
+                    }
                 }
             }
-            const double e = carry + v;
-            const int32_t cc = ccarry + c;
-            if (t < L) {
-                E[t + 1] = e;
-                C[t + 1] = cc;
-            }
-            carry = __shfl(e, kWave - 1, kWave);
-            ccarry = __shfl(cc, kWave - 1, kWave);
-        }
-        if (!in_lds) __threadfence();  // this wave's scratch writes before its reads below
-        wave_sync();
-        auto ts_at = [&](int64_t j) -> int64_t { return in_lds ? s_ts[j] : T[j]; };
-        int64_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound
-        for (int64_t t = lane; t < L; t += kWave) {
-            const int64_t tv = ts_at(t);
-            const double et = E[t + 1];
-            const int32_t ct = C[t + 1];
-            for (int w = 0; w < n_win; ++w) {
-                const int64_t bound = tv - win.w[w];
-                int64_t a = prev[w], e = t;  // first j in [prev, t] with ts_j > bound (j = t qualifies)
-                while (a < e) {
-                    const int64_t m = (a + e) >> 1;
-                    if (ts_at(m) > bound) e = m; else a = m + 1;
-                }
-                prev[w] = a;
-                const int32_t nb = ct - C[a];
-                const double sum = nb > 0 ? et - E[a] : __builtin_nan("");
-                const int64_t o = (int64_t)w * n_out + obase + t * ostride;
-                nb_out[o] = nb;
-                val_out[o] = val_is_sum ? sum : sum / (double)nb;
-            }
-        }
+        };
+        if (in_lds)
+            body(s_e, s_c, [&](int64_t j) { return s_ts[j]; });
+        else
+            body(ge + b + s, gc + b + s, [&](int64_t j) { return T[j]; });
         wave_sync();
     }
 }
@@ -884,32 +929,32 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
         // L1 lines another wave of this CU may hold for a neighbouring segment's scratch
         if (!in_lds) __threadfence();
         wave_sync();
-        // timestamps and prefix counts F(j) = # fraud rows in [0, j) of the segment
-        auto T = [&](int64_t j) -> int64_t { return in_lds ? lts[j] : __builtin_nontemporal_load(gts + b + j); };
-        auto F = [&](int64_t j) -> int32_t {
-            return in_lds ? lf[j] : (j == 0 ? 0 : __builtin_nontemporal_load(scratch + b + j - 1));
-        };
-        auto ub = [&](int64_t lo, int64_t hi, int64_t x) -> int64_t {  // first j in [lo, hi) with T(j) > x
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (T(mid) <= x) lo = mid + 1; else hi = mid;
-            }
-            return lo;
-        };
+        // timestamps and prefix counts F(j) = # fraud rows in [0, j) of the segment, one accessor
+        // pair per memory space: every loop below is instantiated for each (a load through
+        // `in_lds ? lds : global` compiles to a flat load, which takes the vector-memory path and
+        // its latency even for LDS addresses -- the binary searches are chains of such loads)
+        auto T_lds = [&](int64_t j) -> int64_t { return lts[j]; };
+        auto F_lds = [&](int64_t j) -> int32_t { return lf[j]; };
+        auto T_glb = [&](int64_t j) -> int64_t { return __builtin_nontemporal_load(gts + b + j); };
+        auto F_glb = [&](int64_t j) -> int32_t { return j == 0 ? 0 : __builtin_nontemporal_load(scratch + b + j - 1); };
         int nruns = 1;
         int32_t *lr = in_lds ? s_runs[RUNS ? wv : 0] : reinterpret_cast<int32_t *>(lts);
         const int max_runs = in_lds ? kMaxRuns : kMaxRunsLong;
         if (RUNS) {  // run starts: wherever ts descends
             if (lane == 0) lr[0] = 0;
-            int nr = 1;
-            for (int64_t c = 0; c < L; c += kWave) {
-                const int64_t j = c + lane;
-                const bool dsc = j > 0 && j < L && T(j) < T(j - 1);
-                const uint64_t m = __ballot(dsc);
-                const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
-                if (dsc && at < max_runs) lr[at] = (int32_t)j;
-                nr += __popcll(m);
-            }
+            auto find_runs = [&](auto T) {
+                int nr = 1;
+                for (int64_t c = 0; c < L; c += kWave) {
+                    const int64_t j = c + lane;
+                    const bool dsc = j > 0 && j < L && T(j) < T(j - 1);
+                    const uint64_t m = __ballot(dsc);
+                    const int at = nr + __popcll(m & ((1ull << lane) - 1ull));
+                    if (dsc && at < max_runs) lr[at] = (int32_t)j;
+                    nr += __popcll(m);
+                }
+                return nr;
+            };
+            const int nr = in_lds ? find_runs(T_lds) : find_runs(T_glb);
             if (lane == 0 && nr <= max_runs) lr[nr] = (int32_t)L;
             nruns = nr;
             wave_sync();
@@ -969,95 +1014,108 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                 merged = true;
             }
         }
-        for (int64_t i = lane; i < L; i += kWave) {
-            const int64_t t = T(i);
-            // merged: i is a position in the merged order; its record belongs to staging index qi
-            const int64_t qi = merged ? (int64_t)(s_q[RUNS ? wv : 0][i] & 0x7FFF) : i;
-            const int64_t row = dest_of(b + qi);
-            int32_t nbh = 0, frh = 0;
-            int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
-            if (!RUNS || nruns == 1 || merged) {
-                const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
-                nbh = (int32_t)hi;
-                frh = F(hi);
-#pragma unroll
-                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
-                    if (w < n_win) {
-                        const int64_t lo = ub(0, hi, t - delay - win.w[w]);
-                        cn[w] = (int32_t)(hi - lo);
-                        cf[w] = frh - F(lo);
-                    }
+        auto rows_loop = [&](auto T, auto F) {
+            auto ub = [&](int64_t lo, int64_t hi, int64_t x) -> int64_t {  // first j in [lo, hi) with T(j) > x
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (T(mid) <= x) lo = mid + 1; else hi = mid;
                 }
-            } else if (nruns <= max_runs) {
-                for (int r = 0; r < nruns; ++r) {
-                    const int64_t h = ub(lr[r], lr[r + 1], t - delay);
-                    nbh += (int32_t)(h - lr[r]);
-                    frh += F(h) - F(lr[r]);
-                }
-#pragma unroll
-                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
-                    if (w < n_win) {
-                        int32_t nbl = 0, frl = 0;
-                        for (int r = 0; r < nruns; ++r) {
-                            const int64_t lo = ub(lr[r], lr[r + 1], t - delay - win.w[w]);
-                            nbl += (int32_t)(lo - lr[r]);
-                            frl += F(lo) - F(lr[r]);
+                return lo;
+            };
+            for (int64_t i = lane; i < L; i += kWave) {
+                const int64_t t = T(i);
+                // merged: i is a position in the merged order; its record belongs to staging index qi
+                const int64_t qi = merged ? (int64_t)(s_q[RUNS ? wv : 0][i] & 0x7FFF) : i;
+                const int64_t row = dest_of(b + qi);
+                int32_t nbh = 0, frh = 0;
+                int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
+                if (!RUNS || nruns == 1 || merged) {
+                    const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
+                    nbh = (int32_t)hi;
+                    frh = F(hi);
+    #pragma unroll
+                    for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                        if (w < n_win) {
+                            const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                            cn[w] = (int32_t)(hi - lo);
+                            cf[w] = frh - F(lo);
                         }
-                        cn[w] = nbh - nbl;
-                        cf[w] = frh - frl;
+                    }
+                } else if (nruns <= max_runs) {
+                    for (int r = 0; r < nruns; ++r) {
+                        const int64_t h = ub(lr[r], lr[r + 1], t - delay);
+                        nbh += (int32_t)(h - lr[r]);
+                        frh += F(h) - F(lr[r]);
+                    }
+    #pragma unroll
+                    for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                        if (w < n_win) {
+                            int32_t nbl = 0, frl = 0;
+                            for (int r = 0; r < nruns; ++r) {
+                                const int64_t lo = ub(lr[r], lr[r + 1], t - delay - win.w[w]);
+                                nbl += (int32_t)(lo - lr[r]);
+                                frl += F(lo) - F(lr[r]);
+                            }
+                            cn[w] = nbh - nbl;
+                            cf[w] = frh - frl;
+                        }
+                    }
+                } else {  // more unsorted runs than the run list holds: count directly (any order)
+                    int32_t nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
+                    for (int64_t j = 0; j < L; ++j) {
+                        const int64_t tj = T(j);
+                        if (tj > t - delay) continue;
+                        const int fj = F(j + 1) - F(j);
+                        ++nbh;
+                        frh += fj;
+                        for (int w = 0; w < n_win; ++w)
+                            if (tj <= t - delay - win.w[w]) {
+                                ++nbl[w];
+                                frl[w] += fj;
+                            }
+                    }
+    #pragma unroll
+                    for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                        cn[w] = nbh - nbl[w];
+                        cf[w] = frh - frl[w];
                     }
                 }
-            } else {  // more unsorted runs than the run list holds: count directly (any order)
-                int32_t nbl[FDX_MAX_WINDOWS] = {}, frl[FDX_MAX_WINDOWS] = {};
-                for (int64_t j = 0; j < L; ++j) {
-                    const int64_t tj = T(j);
-                    if (tj > t - delay) continue;
-                    const int fj = F(j + 1) - F(j);
-                    ++nbh;
-                    frh += fj;
+                if (compact_n > 0) {  // W = 3 compact record (+ the full record in the overflow area)
+                    const bool fits = cn[0] <= kCompactMax && cn[1] <= kCompactMax && cn[2] <= kCompactMax;
+                    int64_t lo, hi;
+                    if (fits) {
+                        lo = (int64_t)cn[0] | ((int64_t)cn[1] << kCompactBits) | ((int64_t)cn[2] << (2 * kCompactBits));
+                        hi = (int64_t)cf[0] | ((int64_t)cf[1] << kCompactBits) | ((int64_t)cf[2] << (2 * kCompactBits));
+                    } else {
+                        const int64_t off = 2 * compact_n + 3 * row;
+    #pragma unroll
+                        for (int w = 0; w < 3; ++w) rec_out[off + w] = term_word(cn[w], cf[w]);
+                        lo = off | INT64_MIN;
+                        hi = 0;
+                    }
+                    *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
+                } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
+                    // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
+                    // 16-byte alignment) instead of three: fewer random write transactions
+                    int64_t *dst = rec_out + row * 3;
+                    const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
+                    if ((row & 1) == 0) {
+                        *reinterpret_cast<longlong2 *>(dst) = make_longlong2(w0, w1);
+                        dst[2] = w2;
+                    } else {
+                        dst[0] = w0;
+                        *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(w1, w2);
+                    }
+                } else {
                     for (int w = 0; w < n_win; ++w)
-                        if (tj <= t - delay - win.w[w]) {
-                            ++nbl[w];
-                            frl[w] += fj;
-                        }
-                }
-#pragma unroll
-                for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
-                    cn[w] = nbh - nbl[w];
-                    cf[w] = frh - frl[w];
+                        term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, cn[w], cf[w]);
                 }
             }
-            if (compact_n > 0) {  // W = 3 compact record (+ the full record in the overflow area)
-                const bool fits = cn[0] <= kCompactMax && cn[1] <= kCompactMax && cn[2] <= kCompactMax;
-                int64_t lo, hi;
-                if (fits) {
-                    lo = (int64_t)cn[0] | ((int64_t)cn[1] << kCompactBits) | ((int64_t)cn[2] << (2 * kCompactBits));
-                    hi = (int64_t)cf[0] | ((int64_t)cf[1] << kCompactBits) | ((int64_t)cf[2] << (2 * kCompactBits));
-                } else {
-                    const int64_t off = 2 * compact_n + 3 * row;
-#pragma unroll
-                    for (int w = 0; w < 3; ++w) rec_out[off + w] = term_word(cn[w], cf[w]);
-                    lo = off | INT64_MIN;
-                    hi = 0;
-                }
-                *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
-            } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
-                // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
-                // 16-byte alignment) instead of three: fewer random write transactions
-                int64_t *dst = rec_out + row * 3;
-                const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
-                if ((row & 1) == 0) {
-                    *reinterpret_cast<longlong2 *>(dst) = make_longlong2(w0, w1);
-                    dst[2] = w2;
-                } else {
-                    dst[0] = w0;
-                    *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(w1, w2);
-                }
-            } else {
-                for (int w = 0; w < n_win; ++w)
-                    term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, cn[w], cf[w]);
-            }
-        }
+        };
+        if (in_lds)
+            rows_loop(T_lds, F_lds);
+        else
+            rows_loop(T_glb, F_glb);
         wave_sync();
     }
 }
@@ -1455,20 +1513,28 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     // ring on a forked stream, concurrently with the rest on the 128-row ring (twice the
     // blocks per CU); the class boundary is kWalkSplitRows.
     constexpr int split = kWalkSplitRows;
+#define FDX_WALK(SM, RING, P, STREAM, LO, HI)                                                                 \
+    hipLaunchKernelGGL((k_customer_walk<SM, RING, P>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, STREAM,  \
+                       iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, \
+                       LO, HI);                                                                                \
+    FDX_LAUNCHED("k_customer_walk")
+#if FDX_WALK_SINGLE
+    (void)split;
+    FDX_WALK((21 + FDX_WALK_LP - 1) / FDX_WALK_LP, 256, FDX_WALK_LP, st, 0, INT32_MAX);
+    return FDX_OK;
+#else
     ForkStream *f;
     int rc = fork_stream(&f);
     if (rc) return rc;
     FDX_HIP(hipEventRecord(f->fork, st));
     FDX_HIP(hipStreamWaitEvent(f->side, f->fork, 0));
-    hipLaunchKernelGGL((k_customer_walk<21, 256>), dim3((unsigned)n_groups), dim3(64), 0, f->side, iamt_d, seg_off_d,
-                       sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, split, INT32_MAX);
-    FDX_LAUNCHED("k_customer_walk");
-    hipLaunchKernelGGL((k_customer_walk<21, 128>), dim3((unsigned)n_groups), dim3(64), 0, st, iamt_d, seg_off_d,
-                       sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, 0, split);
-    FDX_LAUNCHED("k_customer_walk");
+    FDX_WALK((21 + FDX_WALK_LP - 1) / FDX_WALK_LP, 256, FDX_WALK_LP, f->side, split, INT32_MAX);
+    FDX_WALK((21 + FDX_WALK_SP - 1) / FDX_WALK_SP, 128, FDX_WALK_SP, st, 0, split);
     FDX_HIP(hipEventRecord(f->join, f->side));
     FDX_HIP(hipStreamWaitEvent(st, f->join, 0));
     return FDX_OK;
+#endif
+#undef FDX_WALK
 }
 
 extern "C" int fdx_customer_windows_interleaved(const int64_t *its_d, const double *iamt_d,

@@ -311,6 +311,9 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
                                               _ptr(its), _ptr(iamt), _ptr(irow), _ptr(starts), max_slots,
                                               ctypes.byref(ns), _ptr(ws), ws.numel(), _s(stream))
         if rc == -4 and ns.value > max_slots:
+            if ns.value > S * n:  # every group pads to its longest segment: <= S slots per row
+                raise FdxError(f"customer layout: {ns.value} slots for {n} rows -- inconsistent segment "
+                               "offsets (keys outside [0, n_keys)?)")
             max_slots = ns.value
             continue
         check(rc, "fdx_customer_layout")

@@ -143,19 +143,27 @@ class FraudPipeline:
             self._side = torch.cuda.Stream(device=ts_ns.device)
         side = self._side if overlap else main
         mk("start", main)
-        if validate:
-            rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", main),
-                  ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", main))
         side.wait_stream(main)
+        # customer half first (caller's stream, the critical path): the re-key carries ts and
+        # amount into grouped order
+        scan = self.avg_mode == "scan"
+        walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
+        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
+        mk("rekey_customer", main)
         # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
         # perm); the records come out in input row order, read by the row assembly through irow.
         # Allocated under the side stream's context, so that the caching allocator hands
         # these buffers to nothing on the main stream while the side stream still uses them.
+        # The id range checks run here too (off the critical path; out-of-range ids cannot
+        # make the re-keys write out of bounds) and are read at the layout's host sync.
         compact = self.compact_records and W == 3
         with torch.cuda.stream(side):
             mk("start", side)
             tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
             mk("rekey_terminal", side)
+            if validate:
+                rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", side),
+                      ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", side))
             if compact:
                 trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
                                                     windows_days=self.windows_days, stream=side)
@@ -163,13 +171,8 @@ class FraudPipeline:
                 trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
                                                     windows_days=self.windows_days, stream=side)
             mk("terminal_windows", side)
-        for t in (ts_ns, terminal, fraud):
+        for t in (ts_ns, customer, terminal, fraud):
             t.record_stream(side)  # inputs in use on the side stream
-        # customer half (caller's stream): the re-key carries ts and amount into grouped order
-        scan = self.avg_mode == "scan"
-        walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
-        cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
-        mk("rekey_customer", main)
         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
                                   self.windows_days if walk else None, grouped=True)
         mk("customer_layout", main)

@@ -1,0 +1,43 @@
+"""A/B probe for the customer-window walk: config-2 rows (50k customers, 183 days) -> payload
+re-key -> interleaved layout with window starts -> fdx_customer_windows_walk, timed alone
+(--reps); prints the time and a bit-level digest of the NB / SUM planes so that builds of
+libfdx.so with different walk shapes (tools/build_ab.sh, tools/with_lib.py) can be compared.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from fdx import ops, synth
+
+    dev = torch.device("cuda", 0)
+    g = synth.generate_device(50_000, 100_000, 183, seed=1234, device=dev)
+    perm, seg, gts, gamt = ops.rekey_payload(g["customer"], 50_000, g["ts"], g["amount"])
+    lay = ops.customer_layout(seg, perm, gts, gamt, 3, windows_days=(1, 7, 30), grouped=True)
+    nb, sm = ops.customer_windows_walk(lay, seg)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(args.reps):
+        ops.customer_windows_walk(lay, seg)
+    b.record()
+    torch.cuda.synchronize()
+    real = (lay.irow >= 0)[: lay.n_slots]
+    dig = {"nb": int((nb[:, real].to(torch.int64) * torch.arange(1, real.sum().item() + 1, device=dev)).sum().item()),
+           "sum_bits": int((sm[:, real].view(torch.int64) % 1_000_003).sum().item())}
+    print(json.dumps({"lib": os.path.basename(__import__("fdx")._lib.LIB_PATH), "walk_ms": round(a.elapsed_time(b) / args.reps, 4),
+                      "n_slots": lay.n_slots, "digest": dig}))
+
+
+if __name__ == "__main__":
+    main()
