@@ -96,6 +96,20 @@ int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_seg, const in
                                int32_t n_windows, int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d,
                                double *iamt_d, int32_t *irow_d, int32_t *starts_d, int64_t max_slots,
                                int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes, void *stream);
+/* The layout in two halves, for callers that overlap them with the re-key:
+ * plan -- from the segment offsets alone: sorder_d, goff_d and *n_slots_h (synchronises the
+ * stream: the slot count is read back); fill -- fdx_customer_layout_starts_grouped's slots and
+ * window starts for that plan (its_d / iamt_d / irow_d of n_slots entries, starts_d of
+ * n_windows * n_slots).  fdx_customer_layout* = plan + fill. */
+int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows, int32_t *sorder_d,
+                             uint32_t *goff_d, int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes,
+                             void *stream);
+int fdx_customer_layout_fill_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                            const int64_t *gts_d, const double *gamount_d, const int64_t *window_ns,
+                                            int32_t n_windows, const int32_t *sorder_d, const uint32_t *goff_d,
+                                            int64_t n_slots, int64_t *its_d, double *iamt_d, int32_t *irow_d,
+                                            int32_t *starts_d, void *stream);
+
 /* fdx_customer_layout_starts over GROUPED ts / amount (fdx_rekey_payload outputs: row j of
  * the grouping is gts_d[j], gamount_d[j]) -- the layout then reads every segment as a
  * sequential stream instead of gathering through cperm_d (which still gives irow_d). */
@@ -248,6 +262,15 @@ int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *wor
 int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream);
 
 /* Device-wide exclusive prefix sum of m uint32 values, in place. */
+/* seg_off_d[0..n_keys] of the stable grouping by key -- equal to fdx_rekey's seg_off when every
+ * key lies in [0, n_keys) -- from a key histogram, without sorting (the group sizes of
+ * groupby('CUSTOMER_ID'), feature_transformation.ipynb:1092; the customer layout's plan needs
+ * only these, so it can run while the rows are being re-keyed).  bad_d (optional, int32):
+ * the number of keys outside [0, n_keys). */
+size_t fdx_key_segments_workspace_size(int64_t n_keys);
+int fdx_key_segments(const int32_t *keys_d, int64_t n, int64_t n_keys, int64_t *seg_off_d, int32_t *bad_d,
+                     void *workspace_d, size_t workspace_bytes, void *stream);
+
 size_t fdx_exclusive_scan_u32_workspace_size(int64_t m);
 int fdx_exclusive_scan_u32(uint32_t *data_d, int64_t m, void *workspace_d, void *stream);
 

@@ -378,6 +378,28 @@ int seg_offsets(const uint32_t *sk, int64_t n, int64_t n_keys, int64_t *seg_off,
     return FDX_OK;
 }
 
+// Key histogram -> the segment offsets of the stable grouping by key (= fdx_rekey's seg_off for
+// keys in [0, n_keys)), without sorting: what the customer layout's plan needs, so that it can
+// run while the rows are being re-keyed.  Keys outside the range are counted in *bad.
+__global__ void k_key_hist(const int32_t *__restrict__ keys, int64_t n, int64_t n_keys, uint32_t *__restrict__ cnt,
+                           int32_t *__restrict__ bad) {
+    int nbad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k = keys[i];
+        if (k >= 0 && (int64_t)k < n_keys) atomicAdd(&cnt[k], 1u);
+        else ++nbad;
+    }
+    if (bad) {
+        for (int d = kWave / 2; d > 0; d >>= 1) nbad += __shfl_down(nbad, d, kWave);
+        if ((threadIdx.x & (kWave - 1)) == 0 && nbad) atomicAdd(bad, nbad);
+    }
+}
+
+__global__ void k_widen_u32(const uint32_t *__restrict__ in, int64_t m, int64_t *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
 template <typename T>
 __global__ void k_gather(const T *__restrict__ src, const int32_t *__restrict__ perm, int64_t n,
                          T *__restrict__ dst) {
@@ -803,4 +825,31 @@ extern "C" int fdx_exclusive_scan_u32(uint32_t *data_d, int64_t m, void *workspa
     if (m == 0) return FDX_OK;
     FDX_REQUIRE(data_d && workspace_d, "null pointer");
     return exclusive_scan(data_d, m, reinterpret_cast<uint32_t *>(workspace_d), as_stream(stream));
+}
+
+extern "C" size_t fdx_key_segments_workspace_size(int64_t n_keys) {
+    if (n_keys < 0) n_keys = 0;
+    return align_up(sizeof(uint32_t) * (size_t)(n_keys + 1)) + fdx_exclusive_scan_u32_workspace_size(n_keys + 1);
+}
+
+extern "C" int fdx_key_segments(const int32_t *keys_d, int64_t n, int64_t n_keys, int64_t *seg_off_d, int32_t *bad_d,
+                                void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(n_keys >= 1 && n_keys < (int64_t)INT32_MAX, "n_keys out of range");
+    FDX_REQUIRE(seg_off_d && workspace_d && (n == 0 || keys_d), "null pointer");
+    FDX_REQUIRE(workspace_bytes >= fdx_key_segments_workspace_size(n_keys), "workspace too small");
+    hipStream_t st = as_stream(stream);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(workspace_d);
+    void *sws = reinterpret_cast<char *>(workspace_d) + align_up(sizeof(uint32_t) * (size_t)(n_keys + 1));
+    FDX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (size_t)(n_keys + 1), st));
+    if (bad_d) FDX_HIP(hipMemsetAsync(bad_d, 0, sizeof(int32_t), st));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_key_hist, dim3(stream_grid(n, 256)), dim3(256), 0, st, keys_d, n, n_keys, cnt, bad_d);
+        FDX_LAUNCHED("k_key_hist");
+    }
+    int rc = fdx_exclusive_scan_u32(cnt, n_keys + 1, sws, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_widen_u32, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, cnt, n_keys + 1, seg_off_d);
+    FDX_LAUNCHED("k_widen_u32");
+    return FDX_OK;
 }

@@ -1327,15 +1327,15 @@ extern "C" size_t fdx_customer_layout_workspace_size(int64_t n_seg) {
            fdx_exclusive_scan_u32_workspace_size(n_seg + 1) + 256;
 }
 
-static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
-                           const int64_t *ts_d, const double *amount_d, int32_t n_windows,
-                           int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
-                           int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
-                           size_t ws_bytes, void *stream, const WinArgs *wa, int32_t *starts_d, bool grouped = false) {
+// The layout in two halves.  Plan (segment lengths only, so it can run while the rows are
+// still being re-keyed): segments sorted by decreasing length, the slot offset of every group
+// and the slot count (read back: the one host synchronisation of the layout).  Fill: the slots
+// (and the window starts) from the grouped rows.
+extern "C" int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows, int32_t *sorder_d,
+                                        uint32_t *goff_d, int64_t *n_slots_h, void *ws, size_t ws_bytes,
+                                        void *stream) {
     FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64, "bad argument");
-    FDX_REQUIRE(seg_off_d && cperm_d && ts_d && amount_d && sorder_d && goff_d && its_d && iamt_d && irow_d &&
-                    n_slots_h && ws,
-                "null pointer");
+    FDX_REQUIRE(seg_off_d && sorder_d && goff_d && n_slots_h && ws, "null pointer");
     FDX_REQUIRE(ws_bytes >= fdx_customer_layout_workspace_size(n_seg), "workspace too small");
     hipStream_t st = as_stream(stream);
     const int32_t S = kWave / n_windows;
@@ -1344,12 +1344,10 @@ static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_
     char *w = reinterpret_cast<char *>(ws);
     int32_t *keys = reinterpret_cast<int32_t *>(w);
     w += al256((size_t)n_seg * 4);
-    int64_t *kseg = reinterpret_cast<int64_t *>(w);  // seg offsets of the length sort (unused)
-    w += al256((size_t)(lmax + 2) * 8);
+    w += al256((size_t)(lmax + 2) * 8);  // (reserved)
     hipLaunchKernelGGL(k_seg_len_keys, dim3(stream_grid(n_seg, 256)), dim3(256), 0, st, seg_off_d, n_seg, lmax, keys);
     FDX_LAUNCHED("k_seg_len_keys");
     const size_t rws = fdx_rekey_workspace_size(n_seg, 16);
-    (void)kseg;
     int rc = fdx_rekey(keys, n_seg, 16, lmax + 1, sorder_d, nullptr, nullptr, w, rws, stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_group_slots, dim3(stream_grid(n_groups, 256)), dim3(256), 0, st, seg_off_d, sorder_d,
@@ -1363,28 +1361,68 @@ static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_
     FDX_HIP(hipMemcpyAsync(&total, goff_d + n_groups, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     FDX_HIP(hipStreamSynchronize(st));
     *n_slots_h = total;
-    if ((int64_t)total > max_slots) {
-        set_error("interleaved layout needs %u slots > max_slots %lld", total, (long long)max_slots);
-        return FDX_E_WORKSPACE;
-    }
+    return FDX_OK;
+}
+
+static int customer_layout_fill(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d, const int64_t *ts_d,
+                                const double *amount_d, int32_t n_windows, const int32_t *sorder_d,
+                                const uint32_t *goff_d, int64_t n_slots, int64_t *its_d, double *iamt_d,
+                                int32_t *irow_d, hipStream_t st, const WinArgs *wa, int32_t *starts_d, bool grouped) {
+    FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64 && n_slots >= 0, "bad argument");
+    FDX_REQUIRE(seg_off_d && cperm_d && ts_d && amount_d && sorder_d && goff_d && its_d && iamt_d && irow_d,
+                "null pointer");
+    const int32_t S = kWave / n_windows;
+    const int64_t n_groups = ceil_div(n_seg, S);
     if (!starts_d && grouped)
         hipLaunchKernelGGL((k_interleave<false, true>), dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d,
                            sorder_d, cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, WinArgs{},
-                           n_windows, (int32_t *)nullptr, (int64_t)total);
+                           n_windows, (int32_t *)nullptr, n_slots);
     else if (starts_d && grouped)
         hipLaunchKernelGGL((k_interleave<true, true>), dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
                            cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
-                           (int64_t)total);
+                           n_slots);
     else if (starts_d)
         hipLaunchKernelGGL(k_interleave<true>, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
                            cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, *wa, n_windows, starts_d,
-                           (int64_t)total);
+                           n_slots);
     else
         hipLaunchKernelGGL(k_interleave<false>, dim3((unsigned)n_groups), dim3(256), 0, st, seg_off_d, sorder_d,
                            cperm_d, goff_d, n_seg, S, ts_d, amount_d, its_d, iamt_d, irow_d, WinArgs{}, n_windows,
-                           (int32_t *)nullptr, (int64_t)total);
+                           (int32_t *)nullptr, n_slots);
     FDX_LAUNCHED("k_interleave");
     return FDX_OK;
+}
+
+extern "C" int fdx_customer_layout_fill_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                                                       const int64_t *gts_d, const double *gamount_d,
+                                                       const int64_t *window_ns, int32_t n_windows,
+                                                       const int32_t *sorder_d, const uint32_t *goff_d,
+                                                       int64_t n_slots, int64_t *its_d, double *iamt_d,
+                                                       int32_t *irow_d, int32_t *starts_d, void *stream) {
+    WinArgs wa;
+    int rc = check_windows(window_ns, n_windows, &wa);
+    if (rc) return rc;
+    FDX_REQUIRE(starts_d, "null pointer");
+    return customer_layout_fill(seg_off_d, n_seg, cperm_d, gts_d, gamount_d, n_windows, sorder_d, goff_d, n_slots,
+                                its_d, iamt_d, irow_d, as_stream(stream), &wa, starts_d, true);
+}
+
+// plan + fill in one call (the slot count must fit max_slots: FDX_E_WORKSPACE with *n_slots_h
+// set otherwise)
+static int customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
+                           const int64_t *ts_d, const double *amount_d, int32_t n_windows,
+                           int32_t *sorder_d, uint32_t *goff_d, int64_t *its_d, double *iamt_d,
+                           int32_t *irow_d, int64_t max_slots, int64_t *n_slots_h, void *ws,
+                           size_t ws_bytes, void *stream, const WinArgs *wa, int32_t *starts_d, bool grouped = false) {
+    FDX_REQUIRE(cperm_d && ts_d && amount_d && its_d && iamt_d && irow_d, "null pointer");
+    int rc = fdx_customer_layout_plan(seg_off_d, n_seg, n_windows, sorder_d, goff_d, n_slots_h, ws, ws_bytes, stream);
+    if (rc) return rc;
+    if (*n_slots_h > max_slots) {
+        set_error("interleaved layout needs %lld slots > max_slots %lld", (long long)*n_slots_h, (long long)max_slots);
+        return FDX_E_WORKSPACE;
+    }
+    return customer_layout_fill(seg_off_d, n_seg, cperm_d, ts_d, amount_d, n_windows, sorder_d, goff_d, *n_slots_h,
+                                its_d, iamt_d, irow_d, as_stream(stream), wa, starts_d, grouped);
 }
 
 extern "C" int fdx_customer_layout(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,

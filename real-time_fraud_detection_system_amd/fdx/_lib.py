@@ -68,6 +68,11 @@ SIGNATURES = {
     "fdx_customer_windows_interleaved": (ctypes.c_int, [P, P, P, P, P, c_i64, c_i64, P, c_i32, P, P, P]),
     "fdx_exclusive_scan_u32_workspace_size": (c_sz, [c_i64]),
     "fdx_exclusive_scan_u32": (ctypes.c_int, [P, c_i64, P, P]),
+    "fdx_key_segments_workspace_size": (c_sz, [c_i64]),
+    "fdx_key_segments": (ctypes.c_int, [P, c_i64, c_i64, P, P, P, c_sz, P]),
+    "fdx_customer_layout_plan": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, c_sz, P]),
+    "fdx_customer_layout_fill_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, c_i64, P, P, P, P,
+                                                                P]),
     "fdx_segment_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
     "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
     "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),

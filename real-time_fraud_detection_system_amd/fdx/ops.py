@@ -81,10 +81,11 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
 
 
 def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
-                  flag: torch.Tensor | None = None, stream=None):
+                  flag: torch.Tensor | None = None, stream=None, seg_off: bool = True):
     """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
     grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
-    -> (perm int32, seg_off int64[n_keys+1], pay0 grouped | None, pay1 grouped | None)."""
+    -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False), pay0 grouped | None,
+    pay1 grouped | None)."""
     _dev(keys, torch.int32, "keys")
     n = keys.numel()
     dev = keys.device
@@ -98,7 +99,7 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
         _dev(flag, torch.uint8, "flag")
     kb = max(key_bits_for(n_keys), 1)
     perm = torch.empty(n, dtype=torch.int32, device=dev)
-    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev) if seg_off else None
     o0 = torch.empty_like(pay0) if pay0 is not None else None
     o1 = torch.empty_like(pay1) if pay1 is not None else None
     L = _lib.load()
@@ -319,6 +320,63 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
         check(rc, "fdx_customer_layout")
         return CustomerLayout(sorder, goff, its, iamt, irow, ns.value, starts,
                               None if windows_days is None else tuple(windows_days))
+
+
+def key_segments(keys, n_keys: int, stream=None, bad: torch.Tensor | None = None) -> torch.Tensor:
+    """seg_off int64 [n_keys + 1] of the stable grouping by key (rekey's seg_off for keys in
+    [0, n_keys)) from a key histogram, no sort; bad (int32 [1], optional): out-of-range count."""
+    _dev(keys, torch.int32, "keys")
+    L = _lib.load()
+    dev = keys.device
+    seg = torch.empty(int(n_keys) + 1, dtype=torch.int64, device=dev)
+    ws = workspace(L.fdx_key_segments_workspace_size(int(n_keys)), dev)
+    check(L.fdx_key_segments(_ptr(keys), keys.numel(), int(n_keys), _ptr(seg), _ptr(bad) if bad is not None else None,
+                             _ptr(ws), ws.numel(), _s(stream)), "fdx_key_segments")
+    return seg
+
+
+class LayoutPlan:
+    """fdx_customer_layout_plan's outputs: segment order, group slot offsets, slot count."""
+
+    def __init__(self, sorder, goff, n_slots, n_windows):
+        self.sorder, self.goff, self.n_slots, self.n_windows = sorder, goff, n_slots, n_windows
+
+
+def customer_layout_plan(seg_off, n_windows: int, stream=None) -> LayoutPlan:
+    """The first half of customer_layout, from the segment offsets alone (host-synchronising:
+    the slot count is read back)."""
+    _dev(seg_off, torch.int64, "seg_off")
+    n_seg = seg_off.numel() - 1
+    S = 64 // int(n_windows)
+    dev = seg_off.device
+    L = _lib.load()
+    sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
+    goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
+    ws = workspace(L.fdx_customer_layout_workspace_size(n_seg), dev)
+    ns = ctypes.c_int64(0)
+    check(L.fdx_customer_layout_plan(_ptr(seg_off), n_seg, int(n_windows), _ptr(sorder), _ptr(goff), ctypes.byref(ns),
+                                     _ptr(ws), ws.numel(), _s(stream)), "fdx_customer_layout_plan")
+    return LayoutPlan(sorder, goff, ns.value, int(n_windows))
+
+
+def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_days, stream=None) -> CustomerLayout:
+    """The second half: slots and window starts of a plan from GROUPED ts / amount."""
+    _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
+    _dev(gts, torch.int64, "ts_ns"); _dev(gamt, torch.float64, "amount")
+    W = plan.n_windows
+    if len(windows_days) != W:
+        raise FdxError("windows_days must have n_windows entries")
+    dev, m = gts.device, plan.n_slots
+    its = torch.empty(m, dtype=torch.int64, device=dev)
+    iamt = torch.empty(m, dtype=torch.float64, device=dev)
+    irow = torch.empty(m, dtype=torch.int32, device=dev)
+    starts = torch.empty(W * m, dtype=torch.int32, device=dev)
+    if m:
+        check(_lib.load().fdx_customer_layout_fill_starts_grouped(
+            _ptr(seg_off), seg_off.numel() - 1, _ptr(cperm), _ptr(gts), _ptr(gamt), _win_ns(windows_days), W,
+            _ptr(plan.sorder), _ptr(plan.goff), m, _ptr(its), _ptr(iamt), _ptr(irow), _ptr(starts), _s(stream)),
+            "fdx_customer_layout_fill_starts_grouped")
+    return CustomerLayout(plan.sorder, plan.goff, its, iamt, irow, m, starts, tuple(windows_days))
 
 
 def customer_windows_walk(lay: CustomerLayout, seg_off, stream=None):

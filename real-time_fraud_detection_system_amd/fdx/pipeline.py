@@ -155,7 +155,7 @@ class FraudPipeline:
         # Allocated under the side stream's context, so that the caching allocator hands
         # these buffers to nothing on the main stream while the side stream still uses them.
         # The id range checks run here too (off the critical path; out-of-range ids cannot
-        # make the re-keys write out of bounds) and are read at the layout's host sync.
+        # make the re-keys write out of bounds), read once everything is enqueued.
         compact = self.compact_records and W == 3
         with torch.cuda.stream(side):
             mk("start", side)
@@ -176,9 +176,6 @@ class FraudPipeline:
         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
                                   self.windows_days if walk else None, grouped=True)
         mk("customer_layout", main)
-        if validate:
-            for c in rc:
-                c.check()
         self._slots_hint = lay.its.numel()
         self.last_slots = lay.n_slots
         if scan:  # the windows straight from the grouped rows into the layout's slots
@@ -196,6 +193,9 @@ class FraudPipeline:
         mk("assemble_rows", main)
         ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
         mk("forest_traverse", main)
+        if validate:  # read once everything is enqueued (the counts ran early on the side stream)
+            for c in rc:
+                c.check()
         return proba
 
     def _forest_ws(self, n_rows, ws, device):

@@ -51,6 +51,15 @@ def test_rekey_stable(dev, n, n_keys):
     np.testing.assert_array_equal(perm.cpu().numpy(), ref)
     np.testing.assert_array_equal(sk.cpu().numpy(), keys[ref])
     np.testing.assert_array_equal(seg.cpu().numpy(), np.r_[0, np.cumsum(np.bincount(keys, minlength=n_keys))])
+    if n:  # the histogram form (no sort) gives the same offsets; out-of-range keys are counted
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        np.testing.assert_array_equal(ops.key_segments(T(keys, torch.int32, dev), n_keys, bad=bad).cpu().numpy(),
+                                      seg.cpu().numpy())
+        assert int(bad.item()) == 0
+        k2 = keys.copy()
+        k2[::3] = -1 - k2[::3]
+        ops.key_segments(T(k2, torch.int32, dev), n_keys, bad=bad)
+        assert int(bad.item()) == len(k2[::3])
 
 
 def test_argsort_i64_and_perm_ops(dev):
@@ -349,6 +358,34 @@ def test_layout_starts_walk_equals_interleaved(dev):
     valid = (lay.irow[:n] >= 0).cpu().numpy()
     np.testing.assert_array_equal(nb.cpu().numpy()[:, valid], nb_ref.cpu().numpy()[:, valid])
     np.testing.assert_array_equal(sm.cpu().numpy()[:, valid], sm_ref.cpu().numpy()[:, valid])
+
+
+def test_layout_plan_fill_equals_layout(dev):
+    """fdx_customer_layout_plan (from fdx_key_segments' offsets, no sort) + _fill_starts_grouped
+    == fdx_customer_layout_starts_grouped: same segment order, slots, rows and window starts
+    (absent customers and a segment longer than the 1,024-row LDS stage included)."""
+    from fdx import synth
+
+    d = synth.generate(n_customers=400, n_terminals=500, nb_days=120, seed=32)
+    cust = d["customer"].copy()
+    cust[cust < 40] = 0
+    T = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(dev, t)  # noqa: E731
+    ts, c, amt = T(d["ts"], torch.int64), T(cust, torch.int32), T(d["amount"], torch.float64)
+    cperm, cseg, gts, gamt = ops.rekey_payload(c, 400, ts, amt)
+    ref = ops.customer_layout(cseg, cperm, gts, gamt, 3, windows_days=(1, 7, 30), grouped=True)
+    seg2 = ops.key_segments(c, 400)
+    assert torch.equal(seg2, cseg)
+    plan = ops.customer_layout_plan(seg2, 3)
+    lay = ops.customer_layout_fill(plan, seg2, cperm, gts, gamt, (1, 7, 30))
+    m = ref.n_slots
+    assert lay.n_slots == m
+    for a, b in ((lay.sorder, ref.sorder), (lay.goff, ref.goff), (lay.its[:m], ref.its[:m]),
+                 (lay.iamt[:m], ref.iamt[:m]), (lay.irow[:m], ref.irow[:m])):
+        assert torch.equal(a, b)
+    valid = (ref.irow[:m] >= 0)
+    # the window starts (segment-contiguous, padding unwritten) through the walk that reads them
+    for x, y in zip(ops.customer_windows_walk(lay, seg2), ops.customer_windows_walk(ref, cseg)):
+        assert torch.equal(x[:, valid], y[:, valid])
 
 
 def test_fused_scoring_rank_table_overflows(dev):
