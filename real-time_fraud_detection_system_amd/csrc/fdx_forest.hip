@@ -1072,13 +1072,19 @@ __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
 // and its feature reads in forward order, so the first use in each group waits for the
 // group's last-issued read and one s_waitcnt covers the whole group (LDS reads of a wave
 // return in order): fewer issue slots per step.
+// (Mixing the two -- 2 / 3 / 4 of 10 chains on register ranks, the rest on the planes -- was
+// measured too: 11.3 / 13.1 / 14.9 vs 7.6 ms at config 2, profiles/r03o_hybrid_chain_sweep.txt:
+// the walk's time follows its instruction count, whichever pipe the instructions use.)
 template <int P16, int K, int PW>
 __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                                uint32_t (&nd)[K], int depth, const uint32_t (&w)[8]) {
+    auto fetch_x = [&](int k) -> uint32_t {
+        if (P16 == 4) return reg_rank(w, nd[k]);
+        return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+    };
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-        x[k] = P16 == 4 ? reg_rank(w, nd[k]) : rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+    for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
     auto step = [&]() {
 #pragma unroll
         for (int g = 0; g < K; g += PW) {
@@ -1099,12 +1105,8 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            if constexpr (P16 == 4) {
-                x[k] = reg_rank(w, nd[k]);
-            } else {
-                x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            x[k] = fetch_x(k);
+            if (P16 != 4) __builtin_amdgcn_sched_barrier(0);
         }
     };
     int d = 0;
