@@ -1,11 +1,13 @@
-# Build A/B variants of libfdx.so that differ in one compile-time define of fdx_windows.hip:
-#   bash tools/build_ab.sh NAME "-DFDX_WALK_SHAPE=2"   ->  tools/ab/libfdx_NAME.so
-# (the other objects are the in-tree build's; run `make -C real-time_fraud_detection_system_amd/csrc` first)
+# Build an A/B variant of libfdx.so with extra compile-time defines (every source recompiled):
+#   bash tools/build_ab.sh NAME "-DFDX_WALK_LP=2 -DFDX_RADIX_XCD=1"  ->  tools/ab/libfdx_NAME.so
 set -eu
 NAME=$1; DEFS=$2
 C=real-time_fraud_detection_system_amd/csrc
-mkdir -p tools/ab /tmp/fdx_ab
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude $DEFS -c $C/fdx_windows.hip -o /tmp/fdx_ab/windows_$NAME.o
-objs=$(ls $C/build/*.o | grep -v fdx_windows)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/ab/libfdx_$NAME.so $objs /tmp/fdx_ab/windows_$NAME.o
+B=/tmp/fdx_ab/$NAME
+mkdir -p tools/ab $B
+for f in $C/*.hip $C/*.cpp; do
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Iinclude $DEFS -c $f -o $B/$(basename $f).o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/ab/libfdx_$NAME.so $B/*.o
 echo built tools/ab/libfdx_$NAME.so
