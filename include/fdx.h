@@ -104,6 +104,12 @@ int fdx_customer_layout_starts(const int64_t *seg_off_d, int64_t n_seg, const in
 int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows, int32_t *sorder_d,
                              uint32_t *goff_d, int64_t *n_slots_h, void *workspace_d, size_t workspace_bytes,
                              void *stream);
+/* fdx_customer_layout_plan without the host synchronisation, for <= 65,536 segments (else
+ * FDX_E_UNSUPPORTED): plan_h (caller-owned pinned host int32[2]) receives [slot count, status]
+ * once the stream reaches them; status 1 = plan again with fdx_customer_layout_plan. */
+int fdx_customer_layout_plan_async(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows, int32_t *sorder_d,
+                                   uint32_t *goff_d, int32_t *plan_h, void *workspace_d, size_t workspace_bytes,
+                                   void *stream);
 int fdx_customer_layout_fill_starts_grouped(const int64_t *seg_off_d, int64_t n_seg, const int32_t *cperm_d,
                                             const int64_t *gts_d, const double *gamount_d, const int64_t *window_ns,
                                             int32_t n_windows, const int32_t *sorder_d, const uint32_t *goff_d,

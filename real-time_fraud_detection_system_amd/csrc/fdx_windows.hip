@@ -186,6 +186,167 @@ __global__ void k_group_slots(const int64_t *__restrict__ seg_off, const int32_t
     }
 }
 
+// The layout plan in ONE launch for up to kPlanMaxSeg segments (the radix plan is ~17 small
+// launches, each shorter than its launch: ~0.3 ms of a step went to the host launching them).
+// One block of 16 waves; wave w owns the segments [w*per, (w+1)*per) in index order, 64 per
+// chunk, at most kPlanChunks chunks, and keeps their bins in registers.  The order is exactly the
+// radix plan's -- decreasing length (clamped at 65535), ties by index:
+//   * segments of >= kPlanBins-1 rows ("long", rare): collected in LDS and ranked exactly;
+//   * the others: counting sort on bin = kPlanBins-1-length -- wave-private LDS counters, a
+//     bin-major / wave-minor prefix, then each wave places its chunks in order: the lanes of
+//     one bin find each other by ballot multisplit over the 11 bin bits, read the bin's counter,
+//     and the lowest of them advances it;
+// then the group slot counts (S x the group's first = longest segment) and their exclusive scan
+// into goff[0..n_groups].  *status = 1: more long segments than kPlanMaxLong (the host then
+// plans with the radix path).
+constexpr int kPlanWaves = 16, kPlanChunks = 64, kPlanBins = 2048, kPlanBinBits = 11, kPlanMaxLong = 512;
+constexpr int64_t kPlanMaxSeg = (int64_t)kPlanWaves * kPlanChunks * kWave;  // 65,536
+constexpr int64_t kPlanMaxGroups = 3200;                                       // (>= 65,536 / 21)
+__global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const int64_t *__restrict__ seg_off,
+                                                                          int64_t n_seg, int32_t S, int64_t n_groups,
+                                                                          int32_t *__restrict__ sorder,
+                                                                          uint32_t *__restrict__ goff,
+                                                                          int32_t *__restrict__ status) {
+    __shared__ uint32_t s_h[kPlanWaves][kPlanBins];
+    __shared__ int32_t s_long[kPlanMaxLong];
+    __shared__ int32_t s_nlong;
+    __shared__ uint32_t s_part[kPlanWaves * kWave];
+    __shared__ uint32_t s_gs[kPlanMaxGroups];  // group slot counts
+    constexpr int kT = kPlanWaves * kWave;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    for (int e = tid; e < kPlanWaves * kPlanBins; e += kT) (&s_h[0][0])[e] = 0;
+    if (tid == 0) s_nlong = 0;
+    __syncthreads();
+    const int64_t per = (n_seg + kPlanWaves - 1) / kPlanWaves;
+    const int64_t lo = wv * per, hi = min<int64_t>(n_seg, lo + per);
+    auto len_of = [&](int64_t sg) -> int64_t { return seg_off[sg + 1] - seg_off[sg]; };
+    // 1. bins of this wave's chunks (kept in registers, two u16 per VGPR: 0xFFFF = none, 0 =
+    // long), wave-private counts
+    uint32_t binp[kPlanChunks / 2] = {};
+    auto bin_at = [&](int c) -> int32_t {
+        const int32_t v = (int32_t)((binp[c >> 1] >> (16 * (c & 1))) & 0xFFFFu);
+        return v == 0xFFFF ? -1 : v;
+    };
+    constexpr int kBatch = 8;  // chunks whose offsets are loaded together (one load per segment:
+                                // the next offset comes from the next lane, lane 63 loads it)
+#pragma unroll
+    for (int c0 = 0; c0 < kPlanChunks; c0 += kBatch) {
+        int64_t a[kBatch], e63[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+            const int64_t sg = min<int64_t>(lo + (int64_t)(c0 + j) * kWave + lane, n_seg);
+            a[j] = seg_off[sg];
+            e63[j] = lane == kWave - 1 ? seg_off[min<int64_t>(sg + 1, n_seg)] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+            const int64_t sg = lo + (int64_t)(c0 + j) * kWave + lane;
+            const int64_t nx = __shfl_down(a[j], 1, kWave);
+            const int64_t L = (lane == kWave - 1 ? e63[j] : nx) - a[j];
+            const int32_t bn = sg >= hi ? 0xFFFF : (L >= kPlanBins - 1 ? 0 : (int32_t)(kPlanBins - 1 - L));
+            binp[(c0 + j) >> 1] |= (uint32_t)bn << (16 * ((c0 + j) & 1));
+            if (sg < hi) {
+                if (bn == 0) {
+                    const int at = atomicAdd(&s_nlong, 1);
+                    if (at < kPlanMaxLong) s_long[at] = (int32_t)sg;
+                } else {
+                    atomicAdd(&s_h[wv][bn], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int n_long = s_nlong;
+    if (n_long > kPlanMaxLong) {  // uniform: the host falls back to the radix plan
+        if (tid == 0) *status = 1;
+        return;
+    }
+    // 2. exclusive prefix over (bin, wave) entries e = bin * 16 + wave, after the long segments
+    constexpr int kE = kPlanWaves * kPlanBins, kPerT = kE / kT;
+    uint32_t loc[kPerT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPerT; ++j) {
+        const int e = tid * kPerT + j;
+        loc[j] = s_h[e % kPlanWaves][e / kPlanWaves];
+        sum += loc[j];
+    }
+    s_part[tid] = sum;
+    __syncthreads();
+    for (int d = 1; d < kT; d <<= 1) {  // inclusive scan of the per-thread sums
+        const uint32_t v = tid >= d ? s_part[tid - d] : 0u;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_part[tid] - sum + (uint32_t)n_long;
+#pragma unroll
+    for (int j = 0; j < kPerT; ++j) {
+        const int e = tid * kPerT + j;
+        s_h[e % kPlanWaves][e / kPlanWaves] = run;
+        run += loc[j];
+    }
+    __syncthreads();
+    // long segments: exact rank by (length desc, index asc), lengths clamped as the radix key
+    for (int i = tid; i < n_long; i += kT) {
+        const int32_t si = s_long[i];
+        const int64_t li = min<int64_t>(len_of(si), 65535);
+        int r = 0;
+        for (int j = 0; j < n_long; ++j) {
+            const int32_t sj = s_long[j];
+            const int64_t lj = min<int64_t>(len_of(sj), 65535);
+            r += (lj > li) || (lj == li && sj < si);
+        }
+        sorder[r] = si;
+        if (r % S == 0) s_gs[r / S] = (uint32_t)(S * len_of(si));
+    }
+    // 3. each wave places its chunks in index order
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int c = 0; c < kPlanChunks; ++c) {
+        const int32_t bn = bin_at(c);
+        const bool valid = bn > 0;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < kPlanBinBits; ++bit) {
+            const bool set = (bn >> bit) & 1;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        // the counter's read (every lane of the bin) precedes the leader's update in the wave's
+        // LDS instruction order, which the hardware keeps; no fence (a wavefront-scope fence
+        // also waits for the global store below -- one HBM round trip per chunk)
+        const uint32_t cnt = valid ? s_h[wv][bn] : 0u;
+        if (valid) {
+            const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+            if (below == 0) s_h[wv][bn] = cnt + (uint32_t)__popcll(peers);
+            const uint32_t pos = cnt + below;
+            sorder[pos] = (int32_t)(lo + (int64_t)c * kWave + lane);
+            if (pos % S == 0) s_gs[pos / S] = (uint32_t)(S * (kPlanBins - 1 - bn));  // a group's first
+        }
+    }
+    __syncthreads();
+    // 4. exclusive scan of the group slot counts (goff[n_groups] = total)
+    const int64_t gper = (n_groups + kT - 1) / kT;
+    const int64_t g0 = tid * gper, g1 = min<int64_t>(n_groups, g0 + gper);
+    uint32_t gs = 0;
+    for (int64_t g = g0; g < g1; ++g) gs += s_gs[g];
+    s_part[tid] = gs;
+    __syncthreads();
+    for (int d = 1; d < kT; d <<= 1) {
+        const uint32_t v = tid >= d ? s_part[tid - d] : 0u;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t gr = s_part[tid] - gs;
+    for (int64_t g = g0; g < g1; ++g) {
+        goff[g] = gr;
+        gr += s_gs[g];
+    }
+    if (tid == kT - 1) goff[n_groups] = s_part[kT - 1];
+    if (tid == 0) *status = 0;
+}
+
 // one block per group: slot (t, l) <- time-order row r = cperm[seg_off[s] + t]
 // STARTS: the block then also computes every row's window starts (pandas' variable-window
 // start, see k_customer_starts) -- one wave per segment, the segment's timestamps read back
@@ -855,6 +1016,41 @@ constexpr int kMaxRuns = 64;
 #endif
 constexpr bool kRecPair = FDX_REC_PAIR != 0;
 
+// One row's window counts out: the compact W = 3 record (+ the full record in the overflow
+// area), the 24-byte record as two stores (8 + 16 or 16 + 8 bytes by its 16-byte alignment:
+// fewer random write transactions than three), or the general forms of term_store.
+__device__ __forceinline__ void term_emit(int32_t *nb_out, double *risk_out, int64_t *rec_out, int64_t n,
+                                          int32_t n_win, int64_t compact_n, int64_t q, int64_t row,
+                                          const int32_t (&cn)[FDX_MAX_WINDOWS], const int32_t (&cf)[FDX_MAX_WINDOWS]) {
+    if (compact_n > 0) {
+        const bool fits = cn[0] <= kCompactMax && cn[1] <= kCompactMax && cn[2] <= kCompactMax;
+        int64_t lo, hi;
+        if (fits) {
+            lo = (int64_t)cn[0] | ((int64_t)cn[1] << kCompactBits) | ((int64_t)cn[2] << (2 * kCompactBits));
+            hi = (int64_t)cf[0] | ((int64_t)cf[1] << kCompactBits) | ((int64_t)cf[2] << (2 * kCompactBits));
+        } else {
+            const int64_t off = 2 * compact_n + 3 * row;
+#pragma unroll
+            for (int w = 0; w < 3; ++w) rec_out[off + w] = term_word(cn[w], cf[w]);
+            lo = off | INT64_MIN;
+            hi = 0;
+        }
+        *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
+    } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
+        int64_t *dst = rec_out + row * 3;
+        const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
+        if ((row & 1) == 0) {
+            *reinterpret_cast<longlong2 *>(dst) = make_longlong2(w0, w1);
+            dst[2] = w2;
+        } else {
+            dst[0] = w0;
+            *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(w1, w2);
+        }
+    } else {
+        for (int w = 0; w < n_win; ++w) term_store(nb_out, risk_out, rec_out, n, n_win, q, row, w, cn[w], cf[w]);
+    }
+}
+
 // Terminal windows over GROUPED inputs (fdx_rekey_payload carried ts -- and the fraud bit in
 // bit 31 of the perm -- through the re-key): every read is sequential within a segment.
 //   gts[q]    ts of grouped position q; segments time-sorted, or (RUNS) concatenations of
@@ -1080,36 +1276,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
                         cf[w] = frh - frl[w];
                     }
                 }
-                if (compact_n > 0) {  // W = 3 compact record (+ the full record in the overflow area)
-                    const bool fits = cn[0] <= kCompactMax && cn[1] <= kCompactMax && cn[2] <= kCompactMax;
-                    int64_t lo, hi;
-                    if (fits) {
-                        lo = (int64_t)cn[0] | ((int64_t)cn[1] << kCompactBits) | ((int64_t)cn[2] << (2 * kCompactBits));
-                        hi = (int64_t)cf[0] | ((int64_t)cf[1] << kCompactBits) | ((int64_t)cf[2] << (2 * kCompactBits));
-                    } else {
-                        const int64_t off = 2 * compact_n + 3 * row;
-    #pragma unroll
-                        for (int w = 0; w < 3; ++w) rec_out[off + w] = term_word(cn[w], cf[w]);
-                        lo = off | INT64_MIN;
-                        hi = 0;
-                    }
-                    *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
-                } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
-                    // the 24-byte record in two stores (8 + 16 or 16 + 8 bytes by the record's
-                    // 16-byte alignment) instead of three: fewer random write transactions
-                    int64_t *dst = rec_out + row * 3;
-                    const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
-                    if ((row & 1) == 0) {
-                        *reinterpret_cast<longlong2 *>(dst) = make_longlong2(w0, w1);
-                        dst[2] = w2;
-                    } else {
-                        dst[0] = w0;
-                        *reinterpret_cast<longlong2 *>(dst + 1) = make_longlong2(w1, w2);
-                    }
-                } else {
-                    for (int w = 0; w < n_win; ++w)
-                        term_store(nb_out, risk_out, rec_out, n, n_win, b + qi, row, w, cn[w], cf[w]);
-                }
+                term_emit(nb_out, risk_out, rec_out, n, n_win, compact_n, b + qi, row, cn, cf);
             }
         };
         if (in_lds)
@@ -1117,6 +1284,107 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
         else
             rows_loop(T_glb, F_glb);
         wave_sync();
+    }
+}
+
+// The short-segment pass of the single-run case (segments of 1..kTermShortRows rows, 99.95 % of
+// the rows at config 2), software-pipelined across a wave's segments: the next segment's
+// timestamps and rows words are loaded into registers while the current one is searched, and
+// the rows words (destination row | fraud << 31) are staged in LDS beside the timestamps, so
+// neither the staging nor the record stores wait on a global load (the one-segment-at-a-time
+// form spent 73 % of its wave time in s_waitcnt on HBM round trips, r03r PMC).  Same closed
+// form, same outputs as k_terminal_g.
+__global__ void __launch_bounds__(kTermBlock) k_terminal_short(
+    const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
+    const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
+    int32_t *__restrict__ nb_out, double *__restrict__ risk_out, int64_t *__restrict__ rec_out, int64_t compact_n) {
+    constexpr int LR = kTermShortRows, CH = LR / kWave;
+    __shared__ int64_t s_ts[kTermWaves][LR];
+    __shared__ int32_t s_f[kTermWaves][LR + 1];
+    __shared__ int32_t s_r[kTermWaves][LR];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kTermWaves;
+    int64_t *lts = s_ts[wv];
+    int32_t *lf = s_f[wv], *lr = s_r[wv];
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // the wave's next segment of this pass at or after s (wave-uniform scalar loads)
+    auto next_seg = [&](int64_t s, int64_t &b, int64_t &L) -> int64_t {
+        for (; s < n_seg; s += nwaves) {
+            b = seg_off[s];
+            L = seg_off[s + 1] - b;
+            if (L > 0 && L <= LR) return s;
+        }
+        return n_seg;
+    };
+    int64_t pts[CH];
+    int32_t prw[CH];
+    uint32_t pfr[CH];
+    auto load = [&](int64_t b, int64_t L) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int64_t j = min<int64_t>(c * kWave + lane, L - 1);  // clamped: no branch
+            pts[c] = gts[b + j];
+            prw[c] = rows ? rows[b + j] : (int32_t)(b + j);
+            pfr[c] = gfraud ? gfraud[b + j] : 0u;
+        }
+    };
+    int64_t cb = 0, cl = 0;
+    int64_t cur = next_seg((int64_t)blockIdx.x * kTermWaves + wv, cb, cl);
+    if (cur < n_seg) load(cb, cl);
+    while (cur < n_seg) {
+        // stage the current segment from registers: ts, rows words, prefix fraud counts
+        if (lane == 0) lf[0] = 0;
+        int carry = 0;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int64_t j = c * kWave + lane;
+            const bool in = j < cl;
+            const int f = in ? (gfraud ? (pfr[c] != 0) : (int)((uint32_t)prw[c] >> 31)) : 0;
+            if (in) {
+                lts[j] = pts[c];
+                lr[j] = prw[c] & 0x7FFFFFFF;
+            }
+            const int inc = wave_incl_scan(f, lane) + carry;
+            if (in) lf[j + 1] = inc;
+            carry = __shfl(inc, kWave - 1, kWave);
+        }
+        wave_sync();
+        // the next segment's loads, in flight during this one's searches
+        int64_t nb = 0, nl = 0;
+        const int64_t nxt = next_seg(cur + nwaves, nb, nl);
+        if (nxt < n_seg) load(nb, nl);
+        auto ub = [&](int64_t lo, int64_t hi, int64_t x) -> int64_t {  // first j in [lo, hi) with ts_j > x
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (lts[mid] <= x) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        for (int64_t i = lane; i < cl; i += kWave) {
+            const int64_t t = lts[i];
+            const int64_t row = lr[i];
+            int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
+            const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
+            const int32_t frh = lf[hi];
+#pragma unroll
+            for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
+                if (w < n_win) {
+                    const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                    cn[w] = (int32_t)(hi - lo);
+                    cf[w] = frh - lf[lo];
+                }
+            }
+            term_emit(nb_out, risk_out, rec_out, n, n_win, compact_n, cb + i, row, cn, cf);
+        }
+        wave_sync();
+        cur = nxt;
+        cb = nb;
+        cl = nl;
     }
 }
 
@@ -1219,7 +1487,8 @@ static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, c
         FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
     } else {
-        FDX_TERM_LAUNCH(false, kTermShortRows, 0, kTermShortRows);
+        hipLaunchKernelGGL(k_terminal_short, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off, n_seg, n,
+                           delay_ns, wa, n_windows, nb_d, risk_d, rec_d, compact_n);
         FDX_TERM_LAUNCH(false, kTermLdsRows, lo, inf);
     }
 #undef FDX_TERM_LAUNCH
@@ -1344,7 +1613,25 @@ extern "C" int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg,
     char *w = reinterpret_cast<char *>(ws);
     int32_t *keys = reinterpret_cast<int32_t *>(w);
     w += al256((size_t)n_seg * 4);
-    w += al256((size_t)(lmax + 2) * 8);  // (reserved)
+    int32_t *status = reinterpret_cast<int32_t *>(w);  // (in the reserved range)
+    w += al256((size_t)(lmax + 2) * 8);
+    if (n_seg <= kPlanMaxSeg && n_groups <= kPlanMaxGroups) {  // one launch; the radix plan below if it
+                                                               // reports too many long segments
+        struct {
+            uint32_t total;
+            int32_t status;
+        } h{};
+        hipLaunchKernelGGL(k_layout_plan_small, dim3(1), dim3(kPlanWaves * kWave), 0, st, seg_off_d, n_seg, S, n_groups,
+                           sorder_d, goff_d, status);
+        FDX_LAUNCHED("k_layout_plan_small");
+        FDX_HIP(hipMemcpyAsync(&h.status, status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        FDX_HIP(hipMemcpyAsync(&h.total, goff_d + n_groups, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        FDX_HIP(hipStreamSynchronize(st));
+        if (h.status == 0) {
+            *n_slots_h = h.total;
+            return FDX_OK;
+        }
+    }
     hipLaunchKernelGGL(k_seg_len_keys, dim3(stream_grid(n_seg, 256)), dim3(256), 0, st, seg_off_d, n_seg, lmax, keys);
     FDX_LAUNCHED("k_seg_len_keys");
     const size_t rws = fdx_rekey_workspace_size(n_seg, 16);
@@ -1361,6 +1648,33 @@ extern "C" int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg,
     FDX_HIP(hipMemcpyAsync(&total, goff_d + n_groups, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     FDX_HIP(hipStreamSynchronize(st));
     *n_slots_h = total;
+    return FDX_OK;
+}
+
+// The one-launch plan without the host synchronisation: the slot count and the plan's status go
+// to caller-owned pinned host memory (plan_h[0] = slots, plan_h[1] = status: 0 = done, 1 = too
+// many long segments -- plan again with fdx_customer_layout_plan), read once the stream is past
+// this call.  FDX_E_UNSUPPORTED for more than 65,536 segments.
+extern "C" int fdx_customer_layout_plan_async(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows,
+                                              int32_t *sorder_d, uint32_t *goff_d, int32_t *plan_h, void *ws,
+                                              size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(n_seg >= 1 && n_windows >= 1 && n_windows <= 64, "bad argument");
+    FDX_REQUIRE(seg_off_d && sorder_d && goff_d && plan_h && ws, "null pointer");
+    FDX_REQUIRE(ws_bytes >= fdx_customer_layout_workspace_size(n_seg), "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const int32_t S = kWave / n_windows;
+    const int64_t n_groups = ceil_div(n_seg, S);
+    if (n_seg > kPlanMaxSeg || n_groups > kPlanMaxGroups) {
+        set_error("the one-launch plan takes <= %lld segments and <= %lld groups", (long long)kPlanMaxSeg,
+                  (long long)kPlanMaxGroups);
+        return FDX_E_UNSUPPORTED;
+    }
+    int32_t *status = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + al256((size_t)n_seg * 4));
+    hipLaunchKernelGGL(k_layout_plan_small, dim3(1), dim3(kPlanWaves * kWave), 0, st, seg_off_d, n_seg, S, n_groups,
+                       sorder_d, goff_d, status);
+    FDX_LAUNCHED("k_layout_plan_small");
+    FDX_HIP(hipMemcpyAsync(plan_h, goff_d + n_groups, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    FDX_HIP(hipMemcpyAsync(plan_h + 1, status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     return FDX_OK;
 }
 

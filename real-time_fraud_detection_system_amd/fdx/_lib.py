@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfdx.so")
 
 FDX_OK = 0
+FDX_E_UNSUPPORTED = -3
 FDX_FLAGS_NOTEBOOK = 0
 FDX_FLAGS_SPARK = 1
 FDX_KEY_MOD, FDX_KEY_DIV, FDX_KEY_SUB = 0, 1, 2
@@ -71,6 +72,7 @@ SIGNATURES = {
     "fdx_key_segments_workspace_size": (c_sz, [c_i64]),
     "fdx_key_segments": (ctypes.c_int, [P, c_i64, c_i64, P, P, P, c_sz, P]),
     "fdx_customer_layout_plan": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, c_sz, P]),
+    "fdx_customer_layout_plan_async": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, c_sz, P]),
     "fdx_customer_layout_fill_starts_grouped": (ctypes.c_int, [P, c_i64, P, P, P, P, c_i32, P, P, c_i64, P, P, P, P,
                                                                 P]),
     "fdx_segment_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),

@@ -285,6 +285,11 @@ class ShardedPipeline:
         rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
         cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
         mk("rekey_customer", main)
+        scan = p.avg_mode == "scan"
+        walk = W >= 3
+        # the walk's layout plan right behind the re-key (no host wait): it runs while the host
+        # waits for the exchange's split sizes below
+        pending = ops.customer_layout_plan_async(cseg, W) if (walk and not scan) else None
         # the exchange's split-size sync waits only for the (short) owner re-key on the side
         # stream; enqueueing the whole exchange before the layout's host sync keeps the side
         # stream busy while the customer re-key runs
@@ -293,10 +298,11 @@ class ShardedPipeline:
                                               self.n_terminals_total, p.windows_days, p.delay_days, self.group,
                                               mark=lambda name: mk(name, side), stats=stats)
             sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
-        scan = p.avg_mode == "scan"
-        walk = W >= 3
-        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint, p.windows_days if walk else None,
-                                  grouped=True)  # (host sync on main)
+        if pending is not None:
+            lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, p.windows_days)
+        else:
+            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint,
+                                      p.windows_days if walk else None, grouped=True)  # (host sync on main)
         mk("customer_layout", main)
         rc.check()
         p._slots_hint = lay.its.numel()

@@ -359,6 +359,44 @@ def customer_layout_plan(seg_off, n_windows: int, stream=None) -> LayoutPlan:
     return LayoutPlan(sorder, goff, ns.value, int(n_windows))
 
 
+class PendingPlan:
+    """customer_layout_plan_async's handle: result() waits for the stream to pass the plan
+    (no earlier) and returns the LayoutPlan (re-planning synchronously if the one-launch plan
+    declined)."""
+
+    def __init__(self, seg_off, n_windows, stream):
+        self.seg_off, self.n_windows, self.stream = seg_off, int(n_windows), stream
+        n_seg = seg_off.numel() - 1
+        S = 64 // self.n_windows
+        dev = seg_off.device
+        L = _lib.load()
+        self.sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
+        self.goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
+        self.ws = workspace(L.fdx_customer_layout_workspace_size(n_seg), dev)
+        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        st = stream or torch.cuda.current_stream()
+        rc = L.fdx_customer_layout_plan_async(_ptr(seg_off), n_seg, self.n_windows, _ptr(self.sorder), _ptr(self.goff),
+                                              self.host.data_ptr(), _ptr(self.ws), self.ws.numel(), _s(st))
+        self.ok = rc == _lib.FDX_OK
+        if not self.ok and rc != _lib.FDX_E_UNSUPPORTED:
+            check(rc, "fdx_customer_layout_plan_async")
+        self.ev = torch.cuda.Event()
+        self.ev.record(st)
+
+    def result(self) -> LayoutPlan:
+        if self.ok:
+            self.ev.synchronize()
+            if int(self.host[1]) == 0:
+                return LayoutPlan(self.sorder, self.goff, int(self.host[0]) & 0xFFFFFFFF, self.n_windows)
+        return customer_layout_plan(self.seg_off, self.n_windows, self.stream)
+
+
+def customer_layout_plan_async(seg_off, n_windows: int, stream=None) -> PendingPlan:
+    """Enqueue the layout plan without waiting for it (see PendingPlan)."""
+    _dev(seg_off, torch.int64, "seg_off")
+    return PendingPlan(seg_off, n_windows, stream)
+
+
 def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_days, stream=None) -> CustomerLayout:
     """The second half: slots and window starts of a plan from GROUPED ts / amount."""
     _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")

@@ -163,18 +163,21 @@ class FraudPipeline:
             walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
             cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
             mk("rekey_customer", main)
+            # the walk's layout plan goes right behind the re-key; its slot count is read only
+            # after the terminal half is enqueued (no host wait between the two)
+            pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
             # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
             # perm); the records come out in input row order, read by the row assembly through irow.
             # Allocated under the side stream's context, so that the caching allocator hands
             # these buffers to nothing on the main stream while the side stream still uses them.
-            # The id range checks run here too (off the critical path; out-of-range ids cannot
-            # make the re-keys write out of bounds), read once everything is enqueued.
+            # (Out-of-range ids cannot make the re-keys write out of bounds; the range checks run
+            # here and are read once everything is enqueued.)
             compact = self.compact_records and W == 3
             with torch.cuda.stream(side):
                 mk("start", side)
                 tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
                 mk("rekey_terminal", side)
-                if validate:
+                if validate:  # read once everything is enqueued
                     rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", side),
                           ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", side))
                 if compact:
@@ -186,8 +189,11 @@ class FraudPipeline:
                 mk("terminal_windows", side)
             for t in (ts_ns, customer, terminal, fraud):
                 t.record_stream(side)  # inputs in use on the side stream
-            lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
-                                      self.windows_days if walk else None, grouped=True)
+            if pending is not None:
+                lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
+            else:
+                lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
+                                          self.windows_days if walk else None, grouped=True)
             mk("customer_layout", main)
             self._slots_hint = lay.its.numel()
             self.last_slots = lay.n_slots

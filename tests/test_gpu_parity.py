@@ -388,6 +388,40 @@ def test_layout_plan_fill_equals_layout(dev):
         assert torch.equal(x[:, valid], y[:, valid])
 
 
+@pytest.mark.parametrize("case", ["short", "long", "too_many_long", "ragged", "w4"])
+def test_layout_plan_order(dev, case):
+    """fdx_customer_layout_plan's one-launch plan == the radix plan's order: segments by
+    decreasing length (clamped at 65535), ties by index; group slot offsets and count.  Long
+    segments (>= 2047 rows) are ranked exactly; more than 512 of them take the radix path."""
+    rng = np.random.default_rng(7)
+    if case == "short":
+        lens = rng.integers(0, 800, size=50_000)
+    elif case == "long":
+        lens = np.r_[rng.integers(0, 2100, size=20_000), rng.integers(2040, 70_000, size=300), [70_000] * 3]
+        rng.shuffle(lens)
+    elif case == "w4":
+        lens = rng.integers(0, 300, size=60_000)
+    elif case == "too_many_long":
+        lens = np.r_[rng.integers(0, 50, size=3_000), rng.integers(2047, 2200, size=600)]
+        rng.shuffle(lens)
+    else:
+        lens = rng.integers(0, 5, size=65_536)
+    W = 4 if case == "w4" else 3  # 4 windows: 16 segments per group, more groups than the one-launch plan holds
+    seg = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    plan = ops.customer_layout_plan(T(seg, torch.int64, dev), W)
+    exp = np.argsort(65535 - np.minimum(lens, 65535), kind="stable")
+    n = len(lens)
+    np.testing.assert_array_equal(plan.sorder.cpu().numpy()[:n], exp)
+    S = 64 // W
+    gslots = S * lens[exp[::S]]
+    np.testing.assert_array_equal(plan.goff.cpu().numpy()[: len(gslots) + 1].astype(np.int64),
+                                  np.r_[0, np.cumsum(gslots)])
+    assert plan.n_slots == gslots.sum()
+    pa = ops.customer_layout_plan_async(T(seg, torch.int64, dev), W).result()  # incl. its fallback
+    assert pa.n_slots == plan.n_slots and torch.equal(pa.sorder[:n], plan.sorder[:n])
+    assert torch.equal(pa.goff[: len(gslots) + 1], plan.goff[: len(gslots) + 1])
+
+
 def test_fused_scoring_rank_table_overflows(dev):
     """The scoring-row assembly of the fused path (k_zfill_grouped_w3: integer rank table for
     counts < 256, ratio table for terminal windows with NB < 128, searched otherwise) scores
