@@ -432,20 +432,22 @@ __global__ void __launch_bounds__(256) k_interleave(
             // flat load, which takes the vector-memory path even for LDS addresses), windows
             // unrolled (a runtime-indexed prev[] became a chain of v_cndmask per access)
             auto search = [&](auto T) {
+                // (32-bit positions: a segment is < 2^31 rows; 64-bit index arithmetic doubled the
+                // search's dependent instruction chain)
                 int32_t prev[FDX_MAX_WINDOWS] = {};  // this lane's start of row t - 64: a lower bound (starts rise)
-                for (int64_t t = lane; t < L; t += kWave) {
+                for (int32_t t = lane; t < (int32_t)L; t += kWave) {
                     const int64_t tv = T(t);
 #pragma unroll
                     for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
                         if (w < n_win) {
                             const int64_t bound = tv - win.w[w];
-                            int64_t a = prev[w], e = t;  // first k in [prev, t] with ts_k > bound (k = t qualifies)
+                            int32_t a = prev[w], e = t;  // first k in [prev, t] with ts_k > bound (k = t qualifies)
                             while (a < e) {
-                                const int64_t m = (a + e) >> 1;
+                                const int32_t m = (int32_t)((uint32_t)(a + e) >> 1);
                                 if (T(m) > bound) e = m; else a = m + 1;
                             }
-                            prev[w] = (int32_t)a;
-                            starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = (int32_t)a;
+                            prev[w] = a;
+                            starts[(int64_t)w * n_slots + base + (int64_t)ls * Lg + t] = a;
                         }
                     }
                 }
@@ -1358,23 +1360,23 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_short(
         int64_t nb = 0, nl = 0;
         const int64_t nxt = next_seg(cur + nwaves, nb, nl);
         if (nxt < n_seg) load(nb, nl);
-        auto ub = [&](int64_t lo, int64_t hi, int64_t x) -> int64_t {  // first j in [lo, hi) with ts_j > x
+        auto ub = [&](int32_t lo, int32_t hi, int64_t x) -> int32_t {  // first j in [lo, hi) with ts_j > x
             while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
+                const int32_t mid = (int32_t)((uint32_t)(lo + hi) >> 1);
                 if (lts[mid] <= x) lo = mid + 1; else hi = mid;
             }
             return lo;
         };
-        for (int64_t i = lane; i < cl; i += kWave) {
+        for (int32_t i = lane; i < (int32_t)cl; i += kWave) {
             const int64_t t = lts[i];
             const int64_t row = lr[i];
             int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
-            const int64_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
+            const int32_t hi = ub(0, i, t - delay);  // rows strictly older than t - delay < t
             const int32_t frh = lf[hi];
 #pragma unroll
             for (int w = 0; w < FDX_MAX_WINDOWS; ++w) {
                 if (w < n_win) {
-                    const int64_t lo = ub(0, hi, t - delay - win.w[w]);
+                    const int32_t lo = ub(0, hi, t - delay - win.w[w]);
                     cn[w] = (int32_t)(hi - lo);
                     cf[w] = frh - lf[lo];
                 }
