@@ -256,6 +256,15 @@ int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_
                       const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
                       uint64_t *pay0_out_d, uint64_t *pay1_out_d, void *workspace_d, size_t workspace_bytes,
                       void *stream);
+/* fdx_rekey_payload that also counts the keys outside [0, n_keys) into *bad_d (device int32,
+ * zeroed by the call, written on `stream`) inside the first radix pass's histogram -- the id
+ * range check of the reference's groupby without a kernel of its own.  Out-of-range keys never
+ * make the call write out of bounds; the caller raises when *bad_d != 0 (the grouping would be
+ * wrong), as fdx/ops.py:KeyRangeCheck does. */
+int fdx_rekey_payload_checked(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                              const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
+                              int64_t *seg_off_d, uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d,
+                              void *workspace_d, size_t workspace_bytes, void *stream);
 
 /* Stable argsort of int64 keys (e.g. TX_DATETIME ns): perm_d[j] = input row at sorted
  * position j, ties keep input order.  Used when a caller's frame is not in time order

@@ -133,10 +133,13 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
 // item, only the lowest lane of each group of equal digits (ballot multisplit) adds the
 // group's size: no two lanes of an instruction touch one counter, where one block-shared
 // atomicAdd per key spent ~70 % of its LDS cycles on same-address conflicts (r02 PMC).
+// bad != nullptr (first pass of fdx_rekey_payload_checked): also count the keys >= key_limit
+// (as unsigned: negative int32 ids count too) -- the id range check rides on this pass's reads.
 template <typename K, int BITS>
 __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ keys, int64_t n, int shift,
                                                        K flip, int64_t n_tiles,
-                                                       uint32_t *__restrict__ hist) {
+                                                       uint32_t *__restrict__ hist, uint64_t key_limit = 0,
+                                                       int32_t *__restrict__ bad = nullptr) {
     constexpr int kBins = 1 << BITS;
     constexpr int kWaveSpan = kTile / kWavesPerBlock;
     __shared__ uint32_t s_h[kWavesPerBlock][kBins];
@@ -164,6 +167,13 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
             peers &= bit ? bb : ~bb;
         }
         if (valid && (peers & lt_mask) == 0) h[d] += (uint32_t)__popcll(peers);
+    }
+    if (bad) {
+        int nb = 0;
+#pragma unroll
+        for (int r = 0; r < kItems; ++r)
+            nb += __popcll(__ballot(wbase + (int64_t)r * kWave < n && (uint64_t)key[r] >= key_limit));
+        if (lane == 0 && nb) atomicAdd(bad, nb);
     }
     __syncthreads();
     for (int d = tid; d < kBins; d += kBlock) {
@@ -518,7 +528,8 @@ void launch_scatter(const K *kin, const uint32_t *vin, int64_t n, int shift, K f
 template <typename K>
 int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t *vals_out,
                const SortWs<K> &w, hipStream_t st, const K **sorted, int pw = 0, const uint8_t *flag_in = nullptr,
-               const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr) {
+               const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr, uint64_t key_limit = 0,
+               int32_t *bad = nullptr) {
     const int64_t tiles = ceil_div(n, kTile);
     // 9-bit digits when they need fewer passes than 8-bit ones (17- and 18-bit keys: 2, not 3)
     const int dbits = ((bits + 8) / 9 < (bits + kRadixBits - 1) / kRadixBits) ? 9 : kRadixBits;
@@ -546,12 +557,13 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         uint32_t *vout = last ? vals_out : ((p & 1) ? w.v1 : w.v0);
         uint64_t *pout[2] = {nullptr, nullptr};
         for (int q = 0; q < pw; ++q) pout[q] = last ? pay_out[q] : w.q[q][p & 1];
+        int32_t *bad_p = p == 0 ? bad : nullptr;
         if (dbits == 9)
             hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
-                               tiles, w.hist);
+                               tiles, w.hist, key_limit, bad_p);
         else
             hipLaunchKernelGGL((k_radix_hist<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n,
-                               shift, flip, tiles, w.hist);
+                               shift, flip, tiles, w.hist, key_limit, bad_p);
         FDX_LAUNCHED("k_radix_hist");
         int rc = exclusive_scan(w.hist, tiles * ((int64_t)1 << dbits), w.part, st);
         if (rc) return rc;
@@ -622,10 +634,33 @@ extern "C" size_t fdx_rekey_payload_workspace_size(int64_t n, int32_t key_bits, 
     return sort_ws<uint32_t>(n, nullptr, nullptr, n_payload < 0 ? 0 : (n_payload > 2 ? 2 : n_payload));
 }
 
+static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
+                         const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
+                         uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
+                         size_t workspace_bytes, void *stream);
+
 extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
                                  const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
                                  int64_t *seg_off_d, uint64_t *pay0_out_d, uint64_t *pay1_out_d, void *workspace_d,
                                  size_t workspace_bytes, void *stream) {
+    return rekey_payload(keys_d, n, key_bits, n_keys, flag_d, pay0_d, pay1_d, perm_d, seg_off_d, pay0_out_d,
+                         pay1_out_d, nullptr, workspace_d, workspace_bytes, stream);
+}
+
+extern "C" int fdx_rekey_payload_checked(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                                         const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d,
+                                         int32_t *perm_d, int64_t *seg_off_d, uint64_t *pay0_out_d,
+                                         uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
+                                         size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(bad_d, "null bad_d");
+    return rekey_payload(keys_d, n, key_bits, n_keys, flag_d, pay0_d, pay1_d, perm_d, seg_off_d, pay0_out_d,
+                         pay1_out_d, bad_d, workspace_d, workspace_bytes, stream);
+}
+
+static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
+                         const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
+                         uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
+                         size_t workspace_bytes, void *stream) {
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     FDX_REQUIRE(key_bits >= 1 && key_bits <= 31, "key_bits must be in [1, 31]");
     FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
@@ -633,6 +668,7 @@ extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_b
                     (pay1_d == nullptr || pay0_d != nullptr),
                 "payload inputs and outputs go together (stream 1 needs stream 0)");
     hipStream_t st = as_stream(stream);
+    if (bad_d) FDX_HIP(hipMemsetAsync(bad_d, 0, sizeof(int32_t), st));
     if (n == 0) {
         if (seg_off_d) FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
         return FDX_OK;
@@ -649,7 +685,8 @@ extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_b
     uint64_t *pout[2] = {pay0_out_d, pay1_out_d};
     const uint32_t *sorted = nullptr;
     int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, nullptr,
-                                  reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted, pw, flag_d, pin, pout);
+                                  reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted, pw, flag_d, pin, pout,
+                                  (uint64_t)n_keys, bad_d);
     if (rc) return rc;
     if (seg_off_d) return seg_offsets(sorted, n, n_keys, seg_off_d, st);
     return FDX_OK;

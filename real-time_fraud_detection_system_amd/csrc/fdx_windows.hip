@@ -7,6 +7,7 @@
 //   customer  feature_transformation.ipynb:601-628 (pandas rolling('{w}d').sum()/count())
 //   terminal  feature_transformation.ipynb:1495-1522 (rolling(delay) vs rolling(delay+w))
 #include <cstdlib>
+#include <type_traits>
 
 #include "fdx_internal.h"
 
@@ -985,6 +986,12 @@ constexpr int kTermLdsRows = 1024;  // rows of one segment staged per wave (12 K
 // stage (3 KB per wave instead of 12: about twice the resident waves for this latency-bound
 // kernel), the longer ones in a second launch with the full stage (see terminal_launch).
 constexpr int kTermShortRows = 256;
+// A/B switch (compile time): the W = 3 short pass with all searches interleaved
+#ifndef FDX_TERM_SHORT_NW
+#define FDX_TERM_SHORT_NW 1
+#endif
+constexpr bool kTermShortNW = FDX_TERM_SHORT_NW != 0;
+
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
@@ -1296,6 +1303,13 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_g(
 // neither the staging nor the record stores wait on a global load (the one-segment-at-a-time
 // form spent 73 % of its wave time in s_waitcnt on HBM round trips, r03r PMC).  Same closed
 // form, same outputs as k_terminal_g.
+// NW > 0 (compile-time window count; the launch uses 3 for W = 3): every search of the segment
+// runs at once -- a branchless fixed-depth binary search over [0, i) per (row chunk, bound), all
+// (chunks x (NW + 1)) chains interleaved, so that a segment costs one search's LDS latency
+// (8 dependent reads) rather than chunks x (hi search, then the window searches inside [0, hi)).
+// Bounds over [0, i) equal those over [0, hi): ts is sorted and every ts in [hi, i) exceeds
+// t - delay >= each window's bound.  NW = 0: the runtime window count, one row at a time.
+template <int NW>
 __global__ void __launch_bounds__(kTermBlock) k_terminal_short(
     const int64_t *__restrict__ gts, const uint8_t *__restrict__ gfraud, const int32_t *__restrict__ rows,
     const int64_t *__restrict__ seg_off, int64_t n_seg, int64_t n, int64_t delay, WinArgs win, int32_t n_win,
@@ -1360,6 +1374,63 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_short(
         int64_t nb = 0, nl = 0;
         const int64_t nxt = next_seg(cur + nwaves, nb, nl);
         if (nxt < n_seg) load(nb, nl);
+        if constexpr (NW > 0) {
+            const int32_t L32 = (int32_t)cl;
+            auto chunks = [&](auto nc) {
+                constexpr int NC = decltype(nc)::value;
+                int32_t pos[NC][NW + 1];
+                int64_t x[NC][NW + 1];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const int64_t t = lts[c * kWave + lane];  // past the segment: stale, never emitted
+                    x[c][0] = t - delay;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) x[c][w + 1] = t - delay - win.w[w];
+#pragma unroll
+                    for (int k = 0; k <= NW; ++k) pos[c][k] = 0;
+                }
+                // pos = #j < i with ts_j <= x (ts sorted): steps LR/2 .. 1 reach any i < LR
+#pragma unroll
+                for (int step = LR / 2; step >= 1; step >>= 1) {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        const int32_t i = c * kWave + lane;
+#pragma unroll
+                        for (int k = 0; k <= NW; ++k) {
+                            const int32_t q = pos[c][k] + step;
+                            const bool take = (q <= i) & (lts[q - 1] <= x[c][k]);  // q - 1 < LR
+                            pos[c][k] = take ? q : pos[c][k];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const int32_t i = c * kWave + lane;
+                    if (i < L32) {
+                        int32_t cn[FDX_MAX_WINDOWS], cf[FDX_MAX_WINDOWS];
+                        const int32_t hi = pos[c][0], frh = lf[hi];
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) {
+                            cn[w] = hi - pos[c][w + 1];
+                            cf[w] = frh - lf[pos[c][w + 1]];
+                        }
+                        term_emit(nb_out, risk_out, rec_out, n, NW, compact_n, cb + i, lr[i], cn, cf);
+                    }
+                }
+            };
+            static_assert(CH == 4, "the chunk switch below covers 1..4 chunks of 64 rows");
+            switch ((L32 + kWave - 1) / kWave) {
+                case 1: chunks(std::integral_constant<int, 1>{}); break;
+                case 2: chunks(std::integral_constant<int, 2>{}); break;
+                case 3: chunks(std::integral_constant<int, 3>{}); break;
+                default: chunks(std::integral_constant<int, 4>{}); break;
+            }
+            wave_sync();
+            cur = nxt;
+            cb = nb;
+            cl = nl;
+            continue;
+        }
         auto ub = [&](int32_t lo, int32_t hi, int64_t x) -> int32_t {  // first j in [lo, hi) with ts_j > x
             while (lo < hi) {
                 const int32_t mid = (int32_t)((uint32_t)(lo + hi) >> 1);
@@ -1489,8 +1560,12 @@ static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, c
         FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
     } else {
-        hipLaunchKernelGGL(k_terminal_short, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off, n_seg, n,
-                           delay_ns, wa, n_windows, nb_d, risk_d, rec_d, compact_n);
+        if (n_windows == 3 && kTermShortNW)
+            hipLaunchKernelGGL(k_terminal_short<3>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off,
+                               n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, compact_n);
+        else
+            hipLaunchKernelGGL(k_terminal_short<0>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off,
+                               n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, compact_n);
         FDX_TERM_LAUNCH(false, kTermLdsRows, lo, inf);
     }
 #undef FDX_TERM_LAUNCH

@@ -237,8 +237,9 @@ class ShardedPipeline:
         we, ni = ops.time_flags(ts, p.flags_mode)
         base, n_local = self._range(n_customers_local)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
-        rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")
-        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        bad = torch.empty(1, dtype=torch.int32, device=ts.device)
+        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount, bad=bad)
+        rc = ops.KeyRangeCheck.from_count(bad, n_local, "customer ids of this shard")
         if p.avg_mode == "scan":
             cnb, cavg = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days)
         else:
@@ -282,8 +283,9 @@ class ShardedPipeline:
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
             mk("exchange_splits", side)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
-        rc = ops.KeyRangeCheck(cust, n_local, "customer ids of this shard")  # read after the layout's sync
-        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount)
+        bad = torch.empty(1, dtype=torch.int32, device=ts.device)  # counted in the re-key's first pass
+        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount, bad=bad)
+        rc = ops.KeyRangeCheck.from_count(bad, n_local, "customer ids of this shard")  # read after the layout's sync
         mk("rekey_customer", main)
         scan = p.avg_mode == "scan"
         walk = W >= 3

@@ -81,9 +81,11 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
 
 
 def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
-                  flag: torch.Tensor | None = None, stream=None, seg_off: bool = True):
+                  flag: torch.Tensor | None = None, stream=None, seg_off: bool = True, bad: torch.Tensor | None = None):
     """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
     grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
+    bad (int32 device scalar): receives the number of keys outside [0, n_keys), counted in the
+    first radix pass (fdx_rekey_payload_checked; see KeyRangeCheck.from_count).
     -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False), pay0 grouped | None,
     pay1 grouped | None)."""
     _dev(keys, torch.int32, "keys")
@@ -104,8 +106,14 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
     o1 = torch.empty_like(pay1) if pay1 is not None else None
     L = _lib.load()
     ws = workspace(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), dev)
-    check(L.fdx_rekey_payload(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm), _ptr(seg),
-                              _ptr(o0), _ptr(o1), _ptr(ws), ws.numel(), _s(stream)), "fdx_rekey_payload")
+    if bad is not None:
+        _dev(bad, torch.int32, "bad")
+        check(L.fdx_rekey_payload_checked(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1),
+                                          _ptr(perm), _ptr(seg), _ptr(o0), _ptr(o1), _ptr(bad), _ptr(ws), ws.numel(),
+                                          _s(stream)), "fdx_rekey_payload_checked")
+    else:
+        check(L.fdx_rekey_payload(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm),
+                                  _ptr(seg), _ptr(o0), _ptr(o1), _ptr(ws), ws.numel(), _s(stream)), "fdx_rekey_payload")
     return perm, seg, o0, o1
 
 
@@ -131,16 +139,24 @@ class KeyRangeCheck:
     """Enqueue a key-range count now, read it after the caller's next host synchronisation
     (no extra stall): the count is copied into pinned host memory on the same stream."""
 
-    def __init__(self, keys: torch.Tensor, n_keys: int, what: str = "keys", stream=None):
+    def __init__(self, keys: torch.Tensor | None, n_keys: int, what: str = "keys", stream=None,
+                 count: torch.Tensor | None = None):
         self.what, self.n_keys = what, int(n_keys)
         st = stream or torch.cuda.current_stream()
         self._host = torch.empty(1, dtype=torch.int32, pin_memory=True)
         # count, copy and event all on `st` (the copy must follow the count kernel, and the
         # event must follow the copy), whatever torch's current stream is
         with torch.cuda.stream(st):
-            self._host.copy_(count_out_of_range(keys, 0, n_keys, st), non_blocking=True)
+            self._host.copy_(count if count is not None else count_out_of_range(keys, 0, n_keys, st),
+                             non_blocking=True)
             self._ev = torch.cuda.Event()
             self._ev.record(st)
+
+    @classmethod
+    def from_count(cls, count: torch.Tensor, n_keys: int, what: str = "keys", stream=None) -> "KeyRangeCheck":
+        """Read a count some kernel already made on `stream` (rekey_payload(bad=...)): only the
+        pinned copy is enqueued."""
+        return cls(None, n_keys, what, stream, count=count)
 
     def check(self) -> None:
         self._ev.synchronize()

@@ -44,6 +44,11 @@ class FraudPipeline:
     sums, fully parallel, within ~1e-13 relative of pandas (the counts
     and every other feature stay exact)."""
 
+    # run_fused's stream priorities (lower = higher priority): the critical chain's and the
+    # terminal half's (measured, profiles/r03m* and r03w*)
+    crit_priority = -1
+    side_priority = 0
+
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
                  avg_mode: str = "exact", compact_records: bool = False):
@@ -142,12 +147,12 @@ class FraudPipeline:
         if ts_ns.numel() == 0:  # an empty table: nothing to score
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
-            self._side = torch.cuda.Stream(device=ts_ns.device)
+            self._side = torch.cuda.Stream(device=ts_ns.device, priority=self.side_priority)
             # the customer half -> assembly -> forest chain is the critical path: it runs on a
             # high-priority stream of the pipeline's own, the terminal half on a default one,
             # so that the dispatcher serves the critical kernels first when both have work
             # (measured: 12.35-12.40 -> 12.19-12.22 ms/step at config 2, profiles/r03m*)
-            self._crit = torch.cuda.Stream(device=ts_ns.device, priority=-1)
+            self._crit = torch.cuda.Stream(device=ts_ns.device, priority=self.crit_priority)
         main = self._crit if overlap else caller
         side = self._side if overlap else caller
         if main is not caller:
@@ -161,7 +166,13 @@ class FraudPipeline:
             # grouped order
             scan = self.avg_mode == "scan"
             walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
-            cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main)
+            # the id range checks ride on the re-keys' first histogram pass (bad counts), read once
+            # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
+            bad = torch.empty(2, dtype=torch.int32, device=ts_ns.device) if validate else None
+            cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
+                                                       bad=bad[0:1] if validate else None)
+            if validate:
+                rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
             mk("rekey_customer", main)
             # the walk's layout plan goes right behind the re-key; its slot count is read only
             # after the terminal half is enqueued (no host wait between the two)
@@ -170,16 +181,14 @@ class FraudPipeline:
             # perm); the records come out in input row order, read by the row assembly through irow.
             # Allocated under the side stream's context, so that the caching allocator hands
             # these buffers to nothing on the main stream while the side stream still uses them.
-            # (Out-of-range ids cannot make the re-keys write out of bounds; the range checks run
-            # here and are read once everything is enqueued.)
             compact = self.compact_records and W == 3
             with torch.cuda.stream(side):
                 mk("start", side)
-                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side)
+                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side,
+                                                         bad=bad[1:2] if validate else None)
+                if validate:
+                    rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
                 mk("rekey_terminal", side)
-                if validate:  # read once everything is enqueued
-                    rc = (ops.KeyRangeCheck(customer, n_customers, "customer ids", side),
-                          ops.KeyRangeCheck(terminal, n_terminals, "terminal ids", side))
                 if compact:
                     trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
                                                         windows_days=self.windows_days, stream=side)
@@ -187,7 +196,7 @@ class FraudPipeline:
                     trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
                                                         windows_days=self.windows_days, stream=side)
                 mk("terminal_windows", side)
-            for t in (ts_ns, customer, terminal, fraud):
+            for t in (ts_ns, customer, terminal, fraud) + ((bad,) if validate else ()):
                 t.record_stream(side)  # inputs in use on the side stream
             if pending is not None:
                 lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
@@ -212,7 +221,7 @@ class FraudPipeline:
             mk("assemble_rows", main)
             ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
             mk("forest_traverse", main)
-            if validate:  # read once everything is enqueued (the counts ran early on the side stream)
+            if validate:  # read once everything is enqueued (the counts ran in the re-keys)
                 for c in rc:
                     c.check()
         if main is not caller:

@@ -109,6 +109,16 @@ def test_fused_path_rejects_ids_out_of_range(dev):
     proba = torch.empty(n, dtype=torch.float64, device=dev)
     with pytest.raises(_lib.FdxError, match="customer ids"):
         pipe.run_fused(*args, 300, 500, proba)
+    # a negative terminal id (the terminal re-key's count, read through the side stream)
+    term = d["terminal"].copy()
+    term[n // 3] = -4
+    args = args[:1] + (T(d["customer"], torch.int32, dev), T(term, torch.int32, dev)) + args[3:]
+    with pytest.raises(_lib.FdxError, match="terminal ids"):
+        pipe.run_fused(*args, 300, 500, proba)
+    # in range again: the same pipeline scores (nothing left over from the failed calls)
+    args = args[:1] + (T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev)) + args[3:]
+    pipe.run_fused(*args, 300, 500, proba)
+    torch.cuda.synchronize()
 
 
 # ----------------------------------------------------------------- multi-rank dataflow

@@ -60,6 +60,20 @@ def test_rekey_stable(dev, n, n_keys):
         k2[::3] = -1 - k2[::3]
         ops.key_segments(T(k2, torch.int32, dev), n_keys, bad=bad)
         assert int(bad.item()) == len(k2[::3])
+    # the checked re-key counts the same keys inside its first histogram pass (and still groups)
+    bad = torch.full((1,), 77, dtype=torch.int32, device=dev)
+    pp, sp, _, _ = ops.rekey_payload(T(keys, torch.int32, dev), n_keys, bad=bad)
+    np.testing.assert_array_equal(pp.cpu().numpy(), ref)
+    np.testing.assert_array_equal(sp.cpu().numpy(), seg.cpu().numpy())
+    assert int(bad.item()) == 0
+    if n:
+        k3 = keys.copy()
+        k3[::5] = -1 - k3[::5]                       # negative ids
+        k3[1::7] = n_keys + k3[1::7] % 3             # ids at and just past n_keys
+        k3[2::11] = np.int32(2**31 - 1)              # the largest int32
+        exp = int(np.count_nonzero((k3 < 0) | (k3 >= n_keys)))
+        ops.rekey_payload(T(k3, torch.int32, dev), n_keys, T(np.arange(n, dtype=np.int64), torch.int64, dev), bad=bad)
+        assert int(bad.item()) == exp
 
 
 def test_argsort_i64_and_perm_ops(dev):
