@@ -23,6 +23,13 @@ constexpr int kMaxBins = 512;
 constexpr int kBlock = 256;
 constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096 keys per tile
+// A/B switch (compile time): when the scatter loads its payload streams (0: each after the
+// previous phase's stores; 1: stream 0 behind the key re-order, stream q + 1 during stream q's;
+// 2: stream 0 with the keys)
+#ifndef FDX_RADIX_PREFETCH
+#define FDX_RADIX_PREFETCH 1
+#endif
+constexpr int kRadixPrefetch = FDX_RADIX_PREFETCH;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // ---------------------------------------------------------------- device-wide scan
@@ -282,6 +289,17 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         load_items(std::true_type{});
     else
         load_items(std::false_type{});
+    // payload registers: stream q's 16 values of this lane, coalesced in input order (clamped:
+    // no branch); with kRadixPrefetch the loads of stream 0 go out before the key phases and
+    // those of stream q + 1 while stream q is re-ordered, instead of each after the previous
+    // phase's stores
+    uint64_t pv[PW > 0 ? kItems : 1];
+    auto load_pay = [&](const uint64_t *pin) {
+#pragma unroll
+        for (int r = 0; r < kItems; ++r) pv[r] = pin[min(wbase + (int64_t)r * kWave, n - 1)];
+    };
+    if constexpr (PW > 0)
+        if (kRadixPrefetch == 2) load_pay(p0_in);
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const int64_t i = wbase + (int64_t)r * kWave;
@@ -349,6 +367,8 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
             s_val[p] = val[r];
         }
     }
+    if constexpr (PW > 0)
+        if (kRadixPrefetch == 1) load_pay(p0_in);
     __syncthreads();
     const int64_t tcnt = std::min<int64_t>(kTile, n - base);
     int32_t dsts[kItems];  // destination of tile position tid + j * kBlock
@@ -367,16 +387,13 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
         uint64_t *s_pay = reinterpret_cast<uint64_t *>(s_kv);
 #pragma unroll
         for (int q = 0; q < PW; ++q) {
-            const uint64_t *pin = q == 0 ? p0_in : p1_in;
             uint64_t *pout = q == 0 ? p0_out : p1_out;
-            uint64_t v[kItems];
-#pragma unroll
-            for (int r = 0; r < kItems; ++r)  // coalesced, input order; clamped (no branch)
-                v[r] = pin[min(wbase + (int64_t)r * kWave, n - 1)];
+            if (kRadixPrefetch == 0) load_pay(q == 0 ? p0_in : p1_in);
             __syncthreads();  // the previous contents of the LDS slots are consumed
 #pragma unroll
             for (int r = 0; r < kItems; ++r)
-                if (wbase + (int64_t)r * kWave < n) s_pay[pos[r]] = v[r];
+                if (wbase + (int64_t)r * kWave < n) s_pay[pos[r]] = pv[r];
+            if (kRadixPrefetch != 0 && q + 1 < PW) load_pay(p1_in);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kItems; ++j) {
