@@ -53,7 +53,7 @@ STAGES = [
     ("customer_layout", "K1-cust", [("k_interleave<true, true>", 1)]),
     ("customer_walk", "K1-cust", [("k_customer_walk", 1)]),
     ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 2), ("k_radix_scatter<unsigned int, 9, 1>", 2)]),
-    ("terminal_windows", "K1-term", [("k_terminal_g<false>", 1)]),
+    ("terminal_windows", "K1-term", [("k_terminal_short<3>", 1), ("k_terminal_g<false, 1024>", 1)]),
     ("assemble_rows", "K3", [("k_zfill_grouped_w3", 1)]),
     ("forest_traverse", "K3", [("k_forest_rank", "chunks")]),
 ]

@@ -436,11 +436,13 @@ def test_layout_plan_order(dev, case):
     assert torch.equal(pa.goff[: len(gslots) + 1], plan.goff[: len(gslots) + 1])
 
 
-def test_fused_scoring_rank_table_overflows(dev):
+@pytest.mark.parametrize("compact", [False, True])
+def test_fused_scoring_rank_table_overflows(dev, compact):
     """The scoring-row assembly of the fused path (k_zfill_grouped_w3: integer rank table for
-    counts < 256, ratio table for terminal windows with NB < 128, searched otherwise) scores
-    bit-identically to the float64-X path (full two-level search of every feature) when
-    customer counts reach >= 256 and terminal counts >= 128, with thresholds placed there."""
+    counts < 256, ratio table for terminal windows with NB < 128, searched otherwise; 24-byte
+    or compact terminal records) scores bit-identically to the float64-X path (full two-level
+    search of every feature) when customer counts reach >= 256 and terminal counts >= 128,
+    with thresholds placed there."""
     from fdx import synth
 
     d = synth.generate(n_customers=400, n_terminals=500, nb_days=60, seed=41)
@@ -456,15 +458,37 @@ def test_fused_scoring_rank_table_overflows(dev):
     args = (T(d["ts"], torch.int64, dev), T(cust, torch.int32, dev), T(term, torch.int32, dev),
             T(d["amount"], torch.float64, dev), T(d["fraud"], torch.uint8, dev))
     n = len(d["ts"])
-    pipe = FraudPipeline(forest=forest)
+    pipe = FraudPipeline(forest=forest, compact_records=compact)
     f, p_ref = pipe.run(*args, 400, 500)
     X = f.X.cpu().numpy()
     assert X[:, 7].max() >= 256 and X[:, 13].max() >= 128  # both table overflows occur
-    ws = ops.workspace(forest.workspace_size(n), dev)
+    ws = ops.workspace(forest.workspace_size(n * 11 // 10), dev)
     p1 = torch.empty(n, dtype=torch.float64, device=dev)
     pipe.run_fused(*args, 400, 500, p1, ws)
     np.testing.assert_array_equal(p1.cpu().numpy(), p_ref.cpu().numpy())
     np.testing.assert_array_equal(p_ref.cpu().numpy(), oracle.forest_predict(X, arrays, mean, scale))
+
+
+def test_fused_scoring_nan_amounts(dev):
+    """NaN amounts through the fused path: the assembly's NaN flag routes the traversal through
+    missing_go_to_left, equal to the float64-X path."""
+    from fdx import synth
+
+    d = synth.generate(n_customers=300, n_terminals=400, nb_days=40, seed=43)
+    amt = d["amount"].copy()
+    amt[np.random.default_rng(1).choice(len(amt), 25, replace=False)] = np.nan
+    arrays = random_forest(np.random.default_rng(8), 8, 7)
+    mean, scale = np.zeros(15), np.ones(15)
+    forest = ops.Forest(arrays, 15, mean, scale)
+    args = (T(d["ts"], torch.int64, dev), T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev),
+            T(amt, torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    n = len(d["ts"])
+    pipe = FraudPipeline(forest=forest)
+    f, p_ref = pipe.run(*args, 300, 400)
+    assert np.isnan(f.X.cpu().numpy()[:, 0]).sum() == 25
+    p = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 300, 400, p, ops.workspace(forest.workspace_size(n * 11 // 10), dev))
+    np.testing.assert_array_equal(p.cpu().numpy(), p_ref.cpu().numpy())
 
 
 @pytest.mark.parametrize("variant", [1, 3, 4, 5, 6, 7, 9, 10])
