@@ -30,6 +30,7 @@
 #include <cstring>
 #include <functional>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "fdx_internal.h"
@@ -614,6 +615,24 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
 // segment reads and three ratio-table reads are issued together, unconditionally (clamped
 // addresses; the host pads useg by one segment), so a row costs about one round trip.
 // Results are bit-identical to k_zfill_grouped<16, true> (same arithmetic, same fallbacks).
+// A/B switch (compile time): k_zfill_grouped_w3's segment counts by lane quads (1) or per lane (0)
+#ifndef FDX_ZFILL_QUAD
+#define FDX_ZFILL_QUAD 1
+#endif
+constexpr bool kZfillQuad = FDX_ZFILL_QUAD != 0;
+
+// lane K of each quad of lanes, to all 4 (DPP quad_perm broadcast; every lane of the wave active)
+template <int K>
+__device__ __forceinline__ int32_t quad_bcast(int32_t x) {
+    return __builtin_amdgcn_update_dpp(0, x, K * 0x55, 0xF, 0xF, false);
+}
+// the sum over each quad of lanes, in all 4 (DPP quad_perm [1,0,3,2] then [2,3,0,1])
+__device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)c, 0xB1, 0xF, 0xF, false);
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)c, 0x4E, 0xF, 0xF, false);
+    return c;
+}
+
 struct PrepRow {
     int64_t t;
     double a;
@@ -642,7 +661,17 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
     auto row_of = [&](int64_t j) -> int32_t { return j < n ? (cust_perm ? cust_perm[j] : (int32_t)j) : -1; };
     auto load = [&](int64_t j, int32_t r, PrepRow &L) {
         L.r = r;
-        if (j >= n || r < 0) return;
+        if (j >= n || r < 0) {  // defined values: every lane runs the row arithmetic (quad rounds)
+            L.t = 0;
+            L.a = 0.0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                L.c[w] = 1;
+                L.cv[w] = 0.0;
+                L.tw[w] = 0;
+            }
+            return;
+        }
         L.t = cts[j];
         L.a = camt[j];
 #pragma unroll
@@ -671,21 +700,19 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
             for (int w = 0; w < W; ++w) L.tw[w] = src[w];
         }
     };
+    // wave-uniform loop (stride and the wave's first slot are multiples of 64): every lane of a
+    // wave runs each iteration, so the quads of k_seg_count_quad stay whole; lanes past n and
+    // padding slots compute on defined dummies and store the zero row / nothing
+    const int lane = threadIdx.x & (kWave - 1);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     PrepRow cur;
     load(i, row_of(i), cur);
     int32_t r_next = row_of(i + stride);
-    for (; i < n; i += stride) {
+    for (; i - lane < n; i += stride) {
         PrepRow nxt;
         load(i + stride, r_next, nxt);  // next row's loads in flight during this row
         r_next = row_of(i + 2 * stride);
-        if (cur.r < 0) {  // padding slot of the interleaved layout
-            uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
-            dst[0] = make_uint4(0, 0, 0, 0);
-            dst[1] = make_uint4(0, 0, 0, 0);
-            cur = nxt;
-            continue;
-        }
+        const bool live = i < n && cur.r >= 0;
         const int64_t t = cur.t;
         int64_t day = t / kDay;
         if (t % kDay != 0 && t < 0) --day;
@@ -739,24 +766,65 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
                 if (l < rt.elev[s]) ek[s] = 2 * ek[s] + (s_e[rt.eoff[s] + ek[s]] < v[kW3Search[s]] ? 1 : 0);
         }
         int32_t cs[4];
-        float4 sg[4][4];
+        uint32_t kc[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int f = kW3Search[s];
-            cs[s] = ek[s] - (1 << rt.elev[s]);
-            const float4 *p = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)max(cs[s] - 1, 0) * 16);
+        for (int s = 0; s < 4; ++s) cs[s] = ek[s] - (1 << rt.elev[s]);
+        if constexpr (kZfillQuad) {
+            // a quad of lanes per segment: round K loads lane K's 64-byte segment as 4 x 16 B
+            // (lane j of the quad: bytes 16j..16j+15), so each load instruction touches 16 lines
+            // instead of 64 -- the address unit serves a gather line by line -- and the quad sums
+            // its 4 partial counts (DPP); lane K keeps round K's count
+            const int qj = lane & 3;
+            int32_t sidx[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) sg[s][k] = p[k];
+            for (int s = 0; s < 4; ++s) sidx[s] = max(cs[s] - 1, 0);
+            auto round = [&](auto kk) {
+                constexpr int K = decltype(kk)::value;
+                float4 w4[4];
+                float vk[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int f = kW3Search[s];
+                    const int32_t si = quad_bcast<K>(sidx[s]);
+                    vk[s] = __int_as_float(quad_bcast<K>(__float_as_int(v[f])));
+                    w4[s] = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)si * 16)[qj];
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    uint32_t c = (uint32_t)(w4[s].x < vk[s]) + (uint32_t)(w4[s].y < vk[s]) +
+                                 (uint32_t)(w4[s].z < vk[s]) + (uint32_t)(w4[s].w < vk[s]);
+                    c = quad_sum(c);
+                    kc[s] = qj == K ? c : kc[s];
+                }
+            };
+            round(std::integral_constant<int, 0>{});
+            round(std::integral_constant<int, 1>{});
+            round(std::integral_constant<int, 2>{});
+            round(std::integral_constant<int, 3>{});
+        } else {
+            float4 sg[4][4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int f = kW3Search[s];
+                const float4 *p = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)max(cs[s] - 1, 0) * 16);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) sg[s][k] = p[k];
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int f = kW3Search[s];
+                uint32_t k = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    k += (uint32_t)(sg[s][e].x < v[f]) + (uint32_t)(sg[s][e].y < v[f]) +
+                         (uint32_t)(sg[s][e].z < v[f]) + (uint32_t)(sg[s][e].w < v[f]);
+                kc[s] = k;
+            }
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int f = kW3Search[s];
-            uint32_t k = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                k += (uint32_t)(sg[s][e].x < v[f]) + (uint32_t)(sg[s][e].y < v[f]) + (uint32_t)(sg[s][e].z < v[f]) +
-                     (uint32_t)(sg[s][e].w < v[f]);
-            const uint32_t r = cs[s] > 0 ? (uint32_t)(cs[s] - 1) * 16u + k : 0u;
+            const uint32_t r = cs[s] > 0 ? (uint32_t)(cs[s] - 1) * 16u + kc[s] : 0u;
             q[f] = v[f] != v[f] ? 0xFFFFu : r;
         }
 #pragma unroll
@@ -770,13 +838,17 @@ __global__ void __launch_bounds__(256) k_zfill_grouped_w3(
                 nan |= v[fr_] != v[fr_];
             }
         }
-        if (nan) *nan_flag = 1;
+        if (live && nan) *nan_flag = 1;
         need &= (1u << nf) - 1u;
-        if (need) rank_row_global(v, rt, q, need);  // table overflows (rare): full lower_bound in HBM
+        if (live && need) rank_row_global(v, rt, q, need);  // table overflows (rare): full lower_bound in HBM
         q[15] = 0u;
-        uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
-        dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
-        dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
+        if (i < n) {  // padding slot of the interleaved layout: the zero row
+            uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);
+            dst[0] = live ? make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16)
+                          : make_uint4(0, 0, 0, 0);
+            dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
+                          : make_uint4(0, 0, 0, 0);
+        }
         cur = nxt;
     }
 }
