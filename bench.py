@@ -120,8 +120,9 @@ def parse():
     ap.add_argument("--isolated-steps", type=int, default=3,
                     help="extra untimed steps with every stage on one stream: per-kernel times for the roofline table")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
-    ap.add_argument("--compact-records", action="store_true",
-                    help="terminal count records in the 16-byte compact form (FraudPipeline(compact_records=True))")
+    ap.add_argument("--wide-records", action="store_true",
+                    help="terminal count records in the 24-byte form (FraudPipeline(compact_records=False); "
+                         "default: the 16-byte compact form)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
@@ -328,7 +329,7 @@ def main():
         raise SystemExit("forest parity check against sklearn failed")
 
     ts, cust, term, amt, fr = g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"]
-    pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode, compact_records=args.compact_records)
+    pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode, compact_records=not args.wide_records)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
     marks_all = []   # per timed step: {stage: (start event, end event)}

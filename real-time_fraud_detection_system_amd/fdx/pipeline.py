@@ -51,11 +51,13 @@ class FraudPipeline:
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
-                 avg_mode: str = "exact", compact_records: bool = False):
+                 avg_mode: str = "exact", compact_records: bool = True):
         if avg_mode not in ("exact", "scan"):
             raise ValueError("avg_mode must be 'exact' or 'scan'")
         self.avg_mode = avg_mode
-        # the scoring path's terminal count records in the 16-byte compact form (3 windows)
+        # the scoring path's terminal count records in the 16-byte compact form (3 windows): one
+        # 16-byte store / load per row at random instead of two for the 24-byte record
+        # (terminal windows 0.65 -> 0.41 ms alone, profiles/r03ac_compact_records_ab.txt)
         self.compact_records = bool(compact_records)
         self.windows_days = tuple(int(w) for w in windows_days)
         self.delay_days = int(delay_days)
