@@ -642,7 +642,13 @@ struct PrepRow {
     int32_t r;
 };
 
-__global__ void __launch_bounds__(256) k_zfill_grouped_w3(
+// A/B switch (compile time): minimum waves per SIMD the compiler must fit k_zfill_grouped_w3's
+// registers to (0: the compiler's choice, 156 VGPRs / 3 waves; 4: 128 VGPRs, assembly 1.02-1.09 -> 0.985 ms
+// alone, profiles/r03af_zfill_waves_ab.txt)
+#ifndef FDX_ZFILL_WAVES
+#define FDX_ZFILL_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
