@@ -380,6 +380,8 @@ class PendingPlan:
     (no earlier) and returns the LayoutPlan (re-planning synchronously if the one-launch plan
     declined)."""
 
+    SPIN = 2_000_000  # polls of the pinned result (~0.1 us each) before the blocking wait
+
     def __init__(self, seg_off, n_windows, stream):
         self.seg_off, self.n_windows, self.stream = seg_off, int(n_windows), stream
         n_seg = seg_off.numel() - 1
@@ -389,7 +391,9 @@ class PendingPlan:
         self.sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
         self.goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
         self.ws = workspace(L.fdx_customer_layout_workspace_size(n_seg), dev)
-        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        # [slot count, status], -1 until the stream's copy lands (result() polls for it)
+        self.host = torch.full((2,), -1, dtype=torch.int32, pin_memory=True)
+        self._hv = self.host.numpy()
         st = stream or torch.cuda.current_stream()
         rc = L.fdx_customer_layout_plan_async(_ptr(seg_off), n_seg, self.n_windows, _ptr(self.sorder), _ptr(self.goff),
                                               self.host.data_ptr(), _ptr(self.ws), self.ws.numel(), _s(st))
@@ -401,9 +405,17 @@ class PendingPlan:
 
     def result(self) -> LayoutPlan:
         if self.ok:
-            self.ev.synchronize()
-            if int(self.host[1]) == 0:
-                return LayoutPlan(self.sorder, self.goff, int(self.host[0]) & 0xFFFFFFFF, self.n_windows)
+            # poll the pinned words for a bounded while before the blocking wait: the step's
+            # critical stream idles until the host has read the slot count and launched the
+            # layout fill, and waking from hipEventSynchronize took ~70 us (profiles/r03ad)
+            hv = self._hv
+            for _ in range(self.SPIN):
+                if hv[0] != -1 and hv[1] != -1:
+                    break
+            else:
+                self.ev.synchronize()
+            if int(hv[1]) == 0:
+                return LayoutPlan(self.sorder, self.goff, int(hv[0]) & 0xFFFFFFFF, self.n_windows)
         return customer_layout_plan(self.seg_off, self.n_windows, self.stream)
 
 

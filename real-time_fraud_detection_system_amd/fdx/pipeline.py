@@ -173,12 +173,12 @@ class FraudPipeline:
             bad = torch.empty(2, dtype=torch.int32, device=ts_ns.device) if validate else None
             cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
                                                        bad=bad[0:1] if validate else None)
-            if validate:
-                rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
             mk("rekey_customer", main)
             # the walk's layout plan goes right behind the re-key; its slot count is read only
             # after the terminal half is enqueued (no host wait between the two)
             pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
+            if validate:  # (its pinned copy behind the plan, not in front of it: up to 38 us)
+                rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
             # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
             # perm); the records come out in input row order, read by the row assembly through irow.
             # Allocated under the side stream's context, so that the caching allocator hands
