@@ -30,6 +30,12 @@ constexpr int kTile = kBlock * kItems;  // 4096 keys per tile
 #define FDX_RADIX_PREFETCH 1
 #endif
 constexpr int kRadixPrefetch = FDX_RADIX_PREFETCH;
+// A/B switch (compile time): k_radix_hist's counts by LDS atomics (1; re-keys 0.585 / 0.553 -> 0.553 /
+// 0.534 ms, profiles/r03am_radix_hist_ab.txt) or ballot multisplit (0)
+#ifndef FDX_RADIX_HIST_ATOMIC
+#define FDX_RADIX_HIST_ATOMIC 1
+#endif
+constexpr bool kHistAtomic = FDX_RADIX_HIST_ATOMIC != 0;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // ---------------------------------------------------------------- device-wide scan
@@ -162,18 +168,27 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
         const int64_t i = wbase + (int64_t)r * kWave;
         key[r] = i < n ? keys[i] : (K)0;
     }
+    if constexpr (kHistAtomic) {
+        // counts only (no ranks): one LDS atomic add per key on the wave's own counters -- lanes
+        // of one digit in one instruction serialise on their address, which costs less than the
+        // BITS ballots per key of the multisplit
 #pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const bool valid = wbase + (int64_t)r * kWave < n;
-        const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
-        uint64_t peers = __ballot(valid);
+        for (int r = 0; r < kItems; ++r)
+            if (wbase + (int64_t)r * kWave < n) atomicAdd(&h[digit_of<K, BITS>(key[r], shift, flip)], 1u);
+    } else {
 #pragma unroll
-        for (int b = 0; b < BITS; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
+        for (int r = 0; r < kItems; ++r) {
+            const bool valid = wbase + (int64_t)r * kWave < n;
+            const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < BITS; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            if (valid && (peers & lt_mask) == 0) h[d] += (uint32_t)__popcll(peers);
         }
-        if (valid && (peers & lt_mask) == 0) h[d] += (uint32_t)__popcll(peers);
     }
     if (bad) {
         int nb = 0;
