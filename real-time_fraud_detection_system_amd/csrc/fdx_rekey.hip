@@ -142,10 +142,11 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
 }
 
 // Per-tile digit counts, in the scatter's blocked order (wave w counts the 1,024 consecutive
-// keys [w * 1024, (w + 1) * 1024) of the tile).  Each wave keeps its own LDS counters and, per
-// item, only the lowest lane of each group of equal digits (ballot multisplit) adds the
-// group's size: no two lanes of an instruction touch one counter, where one block-shared
-// atomicAdd per key spent ~70 % of its LDS cycles on same-address conflicts (r02 PMC).
+// keys [w * 1024, (w + 1) * 1024) of the tile).  Each wave keeps its own LDS counters (one
+// block-shared atomicAdd per key spent ~70 % of its LDS cycles on same-address conflicts, r02
+// PMC); by default each key is one LDS atomic add on them (kHistAtomic), else only the lowest
+// lane of each group of equal digits (ballot multisplit) adds the group's size -- no two lanes
+// on one counter, but BITS ballots per key, which the counts alone do not need.
 // bad != nullptr (first pass of fdx_rekey_payload_checked): also count the keys >= key_limit
 // (as unsigned: negative int32 ids count too) -- the id range check rides on this pass's reads.
 template <typename K, int BITS>
