@@ -445,6 +445,28 @@ __global__ void k_seg_mark(const uint32_t *__restrict__ sk, int64_t n, int64_t n
     }
 }
 
+// k_seg_mark over 16-byte aligned keys, 4 per thread and trip: one 16-byte load, the previous
+// key an L1 / L2 hit (the neighbouring thread's line)
+__global__ void k_seg_mark4(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys, int64_t *__restrict__ seg_off) {
+    const int64_t n4 = n / 4;
+    const uint4 *sk4 = reinterpret_cast<const uint4 *>(sk);
+    auto mark = [&](int64_t i, uint32_t k, uint32_t prev) {
+        if ((int64_t)k < n_keys && (i == 0 || prev != k)) seg_off[k] = i;
+    };
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 v = sk4[q];
+        const uint32_t prev = q > 0 ? sk[4 * q - 1] : 0u;
+        const int64_t i = 4 * q;
+        mark(i, v.x, prev);
+        mark(i + 1, v.y, v.x);
+        mark(i + 2, v.z, v.y);
+        mark(i + 3, v.w, v.z);
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)  // the last n % 4 keys
+        mark(i, sk[i], i > 0 ? sk[i - 1] : 0u);
+}
+
 __global__ void k_seg_fill(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys, int64_t *__restrict__ seg_off) {
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n_keys;
          q += (int64_t)gridDim.x * blockDim.x) {
@@ -460,8 +482,14 @@ __global__ void k_seg_fill(const uint32_t *__restrict__ sk, int64_t n, int64_t n
 
 int seg_offsets(const uint32_t *sk, int64_t n, int64_t n_keys, int64_t *seg_off, hipStream_t st) {
     FDX_HIP(hipMemsetAsync(seg_off, 0xFF, sizeof(int64_t) * (size_t)(n_keys + 1), st));
-    hipLaunchKernelGGL(k_seg_mark, dim3(stream_grid(n, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
-    FDX_LAUNCHED("k_seg_mark");
+    if (((uintptr_t)sk & 15) == 0) {  // (the radix buffers; a caller's sorted_keys_d may not be)
+        hipLaunchKernelGGL(k_seg_mark4, dim3(stream_grid(ceil_div(n, 4), 256)), dim3(256), 0, st, sk, n, n_keys,
+                           seg_off);
+        FDX_LAUNCHED("k_seg_mark4");
+    } else {
+        hipLaunchKernelGGL(k_seg_mark, dim3(stream_grid(n, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
+        FDX_LAUNCHED("k_seg_mark");
+    }
     hipLaunchKernelGGL(k_seg_fill, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
     FDX_LAUNCHED("k_seg_fill");
     return FDX_OK;

@@ -76,6 +76,29 @@ def test_rekey_stable(dev, n, n_keys):
         assert int(bad.item()) == exp
 
 
+def test_rekey_sorted_keys_unaligned_output(dev):
+    """fdx_rekey with the caller's sorted_keys_d 4 bytes off a 16-byte boundary: the segment
+    offsets come from the scalar boundary pass (the 4-keys-per-thread one needs alignment)."""
+    from fdx import _lib
+
+    rng = np.random.default_rng(11)
+    n, n_keys = 100_003, 3_000
+    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
+    L = _lib.load()
+    kb = ops.key_bits_for(n_keys)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev)
+    skbuf = torch.empty(n + 4, dtype=torch.int32, device=dev)
+    ws = ops.workspace(L.fdx_rekey_workspace_size(n, kb), dev)
+    kd = T(keys, torch.int32, dev)
+    ops.check(L.fdx_rekey(ops._ptr(kd), n, kb, n_keys, ops._ptr(perm),
+                          skbuf.data_ptr() + 4, ops._ptr(seg), ops._ptr(ws), ws.numel(), None), "fdx_rekey")
+    ref = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(perm.cpu().numpy(), ref)
+    np.testing.assert_array_equal(skbuf[1:n + 1].cpu().numpy(), keys[ref])
+    np.testing.assert_array_equal(seg.cpu().numpy(), np.r_[0, np.cumsum(np.bincount(keys, minlength=n_keys))])
+
+
 def test_argsort_i64_and_perm_ops(dev):
     rng = np.random.default_rng(3)
     k = rng.integers(-(1 << 62), 1 << 62, size=200_001, dtype=np.int64)
