@@ -432,66 +432,61 @@ __global__ void k_copy_u32(const uint32_t *__restrict__ in, uint32_t *__restrict
         out[i] = in[i];
 }
 
-// seg_off[q] = first sorted position whose key >= q, for q in [0, n_keys], in two passes:
-// k_seg_mark -- every segment start i writes seg_off[key_i] = i (one coalesced read of the
-// sorted keys; the slots of absent keys keep the -1 they were filled with) -- then k_seg_fill:
-// an absent key (and q = n_keys) gets its offset by binary search, which every key would
-// need otherwise (85 us at 100k keys over 17.8M rows, a chain of random loads per key; the two
-// passes take ~25 us when every key has rows).
-__global__ void k_seg_mark(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys, int64_t *__restrict__ seg_off) {
+// seg_off[q] = first sorted position whose key >= q, for q in [0, n_keys], in ONE pass over the
+// sorted keys: every boundary i (key sk[i-1] < sk[i], or i = 0) writes seg_off[q] = i for the keys
+// q in (sk[i-1], sk[i]] -- absent keys included, so no search -- and the last row writes n for
+// (sk[n-1], n_keys].  Each q is written once when the keys are sorted and in range.  (Three
+// launches before -- fill -1, mark the present keys, binary-search the absent ones.)  The buffer
+// is zeroed first, so that out-of-range ids -- which sort out of key order and are rejected
+// after the step (fdx_rekey_payload_checked) -- can never leave an offset outside [0, n].
+__device__ __forceinline__ void seg_bound(int64_t i, int64_t prev, int64_t cur, int64_t n_keys,
+                                          int64_t *__restrict__ seg_off) {
+    const int64_t q1 = min(cur, n_keys);
+    for (int64_t q = prev + 1; q <= q1; ++q) seg_off[q] = i;
+}
+
+__global__ void k_seg_bounds(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys,
+                             int64_t *__restrict__ seg_off) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = sk[i];
-        if ((int64_t)k < n_keys && (i == 0 || sk[i - 1] != k)) seg_off[k] = i;
+        const int64_t cur = sk[i];
+        seg_bound(i, i > 0 ? (int64_t)sk[i - 1] : -1, cur, n_keys, seg_off);
+        if (i == n - 1) seg_bound(n, cur, n_keys, n_keys, seg_off);
     }
 }
 
-// k_seg_mark over 16-byte aligned keys, 4 per thread and trip: one 16-byte load, the previous
-// key an L1 / L2 hit (the neighbouring thread's line)
-__global__ void k_seg_mark4(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys, int64_t *__restrict__ seg_off) {
+// k_seg_bounds over 16-byte aligned keys, 4 per thread and trip (one 16-byte load; the previous
+// key an L1 / L2 hit, the neighbouring thread's line)
+__global__ void k_seg_bounds4(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys,
+                              int64_t *__restrict__ seg_off) {
     const int64_t n4 = n / 4;
     const uint4 *sk4 = reinterpret_cast<const uint4 *>(sk);
-    auto mark = [&](int64_t i, uint32_t k, uint32_t prev) {
-        if ((int64_t)k < n_keys && (i == 0 || prev != k)) seg_off[k] = i;
-    };
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
         const uint4 v = sk4[q];
-        const uint32_t prev = q > 0 ? sk[4 * q - 1] : 0u;
         const int64_t i = 4 * q;
-        mark(i, v.x, prev);
-        mark(i + 1, v.y, v.x);
-        mark(i + 2, v.z, v.y);
-        mark(i + 3, v.w, v.z);
+        seg_bound(i, q > 0 ? (int64_t)sk[i - 1] : -1, v.x, n_keys, seg_off);
+        seg_bound(i + 1, v.x, v.y, n_keys, seg_off);
+        seg_bound(i + 2, v.y, v.z, n_keys, seg_off);
+        seg_bound(i + 3, v.z, v.w, n_keys, seg_off);
+        if (i + 3 == n - 1) seg_bound(n, v.w, n_keys, n_keys, seg_off);
     }
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)  // the last n % 4 keys
-        mark(i, sk[i], i > 0 ? sk[i - 1] : 0u);
-}
-
-__global__ void k_seg_fill(const uint32_t *__restrict__ sk, int64_t n, int64_t n_keys, int64_t *__restrict__ seg_off) {
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= n_keys;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        if (q < n_keys && seg_off[q] >= 0) continue;
-        int64_t lo = 0, hi = n;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if ((int64_t)sk[mid] < q) lo = mid + 1; else hi = mid;
-        }
-        seg_off[q] = lo;
+         i += (int64_t)gridDim.x * blockDim.x) {  // the last n % 4 keys
+        const int64_t cur = sk[i];
+        seg_bound(i, i > 0 ? (int64_t)sk[i - 1] : -1, cur, n_keys, seg_off);
+        if (i == n - 1) seg_bound(n, cur, n_keys, n_keys, seg_off);
     }
 }
 
 int seg_offsets(const uint32_t *sk, int64_t n, int64_t n_keys, int64_t *seg_off, hipStream_t st) {
-    FDX_HIP(hipMemsetAsync(seg_off, 0xFF, sizeof(int64_t) * (size_t)(n_keys + 1), st));
+    FDX_HIP(hipMemsetAsync(seg_off, 0, sizeof(int64_t) * (size_t)(n_keys + 1), st));
     if (((uintptr_t)sk & 15) == 0) {  // (the radix buffers; a caller's sorted_keys_d may not be)
-        hipLaunchKernelGGL(k_seg_mark4, dim3(stream_grid(ceil_div(n, 4), 256)), dim3(256), 0, st, sk, n, n_keys,
+        hipLaunchKernelGGL(k_seg_bounds4, dim3(stream_grid(ceil_div(n, 4), 256)), dim3(256), 0, st, sk, n, n_keys,
                            seg_off);
-        FDX_LAUNCHED("k_seg_mark4");
+        FDX_LAUNCHED("k_seg_bounds4");
     } else {
-        hipLaunchKernelGGL(k_seg_mark, dim3(stream_grid(n, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
-        FDX_LAUNCHED("k_seg_mark");
+        hipLaunchKernelGGL(k_seg_bounds, dim3(stream_grid(n, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
+        FDX_LAUNCHED("k_seg_bounds");
     }
-    hipLaunchKernelGGL(k_seg_fill, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, sk, n, n_keys, seg_off);
-    FDX_LAUNCHED("k_seg_fill");
     return FDX_OK;
 }
 

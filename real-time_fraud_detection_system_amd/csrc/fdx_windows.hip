@@ -220,7 +220,9 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     __syncthreads();
     const int64_t per = (n_seg + kPlanWaves - 1) / kPlanWaves;
     const int64_t lo = wv * per, hi = min<int64_t>(n_seg, lo + per);
-    auto len_of = [&](int64_t sg) -> int64_t { return seg_off[sg + 1] - seg_off[sg]; };
+    // (lengths clamped at 0: out-of-range ids, rejected after the step, can leave the offsets
+    // out of order -- never an out-of-bounds counter)
+    auto len_of = [&](int64_t sg) -> int64_t { return max<int64_t>(seg_off[sg + 1] - seg_off[sg], 0); };
     // 1. bins of this wave's chunks (kept in registers, two u16 per VGPR: 0xFFFF = none, 0 =
     // long), wave-private counts
     uint32_t binp[kPlanChunks / 2] = {};
@@ -230,8 +232,10 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     };
     constexpr int kBatch = 8;  // chunks whose offsets are loaded together (one load per segment:
                                 // the next offset comes from the next lane, lane 63 loads it)
+    const int n_chunks = (int)((max<int64_t>(hi - lo, 0) + kWave - 1) / kWave);  // this wave's
 #pragma unroll
     for (int c0 = 0; c0 < kPlanChunks; c0 += kBatch) {
+        if (c0 >= n_chunks) continue;  // (uniform; phase 3 skips these chunks too)
         int64_t a[kBatch], e63[kBatch];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
@@ -243,7 +247,7 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
         for (int j = 0; j < kBatch; ++j) {
             const int64_t sg = lo + (int64_t)(c0 + j) * kWave + lane;
             const int64_t nx = __shfl_down(a[j], 1, kWave);
-            const int64_t L = (lane == kWave - 1 ? e63[j] : nx) - a[j];
+            const int64_t L = max<int64_t>((lane == kWave - 1 ? e63[j] : nx) - a[j], 0);
             const int32_t bn = sg >= hi ? 0xFFFF : (L >= kPlanBins - 1 ? 0 : (int32_t)(kPlanBins - 1 - L));
             binp[(c0 + j) >> 1] |= (uint32_t)bn << (16 * ((c0 + j) & 1));
             if (sg < hi) {
@@ -300,10 +304,13 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
         sorder[r] = si;
         if (r % S == 0) s_gs[r / S] = (uint32_t)(S * len_of(si));
     }
-    // 3. each wave places its chunks in index order
+    // 3. each wave places its chunks in index order (chunks past the wave's range skipped:
+    // uniform; the group index pos / S by a reciprocal multiply, exact for pos < 2^16)
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t s_inv = (uint32_t)((0xFFFFFFFFull + (uint64_t)S) / (uint64_t)S);  // ceil(2^32 / S)
 #pragma unroll
     for (int c = 0; c < kPlanChunks; ++c) {
+        if (c >= n_chunks) continue;  // (not break: the loop stays unrolled, bin_at(c) static)
         const int32_t bn = bin_at(c);
         const bool valid = bn > 0;
         uint64_t peers = __ballot(valid);
@@ -322,7 +329,8 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
             if (below == 0) s_h[wv][bn] = cnt + (uint32_t)__popcll(peers);
             const uint32_t pos = cnt + below;
             sorder[pos] = (int32_t)(lo + (int64_t)c * kWave + lane);
-            if (pos % S == 0) s_gs[pos / S] = (uint32_t)(S * (kPlanBins - 1 - bn));  // a group's first
+            const uint32_t grp = (uint32_t)(((uint64_t)pos * s_inv) >> 32);
+            if (pos == grp * (uint32_t)S) s_gs[grp] = (uint32_t)(S * (kPlanBins - 1 - bn));  // a group's first
         }
     }
     __syncthreads();
@@ -331,20 +339,23 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     const int64_t g0 = tid * gper, g1 = min<int64_t>(n_groups, g0 + gper);
     uint32_t gs = 0;
     for (int64_t g = g0; g < g1; ++g) gs += s_gs[g];
-    s_part[tid] = gs;
-    __syncthreads();
-    for (int d = 1; d < kT; d <<= 1) {
-        const uint32_t v = tid >= d ? s_part[tid - d] : 0u;
-        __syncthreads();
-        s_part[tid] += v;
-        __syncthreads();
+    // (a wave scan, then the 16 wave totals: 1 barrier instead of 20)
+    uint32_t inc = gs;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t t = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc += t;
     }
-    uint32_t gr = s_part[tid] - gs;
+    if (lane == kWave - 1) s_part[wv] = inc;
+    __syncthreads();
+    uint32_t wsum = 0;
+    for (int w = 0; w < wv; ++w) wsum += s_part[w];
+    uint32_t gr = wsum + inc - gs;
     for (int64_t g = g0; g < g1; ++g) {
         goff[g] = gr;
         gr += s_gs[g];
     }
-    if (tid == kT - 1) goff[n_groups] = s_part[kT - 1];
+    if (tid == kT - 1) goff[n_groups] = wsum + inc;
     if (tid == 0) *status = 0;
 }
 
