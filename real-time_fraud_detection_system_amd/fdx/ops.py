@@ -433,6 +433,9 @@ def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_da
     if len(windows_days) != W:
         raise FdxError("windows_days must have n_windows entries")
     dev, m = gts.device, plan.n_slots
+    if m > (64 // W) * max(gts.numel(), 1):  # every group pads to its longest segment: <= S slots per row
+        raise FdxError(f"customer layout: {m} slots for {gts.numel()} rows -- inconsistent segment offsets "
+                       "(keys outside [0, n_keys)?)")
     its = torch.empty(m, dtype=torch.int64, device=dev)
     iamt = torch.empty(m, dtype=torch.float64, device=dev)
     irow = torch.empty(m, dtype=torch.int32, device=dev)

@@ -200,11 +200,17 @@ class FraudPipeline:
                 mk("terminal_windows", side)
             for t in (ts_ns, customer, terminal, fraud) + ((bad,) if validate else ()):
                 t.record_stream(side)  # inputs in use on the side stream
-            if pending is not None:
-                lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
-            else:
-                lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
-                                          self.windows_days if walk else None, grouped=True)
+            try:
+                if pending is not None:
+                    lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
+                else:
+                    lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
+                                              self.windows_days if walk else None, grouped=True)
+            except _lib.FdxError:
+                if validate:  # ids outside the range are the likelier cause: report them
+                    for c in rc:
+                        c.check()
+                raise
             mk("customer_layout", main)
             self._slots_hint = lay.its.numel()
             self.last_slots = lay.n_slots

@@ -115,6 +115,14 @@ def test_fused_path_rejects_ids_out_of_range(dev):
     args = args[:1] + (T(d["customer"], torch.int32, dev), T(term, torch.int32, dev)) + args[3:]
     with pytest.raises(_lib.FdxError, match="terminal ids"):
         pipe.run_fused(*args, 300, 500, proba)
+    # ids past 2^key_bits (they sort among the in-range keys by their low bits, so the grouping
+    # is out of key order): still rejected, and no kernel reads outside its buffers meanwhile
+    for bad_id in (512 + 5, (1 << 30) + 7):  # low 9 bits: 5 and 7
+        cust = d["customer"].copy()
+        cust[n // 4 :: 97] = bad_id
+        args = args[:1] + (T(cust, torch.int32, dev), T(d["terminal"], torch.int32, dev)) + args[3:]
+        with pytest.raises(_lib.FdxError, match="customer ids"):
+            pipe.run_fused(*args, 300, 500, proba)
     # in range again: the same pipeline scores (nothing left over from the failed calls)
     args = args[:1] + (T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev)) + args[3:]
     pipe.run_fused(*args, 300, 500, proba)
