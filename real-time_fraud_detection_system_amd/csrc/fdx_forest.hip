@@ -1225,6 +1225,29 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
         rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w);
 }
 
+// rank_trees with the roots read once per launch (rp = root byte addresses, rn = root nodes,
+// dmax = the deepest of the trees): no scalar loads of root / depth per tile
+template <int R, int GG, int P16, int PIPE>
+__device__ __forceinline__ void rank_trees_from(const char *lds, const uint32_t (&lrow)[R], const uint32_t (&rp)[GG],
+                                                const uint32_t (&rn)[GG], int dmax, bool any_nan,
+                                                const uint8_t *__restrict__ ml, uint32_t (&pa)[R * GG],
+                                                const uint32_t (&w)[8]) {
+    constexpr int K = R * GG;
+    uint32_t lane_base[K], nd[K];
+#pragma unroll
+    for (int g = 0; g < GG; ++g)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            pa[r * GG + g] = rp[g];
+            nd[r * GG + g] = rn[g];
+            lane_base[r * GG + g] = lrow[r];
+        }
+    if (any_nan)
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml, w);
+    else
+        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w);
+}
+
 template <int K>
 __device__ __forceinline__ void rank_leaf_values(const uint32_t (&pa)[K], int64_t node_base,
                                                  const double *__restrict__ lval, double (&v)[K],
@@ -1358,6 +1381,129 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         }
     };
     if (base < r1) fetch(base);
+    // A chunk of at most G trees (every chunk of the bench forest: 5-6 trees of ~3.9k nodes per
+    // 94 KiB) is ONE walk group per tile, so the group pipeline below never runs and each tile
+    // waited for its leaf-value loads (and, last chunk, its output slots) right after its walk.
+    // Here a tile's leaf values are folded into its running sums one tile LATER -- after the next
+    // tile's walk -- and its output slots are loaded with its rank rows: no global load is
+    // waited on right after it is issued.  Same float64 additions in the same (tree) order.
+    auto one_group = [&](auto ntag) {
+        constexpr int NT = decltype(ntag)::value;
+        double pv[R * NT], ap[R];
+        int64_t rowp[R];
+        int32_t dstp[R], dst_n[R];
+        bool okp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ap[r] = 0.0;
+            rowp[r] = 0;
+            dstp[r] = -1;
+            okp[r] = false;
+#pragma unroll
+            for (int g = 0; g < NT; ++g) pv[r * NT + g] = 0.0;
+        }
+        uint32_t rp[NT], rn[NT];  // the chunk's roots, read once
+        int dmax = 0;
+#pragma unroll
+        for (int g = 0; g < NT; ++g) {
+            rp[g] = kNB + (uint32_t)(root[t0 + g] - node_base) * 4u;
+            rn[g] = lds32(lds, rp[g]);
+            dmax = max(dmax, depth[t0 + g]);
+        }
+        auto out_slot = [&](int64_t rw) -> int32_t {  // loaded here, used one tile later
+            return rw < r1 ? (last && out_perm ? out_perm[rw] : (int32_t)rw) : -1;
+        };
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst_n[r] = out_slot(base + r * BLOCK + tid);
+        auto fold = [&]() {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int g = 0; g < NT; ++g) ap[r] += pv[r * NT + g];
+                // formed before the store's branch: sunk into it, the wait for pv would land
+                // behind the store and cover the store too (vmcnt counts stores)
+                asm volatile("" ::"v"(ap[r]));
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!okp[r]) continue;
+                if (last) {
+                    if (dstp[r] >= 0) proba[dstp[r]] = ap[r] / (double)n_trees;  // < 0: padding slot
+                } else {
+                    acc[rowp[r]] = ap[r];
+                }
+            }
+        };
+        for (; base < r1; base += stride) {
+            int64_t row[R];
+            bool ok[R];
+            double a[R];
+            uint32_t w[8];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                row[r] = base + r * BLOCK + tid;
+                ok[r] = row[r] < r1;
+                if constexpr (P16 == 4) {
+                    w[0] = q0[r].x; w[1] = q0[r].y; w[2] = q0[r].z; w[3] = q0[r].w;
+                    w[4] = q1[r].x; w[5] = q1[r].y; w[6] = q1[r].z;
+                    w[7] = (q1[r].w & 0xFFFFu) | (kRankSentinel & 0xFFFF0000u);
+                } else if constexpr (P16 == 2) {
+                    const uint32_t w16[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
+                                              q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
+#pragma unroll
+                    for (int f = 0; f < 32; ++f)
+                        s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)((w16[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
+                } else {
+                    const uint32_t w8[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
+#pragma unroll
+                    for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
+                        const uint32_t u = (w8[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
+                        if (P16)
+                            s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
+                        else
+                            s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+                    }
+                }
+                a[r] = pacc[r];
+            }
+            int32_t dst[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) dst[r] = dst_n[r];
+            if (base + stride < r1) {
+                fetch(base + stride);
+#pragma unroll
+                for (int r = 0; r < R; ++r) dst_n[r] = out_slot(base + stride + r * BLOCK + tid);
+            }
+            uint32_t pt[R * NT];
+            rank_trees_from<R, NT, P16, PIPE>(lds, lrow, rp, rn, dmax, any_nan, ml, pt, w);
+            fold();  // the previous tile
+            rank_leaf_values<R * NT>(pt, node_base, lval, pv, kNB);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ap[r] = a[r];
+                rowp[r] = row[r];
+                dstp[r] = dst[r];
+                okp[r] = ok[r];
+            }
+        }
+        fold();
+    };
+    // (9+ trees, or register ranks: register spills)
+    if (P16 != 4 && !tv && !leaf_out && t1 - t0 <= (G < 8 ? G : 8) && r1 <= INT32_MAX) {
+#define FDX_ONE_GROUP(NT) \
+    if constexpr (G >= NT) \
+        if (t1 - t0 == NT) one_group(std::integral_constant<int, NT>{});
+        FDX_ONE_GROUP(1)
+        FDX_ONE_GROUP(2)
+        FDX_ONE_GROUP(3)
+        FDX_ONE_GROUP(4)
+        FDX_ONE_GROUP(5)
+        FDX_ONE_GROUP(6)
+        FDX_ONE_GROUP(7)
+        FDX_ONE_GROUP(8)
+#undef FDX_ONE_GROUP
+        return;
+    }
     for (; base < r1; base += stride) {
         int64_t row[R];
         bool ok[R];

@@ -1,0 +1,99 @@
+"""Forest chunks that are one walk group (<= 8 trees, every chunk of the bench forest): the tile
+loop folds a tile's leaf values one tile late and loads its output slots with its rank rows
+(k_forest_rank, one_group).  Probabilities must equal sklearn's (golden fixtures, the bench
+model's check rows), the C oracle's and the wide-layout kernel's bit for bit -- chunks of 1..8
+trees, several tiles per block (n past 256 x 1,024 rows), a ragged last tile, NaN rows (the
+missing_go_to_left walk) and the scoring-slot scatter of the fused path.
+Reference call: pyspark/scripts/fraud_detection.py:190-193 (predict_proba of the loaded model).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from fdx import ops
+from fdx._lib import FdxError
+from forest_gen import random_forest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VARIANTS = [1, 2, 3, 4, 5]  # v1 10 / 6 / 8 chains per lane, v2, compact v2
+
+
+def T(a, dt, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+
+
+def _arrays(z):
+    return {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+            for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+
+
+def _set(f, v):
+    try:
+        f.set_variant(v)
+    except FdxError:  # the variant's node format does not hold this forest
+        return False
+    return True
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_one_group_golden_fixtures(dev, golden, variant):
+    """sklearn's own probabilities (3- and 5-tree fixtures: one chunk), ~700k rows."""
+    for name in ("forest_rf3.npz", "forest_rf5d8.npz"):
+        z = golden(name)
+        f = ops.Forest(_arrays(z), 15, z["mean"], z["scale"])
+        if not _set(f, variant):
+            continue
+        reps = -(-700_001 // len(z["X"]))
+        X = np.vstack([z["X"]] * reps)
+        p = f.predict(T(X, torch.float64, dev)).cpu().numpy()
+        np.testing.assert_array_equal(p, np.concatenate([z["proba"]] * reps), err_msg=name)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("n_trees,depth", [(1, 12), (2, 9), (4, 10), (6, 11), (7, 11), (8, 10), (20, 12)])
+def test_one_group_random_forests_vs_oracle(dev, variant, n_trees, depth):
+    """Forests whose chunks hold 1..8 trees (20 deep trees: several chunks, the running sum
+    across launches), then the same rows with NaNs; n not a multiple of the tile."""
+    rng = np.random.default_rng(1000 * n_trees + depth)
+    arr = random_forest(rng, n_trees, depth, p_leaf=0.05)
+    f = ops.Forest(arr, 15)
+    if not _set(f, variant):
+        pytest.skip("node format does not hold this forest")
+    g = ops.Forest(arr, 15)
+    g.set_variant(0)  # the wide-layout kernel as the GPU reference
+    n = 700_001 + n_trees
+    X = rng.normal(size=(n, 15))
+    Xd = T(X, torch.float64, dev)
+    p = f.predict(Xd).cpu().numpy()
+    np.testing.assert_array_equal(p, g.predict(Xd).cpu().numpy())
+    sel = rng.choice(n, 20_000, replace=False)
+    np.testing.assert_array_equal(p[sel], oracle.forest_predict(X[sel], arr))
+    Xn = X.copy()
+    Xn[rng.random(Xn.shape) < 0.03] = np.nan
+    pn = f.predict(T(Xn, torch.float64, dev)).cpu().numpy()
+    np.testing.assert_array_equal(pn[sel], oracle.forest_predict(Xn[sel], arr))
+
+
+def test_one_group_bench_model(dev):
+    """The bench RF(100, depth 20), 18 chunks of 3-6 trees: 700k rows == the wide layout and the
+    oracle (sampled); the check rows == sklearn."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arr = _arrays(z)
+    f = ops.Forest(arr, 15, z["mean"], z["scale"])
+    assert f.n_chunks > 1
+    g = ops.Forest(arr, 15, z["mean"], z["scale"])
+    g.set_variant(0)
+    rng = np.random.default_rng(5)
+    X = np.vstack([z["check_X"]] * 171)
+    X = X * (1 + rng.normal(scale=0.05, size=X.shape) * (rng.random(X.shape) < 0.5))
+    Xd = T(X, torch.float64, dev)
+    p = f.predict(Xd).cpu().numpy()
+    np.testing.assert_array_equal(p, g.predict(Xd).cpu().numpy())
+    sel = rng.choice(len(X), 20_000, replace=False)
+    np.testing.assert_array_equal(p[sel], oracle.forest_predict(X[sel], arr, z["mean"], z["scale"]))
+    pc = f.predict(T(np.vstack([z["check_X"]] * 64), torch.float64, dev)).cpu().numpy()
+    np.testing.assert_array_equal(pc, np.concatenate([z["check_proba"]] * 64))
