@@ -10,3 +10,9 @@ timeout -k 10 400 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --swe
 grep -i "variant_sweep" $O/bench.err | tail -3 || true
 python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['traverse_ms'])"
 echo r03ay done
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/ktrace -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/$O/ktrace_bench.json 2> $GRAFT_REPO_ROOT/$O/ktrace.log
+cd $GRAFT_REPO_ROOT
+python3 tools/step_timeline.py $O/ktrace 2 > $O/timeline.txt
+grep forest $O/timeline.txt | head -20
+echo r03ay trace done
