@@ -932,7 +932,10 @@ __device__ __forceinline__ void walk_step(const uint64_t *s_nodes, const char *g
 // wave-uniform exit test between blocks (all chains of the wave at leaves).  In-distribution
 // rows of the bench forest end at ~5 nodes (depth 20), far-out rows run all 20 steps; testing
 // every kExitEvery steps keeps the test's cost small in the second case.
-constexpr int kExitEvery = 4;
+#ifndef FDX_EXIT_EVERY
+#define FDX_EXIT_EVERY 4
+#endif
+constexpr int kExitEvery = FDX_EXIT_EVERY;
 template <bool NAN_AWARE, bool LDS, int XSTRIDE, int K>
 __device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
                                            uint32_t (&p)[K], uint64_t (&nd)[K], int depth) {
