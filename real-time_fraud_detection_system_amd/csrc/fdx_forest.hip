@@ -1156,9 +1156,11 @@ __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
 // (Mixing the two -- 2 / 3 / 4 of 10 chains on register ranks, the rest on the planes -- was
 // measured too: 11.3 / 13.1 / 14.9 vs 7.6 ms at config 2, profiles/r03o_hybrid_chain_sweep.txt:
 // the walk's time follows its instruction count, whichever pipe the instructions use.)
+// `pre` steps run before the first exit test (the caller's estimate of the steps the wave will
+// need: extra steps at leaves are fixed points); returns the steps run (wave-uniform).
 template <int P16, int K, int PW>
-__device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                               uint32_t (&nd)[K], int depth, const uint32_t (&w)[8]) {
+__device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
+                                              uint32_t (&nd)[K], int depth, const uint32_t (&w)[8], int pre = 0) {
     auto fetch_x = [&](int k) -> uint32_t {
         if (P16 == 4) return reg_rank(w, nd[k]);
         return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
@@ -1191,15 +1193,20 @@ __device__ __forceinline__ void rank_walk_pipe(const char *lds, const uint32_t (
         }
     };
     int d = 0;
+    for (; d + kExitEvery <= pre; d += kExitEvery) {  // whole unrolled intervals, no test
+#pragma unroll
+        for (int e = 0; e < kExitEvery; ++e) step();
+    }
     for (; d + kExitEvery <= depth; d += kExitEvery) {
 #pragma unroll
         for (int e = 0; e < kExitEvery; ++e) step();
         uint32_t moving = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
-        if (!__any(moving != 0)) return;
+        if (!__any(moving != 0)) return d + kExitEvery;
     }
     for (; d < depth; ++d) step();
+    return d;
 }
 
 template <int R, int GG, int P16, int PIPE>
@@ -1231,10 +1238,10 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
 // rank_trees with the roots read once per launch (rp = root byte addresses, rn = root nodes,
 // dmax = the deepest of the trees): no scalar loads of root / depth per tile
 template <int R, int GG, int P16, int PIPE>
-__device__ __forceinline__ void rank_trees_from(const char *lds, const uint32_t (&lrow)[R], const uint32_t (&rp)[GG],
-                                                const uint32_t (&rn)[GG], int dmax, bool any_nan,
-                                                const uint8_t *__restrict__ ml, uint32_t (&pa)[R * GG],
-                                                const uint32_t (&w)[8]) {
+__device__ __forceinline__ int rank_trees_from(const char *lds, const uint32_t (&lrow)[R], const uint32_t (&rp)[GG],
+                                               const uint32_t (&rn)[GG], int dmax, bool any_nan,
+                                               const uint8_t *__restrict__ ml, uint32_t (&pa)[R * GG],
+                                               const uint32_t (&w)[8], int pre) {
     constexpr int K = R * GG;
     uint32_t lane_base[K], nd[K];
 #pragma unroll
@@ -1245,10 +1252,11 @@ __device__ __forceinline__ void rank_trees_from(const char *lds, const uint32_t 
             nd[r * GG + g] = rn[g];
             lane_base[r * GG + g] = lrow[r];
         }
-    if (any_nan)
+    if (any_nan) {
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml, w);
-    else
-        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w);
+        return 0;
+    }
+    return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w, pre);
 }
 
 template <int K>
@@ -1406,7 +1414,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             for (int g = 0; g < NT; ++g) pv[r * NT + g] = 0.0;
         }
         uint32_t rp[NT], rn[NT];  // the chunk's roots, read once
-        int dmax = 0;
+        int dmax = 0, pre = 0;
 #pragma unroll
         for (int g = 0; g < NT; ++g) {
             rp[g] = kNB + (uint32_t)(root[t0 + g] - node_base) * 4u;
@@ -1478,7 +1486,12 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 for (int r = 0; r < R; ++r) dst_n[r] = out_slot(base + stride + r * BLOCK + tid);
             }
             uint32_t pt[R * NT];
-            rank_trees_from<R, NT, P16, PIPE>(lds, lrow, rp, rn, dmax, any_nan, ml, pt, w);
+            // the previous tile's step count, less one exit interval, runs without exit tests
+            // (rows of the bench forest walk ~20 of 20 steps: 5 tests per tile otherwise); when
+            // the first test already found every chain at a leaf, the prefix shrinks by one more
+            // interval, so it follows shorter walks down
+            const int ran = rank_trees_from<R, NT, P16, PIPE>(lds, lrow, rp, rn, dmax, any_nan, ml, pt, w, pre);
+            pre = ran - (ran <= pre + kExitEvery ? 2 : 1) * kExitEvery;
             fold();  // the previous tile
             rank_leaf_values<R * NT>(pt, node_base, lval, pv, kNB);
 #pragma unroll
