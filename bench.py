@@ -4,17 +4,21 @@ A step = one pass of the hot path over one batch already resident in HBM:
   re-key by CUSTOMER_ID -> customer 1/7/30-day windows -> re-key by TERMINAL_ID ->
   terminal delayed-risk windows -> time flags + assemble the 15 input_features +
   StandardScaler -> RandomForest(100 trees, depth 20) predict_proba.
-Workload per GPU (BASELINE.json configs[1]): 50k customers / 100k terminals / 183 days
-(~17.7M tx), synthetic data from the handbook distributions generated on the GPU
-(fdx.synth.generate_device; no host generation inside the GPU lease), scored with the
-config-3 model (bench_assets/rf100_d20.npz, trained with sklearn on config-1 features).
+Workload (plan_workload):
+  N = 1: BASELINE.json configs[1] -- 50k customers / 100k terminals / 183 days (~17.7M tx);
+  N > 1: BASELINE.json configs[3] -- 1M customers / 2M terminals / 365 days (~700M tx) IN
+         TOTAL, strong scaling: rank r owns the contiguous CUSTOMER_ID range
+         [r * 1M / N, (r + 1) * 1M / N) and all its rows; the 2M terminals are one shared id
+         space (owner = id % N) whatever N is.
+Synthetic data from the handbook distributions generated on the GPU (fdx.synth.generate_device;
+no host generation inside the GPU lease), scored with the config-3 model
+(bench_assets/rf100_d20.npz, trained with sklearn on config-1 features).
 
 N GPUs: one process per GPU.  Launched by torch.distributed.run (RANK / WORLD_SIZE set) or,
 when `--gpus N > 1` is given without WORLD_SIZE, this script starts the N ranks itself
-(child processes, before anything touches the GPU) and exits with their status.  Weak
-scaling: each rank owns its own 50k customers (a contiguous CUSTOMER_ID range); terminals
-are shared ids hashed to owner ranks and the terminal half runs after an RCCL all-to-all
-re-key (fdx.distributed).  Rank 0 prints one JSON line.
+(child processes, before anything touches the GPU) and exits with their status.  The
+terminal half runs after an RCCL all-to-all re-key (fdx.distributed).  Rank 0 prints one
+JSON line.
 
 Per-kernel roofline: every stage of a step is bracketed by HIP events on
 the stream it runs on, inside the timed steps; the JSON line carries, per stage, the
@@ -106,9 +110,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--customers", type=int, default=50_000)
-    ap.add_argument("--terminals", type=int, default=100_000)
-    ap.add_argument("--days", type=int, default=183)
+    ap.add_argument("--workload", choices=("auto", "configs1", "configs3"), default="auto",
+                    help="auto: configs[1] per GPU at N = 1, configs[3] split over the ranks at N > 1")
+    ap.add_argument("--customers", type=int, default=None, help="override: customers (per GPU for configs1, "
+                                                                 "in total for configs3)")
+    ap.add_argument("--terminals", type=int, default=None, help="override: terminals (as --customers)")
+    ap.add_argument("--days", type=int, default=None)
     ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-score-rows", type=int, default=200_000,
@@ -117,8 +124,9 @@ def parse():
                     help="traversal kernel shape (fdx_forest_set_variant; -1 = the library default)")
     ap.add_argument("--avg-mode", choices=("exact", "scan"), default="exact",
                     help="customer averages: pandas-exact recurrence (default) or float64 prefix sums (SURVEY §7.4)")
-    ap.add_argument("--isolated-steps", type=int, default=3,
-                    help="extra untimed steps with every stage on one stream: per-kernel times for the roofline table")
+    ap.add_argument("--isolated-steps", type=int, default=5,
+                    help="extra steps after the timed region with every stage on one stream (one more untimed "
+                         "first): per-kernel times for the roofline table (median)")
     ap.add_argument("--sweep-variant", default="", help="comma list of forest variants to time (stderr)")
     ap.add_argument("--wide-records", action="store_true",
                     help="terminal count records in the 24-byte form (FraudPipeline(compact_records=False); "
@@ -126,6 +134,67 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
+
+
+# BASELINE.json configs: [1] = 50k / 100k / 183 days on one GPU, [3] = 1M / 2M / 365 days on 8
+WORKLOADS = {"configs1": (50_000, 100_000, 183), "configs3": (1_000_000, 2_000_000, 365)}
+
+
+def plan_workload(world, rank, workload="auto", customers=None, terminals=None, days=None):
+    """This rank's share of the bench workload.
+    configs1 (weak scaling, the N = 1 default): every rank owns its own `customers` customers
+      [rank * C, (rank + 1) * C) and the terminal id space grows to terminals * world;
+    configs3 (strong scaling, the N > 1 default): `customers` customers IN TOTAL, rank r owns
+      the contiguous range [r * C // world, (r + 1) * C // world); the terminal id space is
+      `terminals` whatever the world size.
+    -> dict(name, scaling, customer_base, n_customers_local, n_customers_total,
+            n_terminals_total, days)"""
+    name = workload if workload != "auto" else ("configs1" if world == 1 else "configs3")
+    c0, t0, d0 = WORKLOADS[name]
+    C = c0 if customers is None else int(customers)
+    T = t0 if terminals is None else int(terminals)
+    D = d0 if days is None else int(days)
+    if name == "configs1":
+        return {"name": name, "scaling": "weak", "customer_base": rank * C, "n_customers_local": C,
+                "n_customers_total": C * world, "n_terminals_total": T * world, "days": D}
+    lo, hi = rank * C // world, (rank + 1) * C // world
+    return {"name": name, "scaling": "strong", "customer_base": lo, "n_customers_local": hi - lo,
+            "n_customers_total": C, "n_terminals_total": T, "days": D}
+
+
+def median(v):
+    v = sorted(v)
+    m = len(v) // 2
+    return v[m] if len(v) % 2 else 0.5 * (v[m - 1] + v[m])
+
+
+# an isolated stage time (the stage alone on one stream) above this multiple of the same stage's
+# in-step time (beside the other stream's stages) cannot be a kernel time: it has absorbed
+# something else (an allocation, a cold pool) and the table falls back to the in-step time
+ISOLATED_MAX_OVER_IN_STEP = 2.0
+
+
+def stage_table(in_step, isolated, stages):
+    """Per-stage timing rows.  in_step / isolated: {stage: [ms per step]}; stages: the
+    (name, unit, kernels) list.  ms_in_step / ms_isolated are MEDIANS over the steps; `ms` (what
+    the rooflines use) is the isolated time unless it exceeds ISOLATED_MAX_OVER_IN_STEP x the
+    in-step time, in which case the isolated sample is rejected (kept as ms_isolated_rejected)."""
+    table = []
+    for name, unit, kernels in stages:
+        if name not in in_step:
+            continue
+        row = {"stage": name, "unit": unit, "ms_in_step": round(median(in_step[name]), 4)}
+        row["ms"] = row["ms_in_step"]
+        if isolated and name in isolated:
+            iso = round(median(isolated[name]), 4)
+            if iso > ISOLATED_MAX_OVER_IN_STEP * row["ms_in_step"]:
+                row["ms_isolated_rejected"] = iso
+            else:
+                row["ms_isolated"] = iso
+                row["ms"] = iso
+        row["kernels"] = [k for k, _ in kernels]
+        table.append(row)
+    return table
 
 
 def spawn_ranks(n):
@@ -306,14 +375,12 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
-    # weak scaling: rank r owns customers [r * C, (r + 1) * C) and adds its own terminals to
-    # one shared terminal map
-    base = rank * args.customers
+    wl = plan_workload(world, rank, args.workload, args.customers, args.terminals, args.days)
+    base, n_cl, n_terms = wl["customer_base"], wl["n_customers_local"], wl["n_terminals_total"]
     t_gen = time.perf_counter()
     # generated on the GPU (HIP Philox generator, csrc/fdx_synth.hip): the handbook
     # distributions of fdx.synth.generate, pinned by tests/test_gpu_synth.py; inputs resident
-    g = synth.generate_device(args.customers, args.terminals * world, args.days, seed=1234 + rank,
-                              customer_offset=base, device=dev)
+    g = synth.generate_device(n_cl, n_terms, wl["days"], seed=1234 + rank, customer_offset=base, device=dev)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
     n_local = g["ts"].numel()
@@ -355,8 +422,7 @@ def main():
     if world > 1 or args.sharded:
         from fdx.distributed import ShardedPipeline
 
-        sp = ShardedPipeline(pipe, world, rank, args.terminals * world, customer_base=base,
-                             n_customers_local=args.customers)
+        sp = ShardedPipeline(pipe, world, rank, n_terms, customer_base=base, n_customers_local=n_cl)
 
         def step(record):
             mark, marks = make_mark(record)
@@ -369,8 +435,7 @@ def main():
 
         def step(record, overlap=True, into=None):
             mark, marks = make_mark(record)
-            pipe.run_fused(ts, lcust, term, amt, fr, args.customers, args.terminals, proba, ws, mark=mark,
-                           overlap=overlap)
+            pipe.run_fused(ts, lcust, term, amt, fr, n_cl, n_terms, proba, ws, mark=mark, overlap=overlap)
             if record and into is not None:
                 into.append(marks)
             elif record:
@@ -403,6 +468,12 @@ def main():
 
     iso_all = []  # per-kernel times: every stage alone on the GPU (after the timed region)
     if marks_all and args.isolated_steps > 0 and not (world > 1 or args.sharded):
+        # one untimed step in this mode first: its buffers come from the caller stream's pool,
+        # which the overlapped steps (on the pipeline's own streams) never warmed -- the first
+        # such step absorbs that pool's allocations (BENCH_r03: 5.65 / 7.57 / 7.92 ms "isolated"
+        # stages of one cold step in a mean of 3)
+        step(False, overlap=False)
+        torch.cuda.synchronize()
         for _ in range(args.isolated_steps):
             step(True, overlap=False, into=iso_all)
         torch.cuda.synchronize()
@@ -433,14 +504,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
         "setup_s": {"generate_on_gpu": round(t_gen, 2)},
         "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234+rank), "
                 "resident in HBM",
-        "config": {"workload": f"configs[1]: {args.customers} customers / {args.terminals} terminals / "
-                               f"{args.days} days per GPU, featurize + RF(100 trees, depth 20) predict_proba",
+        "config": {"workload": (f"configs[1]: {n_cl} customers / {n_terms // world} terminals / {wl['days']} days "
+                                f"per GPU" if wl["name"] == "configs1" else
+                                f"configs[3]: {wl['n_customers_total']} customers / {n_terms} terminals / "
+                                f"{wl['days']} days in total, contiguous customer ranges over {world} GPU(s)")
+                               + ", featurize + RF(100 trees, depth 20) predict_proba",
+                   "customer_range": [base, base + n_cl],
                    "tx_per_gpu": n_local, "global_tx": n_total,
                    "parallelism": f"customer-sharded x{world}" + (" (RCCL all-to-all re-key)" if world > 1 else ""),
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)",
@@ -465,19 +540,11 @@ def main():
                            "measured_peak_source": "tools/lds_probe.hip (profiles/r02_lds_probe.txt): random "
                                                    "ds_read_b32, 32 independent reads in flight per lane"}
     if marks_all:
-        table = []
-        for name, unit, kernels in STAGES + EXCHANGE_STAGES:
-            if name not in marks_all[0]:
-                continue
-            ms = [mk[name][0].elapsed_time(mk[name][1]) for mk in marks_all]
-            t_ms = sum(ms) / len(ms)
-            row = {"stage": name, "unit": unit, "ms_in_step": round(t_ms, 4)}
-            if iso_all:
-                iso = [mk[name][0].elapsed_time(mk[name][1]) for mk in iso_all]
-                row["ms_isolated"] = round(sum(iso) / len(iso), 4)
-            row["ms"] = row.get("ms_isolated", row["ms_in_step"])
-            row.update({"kernels": [k for k, _ in kernels], "pmc_bytes": pmc_bytes(kernels)})
-            table.append(row)
+        ms_of = lambda steps: {name: [mk[name][0].elapsed_time(mk[name][1]) for mk in steps]  # noqa: E731
+                               for name in steps[0] if not name.startswith("_")}
+        table = stage_table(ms_of(marks_all), ms_of(iso_all) if iso_all else None, STAGES + EXCHANGE_STAGES)
+        for row in table:
+            row["pmc_bytes"] = pmc_bytes(next(k for n_, _, k in STAGES + EXCHANGE_STAGES if n_ == row["stage"]))
         # §8(d) units: K1-cust = layout + walk, K3 = assemble + traverse
         units = {}
         for row in table:
@@ -507,11 +574,14 @@ def main():
                           "streams": "rekey_terminal + terminal_windows run on a side stream, concurrently with the "
                                      "customer stages, so stage_sum_ms (of ms_in_step) exceeds ms_per_step by the "
                                      "overlap; ms = ms_isolated: the same stages in extra steps with every stage on "
-                                     "one stream (no concurrent kernel), the per-kernel durations the rooflines use",
+                                     "one stream (no concurrent kernel; median of --isolated-steps after one untimed step in "
+                                     "that mode), the per-kernel durations the rooflines use; an isolated time "
+                                     f"above {ISOLATED_MAX_OVER_IN_STEP}x the in-step time is rejected "
+                                     "(ms_isolated_rejected) and ms falls back to ms_in_step",
                           "end_to_end": {"alg_bytes_per_tx": ALG["end-to-end"], "achieved_GBs": round(e2e, 1),
                                          "time": "ms_per_step",
                                          "frac": round(e2e / HBM_PEAK_GBS, 4)},
-                          "note": "ms_in_step = HIP events around each stage on its stream, mean over the timed steps; "
+                          "note": "ms_in_step = HIP events around each stage on its stream, median over the timed steps; "
                                   "alg bytes = SURVEY.md §8(d) per tx x tx; pmc = rocprofv3 FETCH/WRITE per "
                                   "dispatch x dispatches (profiles/pmc_kernels.json)"}
     if marks_all and (world > 1 or args.sharded):
@@ -576,7 +646,7 @@ def main():
                 forest.set_variant(v)
                 pv = torch.empty_like(proba)
                 try:
-                    pipe.run_fused(ts, cust, term, amt, fr, args.customers, args.terminals, pv, ws)
+                    pipe.run_fused(ts, cust, term, amt, fr, n_cl, n_terms, pv, ws)
                 except _lib.FdxError as e:  # e.g. a 32-slot v2 variant: the fused rows are v1-format only
                     res[v] = {"skipped": str(e)}
                     continue

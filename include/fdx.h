@@ -424,17 +424,14 @@ int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t 
                        int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
                         void *workspace_d, size_t workspace_bytes, void *stream);
-/* Traversal kernel shape (one default per layout; 4-10 exist for the walk-shape study of
- * DESIGN.md §4):
+/* Traversal kernel shape (one default per layout):
  *   0 = wide layout (8-byte nodes, float32 rows; any forest, the only one for > 15 features),
  *   1 = rank layout v1, 1,024 threads x 10 trees per lane (the default when the forest fits v1),
  *   2 = rank layout v2, 32 threshold slots (the default for forests v1 cannot hold),
  *   3 = v2 nodes over 16 compact u16 planes (every feature in one slot),
- *   4 / 5 = v1 with 6 / 8 trees per lane, 6 = v1 10 trees with waits grouped by 5 chains,
- *   7 = v1 9 trees (groups of 3), 8 = v2 with 10 trees, 9 = compact v2 with 10 trees,
- *   10 = v1 nodes with the rank row in registers (no LDS row planes: one LDS read per step,
- *   the whole LDS for nodes), 8 trees per lane -- measured 2.1x slower than 1.
- * Variants > 0 need <= 15 features and the rank layout (FDX_E_UNSUPPORTED otherwise).
+ *   4 = rank layout v2 with 10 trees per lane.
+ * Variants > 0 need <= 15 features and the rank layout (FDX_E_UNSUPPORTED otherwise; a
+ * refused call leaves the forest's node format, variant and chunks as they were).
  * Re-cuts the LDS chunks; results are identical for every variant.  The row format of a
  * prepared workspace depends on the layout: prepare again after switching layouts. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);

@@ -871,8 +871,7 @@ __device__ __forceinline__ uint64_t node_at(const uint64_t *s_nodes, const char 
 // per lane, G trees walked at once per lane (G independent LDS dependency chains), the
 // software-pipelined walk with waits grouped by PIPE chains.  p16 = the rank node / plane
 // format: 0 = v1 (u32 planes), 2 = v2 (32 threshold slots over u16 planes), 3 = v2 nodes over
-// 16 u16 planes (forests whose every feature fits one slot), 4 = v1 nodes, no planes: the
-// lane's rank row stays in VGPRs (see reg_rank).
+// 16 u16 planes (forests whose every feature fits one slot).
 struct Variant {
     int block, rows, group, rank, p16, pipe;
 };
@@ -882,16 +881,11 @@ constexpr Variant kVariants[] = {
                              //    8.43 ms for 6 chains at config 2; 12 chains spill, 11.7 ms)
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
-    {1024, 1, 6, 1, 0, 2},   // 4: v1, 6 chains (the r01/r02 default, fastest of 57 shapes then)
-    {1024, 1, 8, 1, 0, 2},   // 5-7: v1 chain / wait-group study
-    {1024, 1, 10, 1, 0, 5},
-    {1024, 1, 9, 1, 0, 3},
-    {1024, 1, 10, 1, 2, 2},  // 8: v2, 10 chains
-    {1024, 1, 10, 1, 3, 2},  // 9: compact v2, 10 chains
-    {1024, 1, 8, 1, 4, 2},   // 10: v1 nodes, register ranks (one ds_read per step, 10 LDS chunks instead of
-                             //     18): bit-exact, 16.3 vs 7.6 ms at config 2 (r03f; 6 and 9 chains the
-                             //     same, 10 spill) -- the 11-VALU feature select outweighs the LDS read
+    {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
 };
+// (Round 3 also measured v1 with 6 / 8 / 9 chains, compact v2 with 10 chains and register
+// ranks -- the lane's rank row in 8 VGPRs, one ds_read per step: 16.3 vs 7.6 ms -- and removed
+// them; DESIGN.md §4 keeps their numbers.)
 constexpr int kDefaultRankVariant = 1;
 constexpr int kDefaultRankV2Variant = 2;
 constexpr int kDefaultRankCompactVariant = 3;
@@ -1068,46 +1062,17 @@ constexpr uint32_t kOffMask = (P16 == 2 || P16 == 3) ? 0x7FFu : 0xFFFu;
 // 3 = the v2 node format over 16 u16 planes of 1,024 rows (32 KiB): forests whose every feature
 // fits one slot (slot = feature, the v1 row format); the node region starts at 32 KiB, so a
 // chunk holds a third more nodes than with 64 KiB of planes (fewer chunk launches per batch)
-// 4 = register ranks: no planes, the node region is the whole LDS
 template <int P16>
-constexpr uint32_t kNodeB = P16 == 3 ? 32768u : P16 == 4 ? 0u : kRankNodeB;
-
-// P16 == 4: the lane's rank row -- 16 u16 ranks in 8 VGPRs, slot 15 = the v1 sentinel 0x4000 --
-// replaces the LDS row planes, so a step reads only its node.  The node's feature f (bits
-// [15:12] of s, the XORed node) is selected in registers: v_perm_b32 takes u16 f & 3 out of
-// each of the four VGPR pairs (selector bytes 2j, 2j + 1; the high bytes 0x0C give zeros),
-// then two v_bfi_b32 levels pick the pair by f >> 2 (masks = bits 14 and 15 of s
-// sign-extended).  11 VALU in place of one ds_read_b32 and its address op.
-__device__ __forceinline__ uint32_t reg_rank(const uint32_t (&w)[8], uint32_t s) {
-    const uint32_t sel = __builtin_amdgcn_ubfe(s, 12, 2) * 0x0202u + 0x0C0C0100u;
-    const uint32_t p0 = __builtin_amdgcn_perm(w[1], w[0], sel);
-    const uint32_t p1 = __builtin_amdgcn_perm(w[3], w[2], sel);
-    const uint32_t p2 = __builtin_amdgcn_perm(w[5], w[4], sel);
-    const uint32_t p3 = __builtin_amdgcn_perm(w[7], w[6], sel);
-    // one asm block: in C the compiler turns the 0 / -1 masks into v_cmp + v_cndmask through
-    // VCC (two more VALU and an s_nop per level), and around separate asm statements it pads
-    // with s_nop
-    uint32_t m, a, b, x;
-    asm("v_bfe_i32 %[m], %[s], 14, 1\n\t"
-        "v_bfi_b32 %[a], %[m], %[p1], %[p0]\n\t"
-        "v_bfi_b32 %[b], %[m], %[p3], %[p2]\n\t"
-        "v_bfe_i32 %[m], %[s], 15, 1\n\t"
-        "v_bfi_b32 %[x], %[m], %[b], %[a]"
-        : [m] "=&v"(m), [a] "=&v"(a), [b] "=&v"(b), [x] "=&v"(x)
-        : [s] "v"(s), [p0] "v"(p0), [p1] "v"(p1), [p2] "v"(p2), [p3] "v"(p3));
-    return x;
-}
+constexpr uint32_t kNodeB = P16 == 3 ? 32768u : kRankNodeB;
 
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                          uint32_t (&nd)[K], const uint8_t *__restrict__ mleft,
-                                          const uint32_t (&w)[8]) {
+                                          uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        x[k] = P16 == 4 ? reg_rank(w, nd[k])
-               : P16    ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
-                        : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+        x[k] = P16 ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
+                   : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint32_t st;
@@ -1125,18 +1090,17 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
 
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                          uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft,
-                                          const uint32_t (&w)[8]) {
+                                          uint32_t (&nd)[K], int depth, const uint8_t *__restrict__ mleft) {
     int d = 0;
     for (; d + kExitEvery <= depth; d += kExitEvery) {
 #pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft, w);
+        for (int e = 0; e < kExitEvery; ++e) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
         uint32_t moving = 0;  // leaves (and only leaves) have right offset 0
 #pragma unroll
         for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
         if (!__any(moving != 0)) return;
     }
-    for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft, w);
+    for (; d < depth; ++d) rank_step<NAN_AWARE, P16, K>(lds, lane_base, pa, nd, mleft);
 }
 
 // Walk trees [t, t+GG) for the R rows of this lane (chain k = r*GG + g); pa = final leaves.
@@ -1153,18 +1117,12 @@ __device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
 // and its feature reads in forward order, so the first use in each group waits for the
 // group's last-issued read and one s_waitcnt covers the whole group (LDS reads of a wave
 // return in order): fewer issue slots per step.
-// (Mixing the two -- 2 / 3 / 4 of 10 chains on register ranks, the rest on the planes -- was
-// measured too: 11.3 / 13.1 / 14.9 vs 7.6 ms at config 2, profiles/r03o_hybrid_chain_sweep.txt:
-// the walk's time follows its instruction count, whichever pipe the instructions use.)
 // `pre` steps run before the first exit test (the caller's estimate of the steps the wave will
 // need: extra steps at leaves are fixed points); returns the steps run (wave-uniform).
 template <int P16, int K, int PW>
 __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
-                                              uint32_t (&nd)[K], int depth, const uint32_t (&w)[8], int pre = 0) {
-    auto fetch_x = [&](int k) -> uint32_t {
-        if (P16 == 4) return reg_rank(w, nd[k]);
-        return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
-    };
+                                              uint32_t (&nd)[K], int depth, int pre = 0) {
+    auto fetch_x = [&](int k) -> uint32_t { return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]); };
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
@@ -1189,7 +1147,7 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             x[k] = fetch_x(k);
-            if (P16 != 4) __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     int d = 0;
@@ -1213,7 +1171,7 @@ template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
                                            int64_t node_base, bool any_nan, const uint8_t *__restrict__ ml,
-                                           uint32_t (&pa)[R * GG], const uint32_t (&w)[8]) {
+                                           uint32_t (&pa)[R * GG]) {
     constexpr int K = R * GG;
     uint32_t lane_base[K], nd[K];
     int dmax = 0;
@@ -1230,9 +1188,9 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
         }
     }
     if (any_nan)
-        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml, w);
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
     else
-        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w);
+        rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
 }
 
 // rank_trees with the roots read once per launch (rp = root byte addresses, rn = root nodes,
@@ -1240,8 +1198,7 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
 template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ int rank_trees_from(const char *lds, const uint32_t (&lrow)[R], const uint32_t (&rp)[GG],
                                                const uint32_t (&rn)[GG], int dmax, bool any_nan,
-                                               const uint8_t *__restrict__ ml, uint32_t (&pa)[R * GG],
-                                               const uint32_t (&w)[8], int pre) {
+                                               const uint8_t *__restrict__ ml, uint32_t (&pa)[R * GG], int pre) {
     constexpr int K = R * GG;
     uint32_t lane_base[K], nd[K];
 #pragma unroll
@@ -1253,10 +1210,10 @@ __device__ __forceinline__ int rank_trees_from(const char *lds, const uint32_t (
             lane_base[r * GG + g] = lrow[r];
         }
     if (any_nan) {
-        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml, w);
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
         return 0;
     }
-    return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, w, pre);
+    return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, pre);
 }
 
 template <int K>
@@ -1337,8 +1294,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots
     constexpr int kPlaneRows = kRankPlaneRows;
     constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
-    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : P16 == 4 ? 0 : kRankXWords;  // row-plane words in LDS
-    static_assert(P16 != 4 || R == 1, "register ranks: one row per lane");
+    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS
     constexpr uint32_t kNB = kNodeB<P16>;
     if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
         const int c = blockIdx.y;
@@ -1349,7 +1305,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         first = 1;
         last = 0;
     }
-    static_assert(P16 == 4 || BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
+    static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
@@ -1449,16 +1405,11 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             int64_t row[R];
             bool ok[R];
             double a[R];
-            uint32_t w[8];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 row[r] = base + r * BLOCK + tid;
                 ok[r] = row[r] < r1;
-                if constexpr (P16 == 4) {
-                    w[0] = q0[r].x; w[1] = q0[r].y; w[2] = q0[r].z; w[3] = q0[r].w;
-                    w[4] = q1[r].x; w[5] = q1[r].y; w[6] = q1[r].z;
-                    w[7] = (q1[r].w & 0xFFFFu) | (kRankSentinel & 0xFFFF0000u);
-                } else if constexpr (P16 == 2) {
+                if constexpr (P16 == 2) {
                     const uint32_t w16[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                               q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
@@ -1490,7 +1441,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             // (rows of the bench forest walk ~20 of 20 steps: 5 tests per tile otherwise); when
             // the first test already found every chain at a leaf, the prefix shrinks by one more
             // interval, so it follows shorter walks down
-            const int ran = rank_trees_from<R, NT, P16, PIPE>(lds, lrow, rp, rn, dmax, any_nan, ml, pt, w, pre);
+            const int ran = rank_trees_from<R, NT, P16, PIPE>(lds, lrow, rp, rn, dmax, any_nan, ml, pt, pre);
             pre = ran - (ran <= pre + kExitEvery ? 2 : 1) * kExitEvery;
             fold();  // the previous tile
             rank_leaf_values<R * NT>(pt, node_base, lval, pv, kNB);
@@ -1504,8 +1455,8 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         }
         fold();
     };
-    // (9+ trees, or register ranks: register spills)
-    if (P16 != 4 && !tv && !leaf_out && t1 - t0 <= (G < 8 ? G : 8) && r1 <= INT32_MAX) {
+    // (9+ trees: register spills)
+    if (!tv && !leaf_out && t1 - t0 <= (G < 8 ? G : 8) && r1 <= INT32_MAX) {
 #define FDX_ONE_GROUP(NT) \
     if constexpr (G >= NT) \
         if (t1 - t0 == NT) one_group(std::integral_constant<int, NT>{});
@@ -1524,16 +1475,11 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         int64_t row[R];
         bool ok[R];
         double a[R];
-        uint32_t w[8];  // P16 == 4: the lane's rank row, slot 15 = the sentinel
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             row[r] = base + r * BLOCK + tid;
             ok[r] = row[r] < r1;
-            if constexpr (P16 == 4) {
-                w[0] = q0[r].x; w[1] = q0[r].y; w[2] = q0[r].z; w[3] = q0[r].w;
-                w[4] = q1[r].x; w[5] = q1[r].y; w[6] = q1[r].z;
-                w[7] = (q1[r].w & 0xFFFFu) | (kRankSentinel & 0xFFFF0000u);
-            } else if constexpr (P16 == 2) {
+            if constexpr (P16 == 2) {
                 const uint32_t w[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                         q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
@@ -1558,7 +1504,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         int t = t0;
         for (; t + G <= t1; t += G) {
             uint32_t pa[K];
-            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa, w);
+            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
             if (pending) rank_accumulate<R, G>(a, pv);
             rank_leaf_values<K>(pa, node_base, lval, pv, kNB);
             if (tv) rank_tree_values<R, G>(pv, t, row, ok, tv, tv_n);
@@ -1571,7 +1517,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         if (nt == NT) {                                                                                    \
             uint32_t pt[R * NT];                                                                           \
             double vt[R * NT];                                                                             \
-            rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt, w);        \
+            rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);           \
             if (pending) rank_accumulate<R, G>(a, pv);                                                     \
             pending = false;                                                                               \
             rank_leaf_values<R * NT>(pt, node_base, lval, vt, kNB);                                        \
@@ -1589,8 +1535,6 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         FDX_RANK_TAIL(7)
         FDX_RANK_TAIL(8)
         FDX_RANK_TAIL(9)
-        FDX_RANK_TAIL(10)
-        FDX_RANK_TAIL(11)
 #undef FDX_RANK_TAIL
         if (pending) rank_accumulate<R, G>(a, pv);
         if (tv) continue;
@@ -1900,7 +1844,6 @@ int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
 constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
-constexpr int64_t kRankNodeCapReg = kLdsTotal / 4 - 1;  // register ranks: no planes
 
 bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; }
 
@@ -1909,7 +1852,7 @@ bool rank_mode(const fdx_forest_s *F) { return kVariants[F->variant].rank != 0; 
 // (wide layout only: a rank-layout forest has every tree within the budget by construction).
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
-    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : v.p16 == 4 ? kRankNodeCapReg : kRankNodeCap)
+    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
                                      : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
@@ -1954,36 +1897,34 @@ int upload_chunks(fdx_forest_s *F) {
 extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(variant >= 0 && variant < kNumVariants, "variant must be in [0, %d)", kNumVariants);
-    FDX_REQUIRE(variant == 0 || F->zstride == 16, "variants > 0 need <= 16 features");
-    if (kVariants[variant].rank && !F->rank_ok) {
+    FDX_REQUIRE(variant == 0 || F->zstride == 16, "variants > 0 need <= 15 features");
+    const Variant &v = kVariants[variant];
+    if (v.rank && !F->rank_ok) {
         set_error("variant %d needs the rank layout, which this forest does not fit", variant);
         return FDX_E_UNSUPPORTED;
     }
-    if (kVariants[variant].rank && variant_format(kVariants[variant]) != forest_format(F)) {
-        // the variant runs on another node format: rebuild the rank layout in it
-        const int want = variant_format(kVariants[variant]), had = forest_format(F);
-        int rc = install_rank_layout(F, want == 2, nullptr);
-        if (rc) {
-            install_rank_layout(F, had == 2, nullptr);  // restore the previous format
-            set_error("variant %d needs rank layout v%d, which this forest does not fit", variant, want);
-            return FDX_E_UNSUPPORTED;
-        }
-    }
-    if (kVariants[variant].rank && kVariants[variant].p16 == 3 && !F->rank_identity) {
-        set_error("variant %d needs one threshold slot per feature (<= 16 slots)", variant);
+    const int prev = F->variant, had = forest_format(F);
+    // every failure below leaves the forest exactly as it was: the previous node format (the
+    // rank layout is rebuilt in it when it was switched), the previous variant and its chunks
+    auto refuse = [&](const char *why, int a) {
+        if (forest_format(F) != had) install_rank_layout(F, had == 2, nullptr);
+        F->variant = prev;
+        build_chunks(F);
+        upload_chunks(F);
+        set_error(why, variant, a);
         return FDX_E_UNSUPPORTED;
+    };
+    if (v.rank && variant_format(v) != had) {  // the variant runs on the other node format
+        if (install_rank_layout(F, variant_format(v) == 2, nullptr))
+            return refuse("variant %d needs rank layout v%d, which this forest does not fit", variant_format(v));
     }
-    const int prev = F->variant;
+    if (v.rank && v.p16 == 3 && !F->rank_identity)
+        return refuse("variant %d needs one threshold slot per feature (<= %d slots)", 16);
     F->variant = variant;
     build_chunks(F);
     bool rank_fits = true;  // a rank kernel walks LDS-resident chunks only
     for (const auto &c : F->chunks) rank_fits = rank_fits && c.in_lds;
-    if (kVariants[variant].rank && !rank_fits) {
-        F->variant = prev;
-        build_chunks(F);
-        set_error("variant %d: a tree does not fit its LDS node budget", variant);
-        return FDX_E_UNSUPPORTED;
-    }
+    if (v.rank && !rank_fits) return refuse("variant %d: a tree does not fit its LDS node budget", 0);
     return upload_chunks(F);
 }
 
@@ -2507,13 +2448,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             switch (F->variant) {
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
-                case 4: FDX_LAUNCH_RANK(1024, 1, 6, 0, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 8, 0, 2); break;
-                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 0, 5); break;
-                case 7: FDX_LAUNCH_RANK(1024, 1, 9, 0, 3); break;
-                case 8: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                case 9: FDX_LAUNCH_RANK(1024, 1, 10, 3, 2); break;
-                case 10: FDX_LAUNCH_RANK(1024, 1, 8, 4, 2); break;
+                case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -50,3 +50,52 @@ def test_sklearn_forest_rebuilt_from_arrays_matches_saved_output():
 def test_host_info_fields():
     info = _bench().host_info()
     assert info["nproc"] >= 1 and info["affinity_cpus"] >= 1 and info["joblib_cpus"] >= 1
+
+
+def test_plan_workload_configs1_at_one_gpu():
+    b = _bench()
+    w = b.plan_workload(1, 0)
+    assert w["name"] == "configs1" and w["scaling"] == "weak"
+    assert (w["customer_base"], w["n_customers_local"], w["n_terminals_total"], w["days"]) == (0, 50_000, 100_000, 183)
+
+
+def test_plan_workload_configs3_strong_scaling_over_8_ranks():
+    """bench.py --gpus 8 runs BASELINE.json configs[3]: 1M customers / 2M terminals / 365 days in
+    total, contiguous customer ranges, the terminal id space independent of N."""
+    b = _bench()
+    for world in (2, 4, 8):
+        plans = [b.plan_workload(world, r) for r in range(world)]
+        assert all(p["name"] == "configs3" and p["scaling"] == "strong" for p in plans)
+        assert all(p["n_terminals_total"] == 2_000_000 and p["days"] == 365 for p in plans)
+        assert plans[0]["customer_base"] == 0
+        for a, c in zip(plans, plans[1:]):
+            assert a["customer_base"] + a["n_customers_local"] == c["customer_base"]
+        assert sum(p["n_customers_local"] for p in plans) == 1_000_000
+    p8 = [b.plan_workload(8, r) for r in range(8)]
+    assert [(p["customer_base"], p["n_customers_local"]) for p in p8] == [(r * 125_000, 125_000) for r in range(8)]
+
+
+def test_stage_table_medians_and_rejects_inflated_isolated_times():
+    """An isolated stage time more than 2x its in-step time (BENCH_r03: one cold step of 15-21 ms
+    folded into a mean of 3) is rejected: the roofline uses the in-step median instead."""
+    b = _bench()
+    stages = [("rekey_customer", "K2", []), ("customer_walk", "K1-cust", []), ("forest_traverse", "K3", [])]
+    in_step = {"rekey_customer": [0.9, 0.95, 1.0], "customer_walk": [1.0, 1.0, 1.1], "forest_traverse": [7.2, 7.1, 7.3]}
+    iso = {"rekey_customer": [0.58, 15.9, 0.59], "customer_walk": [21.0, 22.0, 0.75], "forest_traverse": [7.0, 7.1, 7.2]}
+    rows = {r["stage"]: r for r in b.stage_table(in_step, iso, stages)}
+    assert rows["rekey_customer"]["ms"] == 0.59 and rows["rekey_customer"]["ms_isolated"] == 0.59  # median
+    assert "ms_isolated" not in rows["customer_walk"]
+    assert rows["customer_walk"]["ms_isolated_rejected"] == 21.0
+    assert rows["customer_walk"]["ms"] == rows["customer_walk"]["ms_in_step"] == 1.0
+    assert rows["forest_traverse"]["ms"] == 7.1
+    assert b.stage_table(in_step, None, stages)[0]["ms"] == 0.95
+
+
+def test_bench_stream_splits_configs4_state_over_ranks():
+    """bench_stream.py --gpus N: the 1M / 2M-key state of configs[4] split over the ranks."""
+    import re
+
+    src = open(os.path.join(ROOT, "bench_stream.py")).read()
+    assert re.search(r'"--customers", type=int, default=1_000_000', src)
+    assert re.search(r'"--terminals", type=int, default=2_000_000', src)
+    assert "n_c = args.customers // world" in src and "configs[4]" in src

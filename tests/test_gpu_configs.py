@@ -214,10 +214,13 @@ def test_deployed_model_rank_layout_v2(dev):
     np.testing.assert_array_equal(got, z["test_proba1"][idx])
 
 
-def test_config4_one_rank_shard(dev):
-    """configs[3] (1M customers / 2M terminals / 365 days, 8 GPUs) as ONE rank sees it: rank
-    3 of 8 owns customers [375000, 500000) and all their rows (~90M tx; the terminal ids range
-    over all 2M).  The sharded path (world 1 process group: its re-key exchange, owner-side
+@pytest.mark.parametrize("base,n_c", [(375_000, 125_000), (0, 500_000)], ids=["rank3of8", "rank0of2"])
+def test_config4_one_rank_shard(dev, base, n_c):
+    """configs[3] (1M customers / 2M terminals / 365 days) as ONE rank sees it: rank 3 of 8
+    owns customers [375000, 500000) and all their rows (~88M tx; the terminal ids range over
+    all 2M); rank 0 of 2 (bench.py --gpus 2, strong scaling) owns [0, 500000), ~350M tx --
+    every 8-byte column and the 32-byte scoring rows then span more than 2^31 bytes, so any
+    32-bit offset arithmetic in a kernel would show here.  The sharded path (world 1 process group: its re-key exchange, owner-side
     records and reply assembly run through RCCL to self) must give the probabilities of the
     single-GPU fused path on the re-based ids on every row, and the sampled customers' and
     terminals' features must equal the C oracle's."""
@@ -227,12 +230,12 @@ def test_config4_one_rank_shard(dev):
 
     from fdx.distributed import ShardedPipeline
 
-    base, n_c, n_t = 375_000, 125_000, 2_000_000
+    n_t = 2_000_000
     arrays, z = _model()
     forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
     g = synth.generate_device(n_c, n_t, 365, seed=77, customer_offset=base, device=dev)
     n = g["ts"].numel()
-    assert n > 60_000_000
+    assert n > 480 * n_c
     args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
     pipe = FraudPipeline(forest=forest)
     ws = ops.workspace(forest.workspace_size(n * 11 // 10), dev)

@@ -19,7 +19,7 @@ from forest_gen import random_forest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = [1, 2, 3, 4, 5]  # v1 10 / 6 / 8 chains per lane, v2, compact v2
+VARIANTS = [1, 2, 3, 4]  # v1 (10 chains per lane), v2 (6), compact v2 (6), v2 (10)
 
 
 def T(a, dt, dev):
@@ -97,3 +97,27 @@ def test_one_group_bench_model(dev):
     np.testing.assert_array_equal(p[sel], oracle.forest_predict(X[sel], arr, z["mean"], z["scale"]))
     pc = f.predict(T(np.vstack([z["check_X"]] * 64), torch.float64, dev)).cpu().numpy()
     np.testing.assert_array_equal(pc, np.concatenate([z["check_proba"]] * 64))
+
+
+def test_refused_variant_leaves_the_forest_intact(dev):
+    """a refused set_variant must leave the forest as it was.  The deployed model
+    (rank layout v2, 22 threshold slots) cannot run v1 (a feature has 96k thresholds: the v1
+    rebuild fails after the v2 buffers were freed) nor compact v2 (more slots than features);
+    after each refusal the forest is back in v2 with its variant and chunks, and predict is
+    still sklearn's on the notebook's test rows."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf_deployed.npz"))
+    f = ops.Forest(_arrays(z), 15, z["mean"], z["scale"])
+    v0, nc0 = f.variant, f.n_chunks
+    assert v0 == 2
+    X = T(z["test_X"][:20_000], torch.float64, dev)
+    want = z["test_proba1"][:20_000]
+    for bad in (1, 3, 1):
+        with pytest.raises(FdxError):
+            f.set_variant(bad)
+        assert f.variant == v0
+        np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+    f.set_variant(4)
+    np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+    f.set_variant(2)
+    assert f.n_chunks == nc0
+    np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
