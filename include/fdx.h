@@ -273,6 +273,13 @@ int fdx_rekey_payload_checked(const int32_t *keys_d, int64_t n, int32_t key_bits
 size_t fdx_argsort_i64_workspace_size(int64_t n);
 int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d, void *workspace_d,
                     size_t workspace_bytes, void *stream);
+/* Dense ids of arbitrary int64 keys, order-preserving: ids_d[i] = the rank of keys_d[i] among
+ * the distinct keys (0-based), *n_unique_d (device int64) = the number of distinct keys --
+ * what pandas' groupby does with ids that are not dense in [0, n) (the drop-in's sparse-id
+ * path; feature_transformation.ipynb:1092, :2435).  Sort-based (fdx_argsort_i64), no host sync. */
+size_t fdx_dense_ids_i64_workspace_size(int64_t n);
+int fdx_dense_ids_i64(const int64_t *keys_d, int64_t n, int32_t *ids_d, int64_t *n_unique_d, void *workspace_d,
+                      size_t workspace_bytes, void *stream);
 /* *flag_d = 1 if keys_d is non-decreasing, else 0 (stream-ordered). */
 int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream);
 

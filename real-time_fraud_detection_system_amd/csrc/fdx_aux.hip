@@ -417,7 +417,9 @@ extern "C" size_t fdx_dedup_latest_workspace_size(int64_t n) {
 
 extern "C" int fdx_dedup_latest(const int64_t *key_d, const int64_t *kafka_ts_d, int64_t n, uint8_t *keep_d,
                                 int32_t *bad_d, void *workspace_d, size_t workspace_bytes, void *stream) {
-    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    // hash slots are stored as int32 (negative = no slot) and the table holds up to 2n+ slots:
+    // n <= 2^30 keeps every slot index below 2^31
+    FDX_REQUIRE(n >= 0 && n <= (int64_t(1) << 30), "n out of range (dedup batches hold at most 2^30 records)");
     if (n == 0) return FDX_OK;
     FDX_REQUIRE(key_d && kafka_ts_d && keep_d && bad_d, "null pointer");
     const size_t need = fdx_dedup_latest_workspace_size(n);

@@ -770,6 +770,72 @@ extern "C" int fdx_argsort_i64(const int64_t *keys_d, int64_t n, int32_t *perm_d
                                 reinterpret_cast<uint32_t *>(perm_d), w, as_stream(stream), &sorted);
 }
 
+// ---- dense ids of arbitrary int64 keys (the drop-ins' groupby on ids that are not dense) ----
+// flags[i] = 1 where the sorted key differs from its predecessor (sorted = sign-flipped u64)
+__global__ void k_new_key_flags(const uint64_t *__restrict__ sorted, int64_t n, uint32_t *__restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        flags[i] = i > 0 && sorted[i] != sorted[i - 1];
+}
+// ids[perm[i]] = #distinct keys among sorted[0..i] - 1 (= exclusive count + own flag)
+__global__ void k_dense_scatter(const uint64_t *__restrict__ sorted, const uint32_t *__restrict__ excl,
+                                const int32_t *__restrict__ perm, int64_t n, int32_t *__restrict__ ids,
+                                int64_t *__restrict__ n_unique) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = (int32_t)(excl[i] + (i > 0 && sorted[i] != sorted[i - 1] ? 1u : 0u));
+        ids[perm[i]] = r;
+        if (i == n - 1) *n_unique = (int64_t)r + 1;
+    }
+}
+
+static size_t dense_ids_parts(int64_t n, size_t *off_perm, size_t *off_flags, size_t *off_scan) {
+    const size_t a = align_up(sort_ws<uint64_t>(n, nullptr, nullptr));
+    const size_t b = align_up(sizeof(int32_t) * (size_t)n);
+    const size_t c = align_up(sizeof(uint32_t) * (size_t)n);
+    if (off_perm) *off_perm = a;
+    if (off_flags) *off_flags = a + b;
+    if (off_scan) *off_scan = a + b + c;
+    return a + b + c + fdx_exclusive_scan_u32_workspace_size(n);
+}
+
+extern "C" size_t fdx_dense_ids_i64_workspace_size(int64_t n) {
+    return dense_ids_parts(n < 0 ? 0 : n, nullptr, nullptr, nullptr);
+}
+
+extern "C" int fdx_dense_ids_i64(const int64_t *keys_d, int64_t n, int32_t *ids_d, int64_t *n_unique_d,
+                                 void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(n_unique_d, "null n_unique");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        FDX_HIP(hipMemsetAsync(n_unique_d, 0, sizeof(int64_t), st));
+        return FDX_OK;
+    }
+    FDX_REQUIRE(keys_d && ids_d && workspace_d, "null pointer");
+    size_t o_perm, o_flags, o_scan;
+    const size_t need = dense_ids_parts(n, &o_perm, &o_flags, &o_scan);
+    if (workspace_bytes < need) {
+        set_error("dense ids workspace too small: %zu < %zu", workspace_bytes, need);
+        return FDX_E_WORKSPACE;
+    }
+    char *ws = reinterpret_cast<char *>(workspace_d);
+    int32_t *perm = reinterpret_cast<int32_t *>(ws + o_perm);
+    uint32_t *flags = reinterpret_cast<uint32_t *>(ws + o_flags);
+    SortWs<uint64_t> w;
+    sort_ws<uint64_t>(n, &w, ws);
+    const uint64_t *sorted = nullptr;
+    int rc = radix_sort<uint64_t>(reinterpret_cast<const uint64_t *>(keys_d), n, 64, 1ull << 63, nullptr,
+                                  reinterpret_cast<uint32_t *>(perm), w, st, &sorted);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_new_key_flags, dim3(stream_grid(n, 256)), dim3(256), 0, st, sorted, n, flags);
+    FDX_LAUNCHED("k_new_key_flags");
+    rc = exclusive_scan(flags, n, reinterpret_cast<uint32_t *>(ws + o_scan), st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_dense_scatter, dim3(stream_grid(n, 256)), dim3(256), 0, st, sorted, flags, perm, n, ids_d,
+                       n_unique_d);
+    FDX_LAUNCHED("k_dense_scatter");
+    return FDX_OK;
+}
+
 extern "C" int fdx_is_sorted_i64(const int64_t *keys_d, int64_t n, int32_t *flag_d, void *stream) {
     FDX_REQUIRE(n >= 0 && flag_d, "bad argument");
     hipStream_t st = as_stream(stream);

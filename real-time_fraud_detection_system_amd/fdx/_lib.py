@@ -112,6 +112,8 @@ SIGNATURES = {
     "fdx_customer_windows_scan_slots": (ctypes.c_int, [P, P, c_i64, c_i64, P, P, c_i64, c_i32, P, P, P, P, c_sz, P]),
     "fdx_argsort_i64_workspace_size": (c_sz, [c_i64]),
     "fdx_argsort_i64": (ctypes.c_int, [P, c_i64, P, P, c_sz, P]),
+    "fdx_dense_ids_i64_workspace_size": (c_sz, [c_i64]),
+    "fdx_dense_ids_i64": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),
     "fdx_is_sorted_i64": (ctypes.c_int, [P, c_i64, P, P]),
     "fdx_gather": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),
     "fdx_scatter": (ctypes.c_int, [P, c_i32, P, c_i64, P, P]),

@@ -128,10 +128,12 @@ def exchange_begin(K, term, world, group=None):
     """Phase 1 (enqueue only, no host sync): owner keys, re-key by owner, split exchange."""
     owner = K.owner_keys(term, world)
     send_perm, send_seg = K.rekey(owner, world)
-    send_counts = (send_seg[1:] - send_seg[:-1]).to(torch.int64)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    return send_perm, send_counts, recv_counts
+    # peer p gets the pair (send_seg[p], send_seg[p + 1]): the split sizes are differences of
+    # the pairs, taken on the host once they are read (exchange_finish) -- no device arithmetic
+    send_pairs = send_seg.unfold(0, 2, 1).contiguous()    # [world, 2] int64 (a copy)
+    recv_pairs = torch.empty_like(send_pairs)
+    dist.all_to_all_single(recv_pairs, send_pairs, group=group)
+    return send_perm, send_pairs, recv_pairs
 
 
 def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows_days=(1, 7, 30), delay_days=7,
@@ -143,8 +145,9 @@ def exchange_finish(K, state, ts, term, fraud, world, n_terminals_total, windows
     mark(name) is called after each phase is enqueued on the current stream (bench.py records
     HIP events there); stats (a dict) receives the split sizes and bytes per peer."""
     mk = mark or (lambda _name: None)
-    send_perm, send_counts, recv_counts = state
-    sc, rc = send_counts.tolist(), recv_counts.tolist()   # host sync: split sizes
+    send_perm, send_pairs, recv_pairs = state
+    sc = [b - a for a, b in send_pairs.tolist()]   # host sync: split sizes
+    rc = [b - a for a, b in recv_pairs.tolist()]
     rec = K.exchange_pack(ts, term, fraud, send_perm)
     recv = torch.empty((sum(rc), 2), dtype=torch.int64, device=rec.device)
     mk("exchange_pack")

@@ -68,8 +68,8 @@ def _dense_keys(keys: np.ndarray, dev):
     k = torch.from_numpy(np.ascontiguousarray(keys.astype(np.int64))).to(dev)
     if len(keys) and keys.min() >= 0 and keys.max() < (1 << 24):
         return k.to(torch.int32), int(keys.max()) + 1
-    uniq, inv = torch.unique(k, sorted=True, return_inverse=True)
-    return inv.to(torch.int32), int(uniq.numel())
+    ids, n_unique = ops.dense_ids_i64(k)  # sort-based dense re-id on the GPU (fdx_dense_ids_i64)
+    return ids, int(n_unique.item())
 
 
 def _grouped_order(df: pd.DataFrame, key_col: str, dev):

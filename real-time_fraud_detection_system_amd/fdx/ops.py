@@ -8,6 +8,7 @@ streams; all arithmetic happens in the HIP kernels of libfdx.so.
 from __future__ import annotations
 
 import ctypes
+import time
 from typing import Sequence
 
 import numpy as np
@@ -173,6 +174,20 @@ def argsort_i64(keys: torch.Tensor, stream=None) -> torch.Tensor:
     ws = workspace(L.fdx_argsort_i64_workspace_size(n), keys.device)
     check(L.fdx_argsort_i64(_ptr(keys), n, _ptr(perm), _ptr(ws), ws.numel(), _s(stream)), "fdx_argsort_i64")
     return perm
+
+
+def dense_ids_i64(keys: torch.Tensor, stream=None):
+    """(ids int32 [n], n_unique int64 device tensor [1]): order-preserving dense ids of int64
+    keys (fdx_dense_ids_i64)."""
+    _dev(keys, torch.int64, "keys")
+    n = keys.numel()
+    ids = torch.empty(n, dtype=torch.int32, device=keys.device)
+    nu = torch.empty(1, dtype=torch.int64, device=keys.device)
+    L = _lib.load()
+    ws = workspace(L.fdx_dense_ids_i64_workspace_size(n), keys.device)
+    check(L.fdx_dense_ids_i64(_ptr(keys), n, _ptr(ids), _ptr(nu), _ptr(ws), ws.numel(), _s(stream)),
+          "fdx_dense_ids_i64")
+    return ids, nu
 
 
 def is_sorted_i64(keys: torch.Tensor, stream=None) -> bool:
@@ -380,7 +395,9 @@ class PendingPlan:
     (no earlier) and returns the LayoutPlan (re-planning synchronously if the one-launch plan
     declined)."""
 
-    SPIN = 2_000_000  # polls of the pinned result (~0.1 us each) before the blocking wait
+    # wall time to poll the pinned result before the blocking wait: the plan lands ~1-2 ms after
+    # it is enqueued at config 2 (behind the customer re-key), so the poll usually ends first
+    SPIN_S = 5e-3
 
     def __init__(self, seg_off, n_windows, stream):
         self.seg_off, self.n_windows, self.stream = seg_off, int(n_windows), stream
@@ -408,12 +425,13 @@ class PendingPlan:
             # poll the pinned words for a bounded while before the blocking wait: the step's
             # critical stream idles until the host has read the slot count and launched the
             # layout fill, and waking from hipEventSynchronize took ~70 us (profiles/r03ad)
+            # (bounded by wall time, not a poll count: a Python poll costs 0.1-0.2 us and holds the GIL)
             hv = self._hv
-            for _ in range(self.SPIN):
-                if hv[0] != -1 and hv[1] != -1:
+            t_end = time.perf_counter() + self.SPIN_S
+            while hv[0] == -1 or hv[1] == -1:
+                if time.perf_counter() > t_end:
+                    self.ev.synchronize()
                     break
-            else:
-                self.ev.synchronize()
             if int(hv[1]) == 0:
                 return LayoutPlan(self.sorder, self.goff, int(hv[0]) & 0xFFFFFFFF, self.n_windows)
         return customer_layout_plan(self.seg_off, self.n_windows, self.stream)
@@ -506,20 +524,6 @@ def terminal_windows_compact(gts, seg_off, rows=None, gfraud=None, delay_days=7,
     return rec
 
 
-def compact_records_unpack(rec: torch.Tensor, n: int) -> torch.Tensor:
-    """terminal_windows_compact's array -> the [n, 3] int64 count records (NB | FRAUD << 32),
-    with torch ops (tests and inspection; the scoring path reads the compact form itself)."""
-    pair = rec[: 2 * n].view(n, 2)
-    lo, hi = pair[:, 0], pair[:, 1]
-    m = (1 << 21) - 1
-    out = torch.stack([((lo >> (21 * w)) & m) | (((hi >> (21 * w)) & m) << 32) for w in range(3)], dim=1)
-    esc = lo < 0
-    if bool(esc.any()):
-        off = (lo[esc] & ((1 << 63) - 1)).long()
-        out[esc] = torch.stack([rec[off + w] for w in range(3)], dim=1)
-    return out
-
-
 def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
                              runs: bool = False, records: bool = True, stream=None):
     """Terminal windows over grouped inputs (rekey_payload(terminal, ts, flag=fraud) outputs):
@@ -549,16 +553,6 @@ def terminal_windows_grouped(gts, seg_off, rows=None, gfraud=None, delay_days=7,
     risk = torch.empty((W, n), dtype=torch.float64, device=dev)
     check(L.fdx_terminal_windows_grouped(*args, _ptr(nb), _ptr(risk), None, _ptr(scratch), _s(stream)),
           "fdx_terminal_windows_grouped")
-    return nb, risk
-
-
-def unpack_term_records(rec: torch.Tensor):
-    """Count records -> (nb int32 [W, n], risk float64 [W, n]) with the kernels' division."""
-    w = rec.T
-    nb = (w & 0xFFFFFFFF).to(torch.int32)
-    fr = (w >> 32) & 0xFFFFFFFF
-    risk = torch.where(nb > 0, fr.to(torch.float64) / nb.clamp(min=1).to(torch.float64),
-                       torch.zeros((), dtype=torch.float64, device=rec.device))
     return nb, risk
 
 

@@ -178,3 +178,40 @@ def test_predict_proba_both_columns_bit_exact(golden):
     rf.fit(X[:6000], z["TX_FRAUD"][:6000])
     got = fdx.GpuForest(rf).predict_proba(X[6000:])
     np.testing.assert_array_equal(got, rf.predict_proba(X[6000:].astype(np.float32)))
+
+
+def test_sparse_and_negative_ids_group_like_pandas(golden):
+    """Ids that are not dense (huge, negative, gappy) take the sort-based dense re-id on the GPU
+    (fdx_dense_ids_i64): the features must equal those of the same frame with dense ids."""
+    z = golden("tiny_b.npz")
+    df = _frame(z)
+    rng = np.random.default_rng(11)
+    for col in ("CUSTOMER_ID", "TERMINAL_ID"):
+        ids = np.unique(df[col].values)
+        sparse = np.sort(rng.choice(np.arange(-(1 << 40), 1 << 40, 7919, dtype=np.int64), len(ids), replace=False))
+        remap = dict(zip(ids, sparse))
+        ds = df.copy()
+        ds[col] = ds[col].map(remap).astype(np.int64)
+        if col == "CUSTOMER_ID":
+            a = fdx.get_customer_spending_behaviour_features(df)[CUST].sort_index()
+            b = fdx.get_customer_spending_behaviour_features(ds)[CUST].sort_index()
+        else:
+            a = fdx.get_count_risk_rolling_window(df)[TERM].sort_index()
+            b = fdx.get_count_risk_rolling_window(ds)[TERM].sort_index()
+        np.testing.assert_array_equal(a.values, b.values)
+
+
+def test_dense_ids_i64_kernel(dev):
+    import torch
+
+    from fdx import ops
+
+    rng = np.random.default_rng(5)
+    for n in (1, 7, 100_003):
+        k = rng.integers(-(1 << 62), 1 << 62, n // 3 + 1)[rng.integers(0, n // 3 + 1, n)]
+        ids, nu = ops.dense_ids_i64(torch.from_numpy(k).to(dev))
+        u, inv = np.unique(k, return_inverse=True)
+        np.testing.assert_array_equal(ids.cpu().numpy(), inv.astype(np.int32))
+        assert int(nu.item()) == len(u)
+    ids, nu = ops.dense_ids_i64(torch.empty(0, dtype=torch.int64, device=dev))
+    assert ids.numel() == 0 and int(nu.item()) == 0

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import oracle
+from record_decode import unpack_term_records
 from forest_gen import random_forest
 from fdx import ops
 from fdx.pipeline import FraudPipeline
@@ -196,9 +197,9 @@ def test_windows_random_edge_cases(dev, max_len):
         gts, gfr, gseg = T(ts, torch.int64, dev), T(fr, torch.uint8, dev), T(seg, torch.int64, dev)
         rec = ops.terminal_windows_grouped(gts, gseg, gfraud=gfr, delay_days=7, windows_days=windows)
         W = len(windows)
-        rnb, rrisk = ops.unpack_term_records(rec)
-        np.testing.assert_array_equal(rnb.cpu().numpy(), onb)
-        np.testing.assert_array_equal(rrisk.cpu().numpy(), orisk)
+        rnb, rrisk = unpack_term_records(rec)
+        np.testing.assert_array_equal(rnb, onb)
+        np.testing.assert_array_equal(rrisk, orisk)
         # rows=perm: the record of grouped position q lands at row perm[q]
         perm = np.random.default_rng(W).permutation(len(ts)).astype(np.int32)
         rec2 = ops.terminal_windows_grouped(gts, gseg, rows=T(perm, torch.int32, dev), gfraud=gfr, delay_days=7,

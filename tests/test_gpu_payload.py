@@ -13,6 +13,7 @@ import pytest
 import torch
 
 import oracle
+from record_decode import compact_records_unpack, unpack_term_records
 from fdx import ops, synth
 from fdx.pipeline import FraudPipeline
 
@@ -79,9 +80,9 @@ def test_terminal_grouped_hot_terminal_records_and_columns(dev):
     # column form at grouped positions, fraud from a grouped byte column
     p = perm.cpu().numpy() & 0x7FFFFFFF
     nb, risk = ops.terminal_windows_grouped(gts, seg, gfraud=T(fraud[p], torch.uint8, dev), records=False)
-    onb, orisk = ops.unpack_term_records(T(ref[p], torch.int64, dev))
-    np.testing.assert_array_equal(nb.cpu().numpy(), onb.cpu().numpy())
-    np.testing.assert_array_equal(risk.cpu().numpy(), orisk.cpu().numpy())
+    onb, orisk = unpack_term_records(ref[p])
+    np.testing.assert_array_equal(nb.cpu().numpy(), onb)
+    np.testing.assert_array_equal(risk.cpu().numpy(), orisk)
 
 
 @pytest.mark.parametrize("parts", [1, 3, 8, 100])
@@ -155,13 +156,13 @@ def test_compact_records_equal_full_records(dev):
     rec = ops.terminal_windows_compact(gts, seg, rows=perm)
     assert rec.numel() == 5 * len(ts)
     assert not bool((rec[: 2 * len(ts)].view(-1, 2)[:, 0] < 0).any())  # everything fits 21 bits
-    np.testing.assert_array_equal(ops.compact_records_unpack(rec, len(ts)).cpu().numpy(), ref)
+    np.testing.assert_array_equal(compact_records_unpack(rec, len(ts)), ref)
     src = rng.integers(0, 8, len(ts))
     order = np.argsort(src, kind="stable")
     perm, seg, gts, _ = ops.rekey_payload(T(term[order], torch.int32, dev), 40, T(ts[order], torch.int64, dev),
                                           flag=T(fraud[order], torch.uint8, dev))
     rec = ops.terminal_windows_compact(gts, seg, rows=perm, runs=True)
-    np.testing.assert_array_equal(ops.compact_records_unpack(rec, len(ts)).cpu().numpy(), ref[order])
+    np.testing.assert_array_equal(compact_records_unpack(rec, len(ts)), ref[order])
 
 
 def test_compact_records_overflow_rows(dev, golden):
@@ -183,7 +184,7 @@ def test_compact_records_overflow_rows(dev, golden):
     n = len(ts)
     esc = (rec[: 2 * n].view(n, 2)[:, 0] < 0).cpu().numpy()
     assert esc.sum() > 0 and esc[:n_hot].sum() == 0
-    assert torch.equal(ops.compact_records_unpack(rec, n), full)
+    np.testing.assert_array_equal(compact_records_unpack(rec, n), full.cpu().numpy())
     assert int((full[:, 0] & 0xFFFFFFFF).max()) > (1 << 21)
     z = golden("forest_rf5d8.npz")
     arrays = {k: z[k] for k in ("left", "right", "feature", "threshold", "missing_left", "value1", "node_offsets")}
