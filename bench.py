@@ -50,6 +50,11 @@ LDS_RANDOM_STEPS = 1.561e11 * 64 / 2
 
 # SURVEY.md §8(d) algorithmic bytes per transaction (compact logical I/O, read once + write once)
 ALG = {"K2": 30, "K1-cust": 58, "K1-term": 49, "K3": 90, "end-to-end": 107}
+# what one step actually reads and writes per transaction, end to end: the raw columns in (ts 8,
+# customer 4, terminal 4, amount 8, fraud 1 = 25 B), proba out (8 B), and -- with the featurized
+# table emitted -- the 14 feature columns in §8(d)'s compact form (3 x int32 + 3 x f64 per half,
+# 2 x u8 flags = 74 B; the fdx_feature_row record pads them to 80 B, counted at 74)
+E2E_IN, E2E_PROBA, E2E_FEATURES = 25, 8, 74
 # bench stages (marks of FraudPipeline.run_fused) -> §8(d) unit and the kernels they launch
 # (substring of the rocprofv3 kernel name, dispatches per step; "chunks" = forest chunks)
 STAGES = [
@@ -131,6 +136,10 @@ def parse():
     ap.add_argument("--wide-records", action="store_true",
                     help="terminal count records in the 24-byte form (FraudPipeline(compact_records=False); "
                          "default: the 16-byte compact form)")
+    ap.add_argument("--no-emit-features", dest="emit_features", action="store_false",
+                    help="do not write the featurized table (default: every step writes the 14 feature columns "
+                         "per transaction as fdx_feature_row records in input row order, SURVEY.md §8(d)'s compact "
+                         "form, besides scoring)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
@@ -399,6 +408,7 @@ def main():
     pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode, compact_records=not args.wide_records)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
+    rows_out = ops.feature_rows(n_local, dev) if args.emit_features else None  # the featurized table
     marks_all = []   # per timed step: {stage: (start event, end event)}
     trav = []        # per timed step: (start, end) of the forest traversal
     shard_stats = {}  # the exchange's split sizes / bytes per peer (N > 1)
@@ -426,7 +436,7 @@ def main():
 
         def step(record):
             mark, marks = make_mark(record)
-            sp.run(ts, cust, term, amt, fr, proba, ws, mark=mark, stats=shard_stats)
+            sp.run(ts, cust, term, amt, fr, proba, ws, mark=mark, stats=shard_stats, rows_out=rows_out)
             if record:
                 marks_all.append(marks)
                 trav.append(marks["forest_traverse"])
@@ -435,7 +445,8 @@ def main():
 
         def step(record, overlap=True, into=None):
             mark, marks = make_mark(record)
-            pipe.run_fused(ts, lcust, term, amt, fr, n_cl, n_terms, proba, ws, mark=mark, overlap=overlap)
+            pipe.run_fused(ts, lcust, term, amt, fr, n_cl, n_terms, proba, ws, mark=mark, overlap=overlap,
+                           rows_out=rows_out)
             if record and into is not None:
                 into.append(marks)
             elif record:
@@ -519,7 +530,8 @@ def main():
                    "tx_per_gpu": n_local, "global_tx": n_total,
                    "parallelism": f"customer-sharded x{world}" + (" (RCCL all-to-all re-key)" if world > 1 else ""),
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)",
-                   "customer_averages": args.avg_mode},
+                   "customer_averages": args.avg_mode,
+                   "features_emitted": bool(args.emit_features)},
         "roofline": {"kernel": "k_forest_rank", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(max(fk)) if fk else None, "traffic_unit": "HBM bytes per launch (PMC)",
@@ -569,7 +581,8 @@ def main():
                           "pmc_traffic_bytes": round(u["pmc"]) if u["pmc_ok"] and pmc else None,
                           "traffic_over_alg": round(u["pmc"] / alg, 2) if u["pmc_ok"] and pmc else None})
         step_ms = sum(r["ms_in_step"] for r in table)
-        e2e = ALG["end-to-end"] * n_local / (dt / args.steps) / 1e9
+        e2e_b = E2E_IN + E2E_PROBA + (E2E_FEATURES if args.emit_features else 0)
+        e2e = e2e_b * n_local / (dt / args.steps) / 1e9
         out["kernels"] = {"per_stage": table, "per_unit": krows, "stage_sum_ms": round(step_ms, 3),
                           "streams": "rekey_terminal + terminal_windows run on a side stream, concurrently with the "
                                      "customer stages, so stage_sum_ms (of ms_in_step) exceeds ms_per_step by the "
@@ -578,8 +591,12 @@ def main():
                                      "that mode), the per-kernel durations the rooflines use; an isolated time "
                                      f"above {ISOLATED_MAX_OVER_IN_STEP}x the in-step time is rejected "
                                      "(ms_isolated_rejected) and ms falls back to ms_in_step",
-                          "end_to_end": {"alg_bytes_per_tx": ALG["end-to-end"], "achieved_GBs": round(e2e, 1),
-                                         "time": "ms_per_step",
+                          "end_to_end": {"alg_bytes_per_tx": e2e_b, "achieved_GBs": round(e2e, 1),
+                                         "time": "ms_per_step", "features_emitted": bool(args.emit_features),
+                                         "bytes": f"raw columns in {E2E_IN} + proba out {E2E_PROBA}"
+                                                  + (f" + feature columns out {E2E_FEATURES}" if args.emit_features
+                                                     else " (featurized table not written: --no-emit-features)")
+                                                  + f"; SURVEY.md §8(d)'s fused ideal is {ALG['end-to-end']}",
                                          "frac": round(e2e / HBM_PEAK_GBS, 4)},
                           "note": "ms_in_step = HIP events around each stage on its stream, median over the timed steps; "
                                   "alg bytes = SURVEY.md §8(d) per tx x tx; pmc = rocprofv3 FETCH/WRITE per "

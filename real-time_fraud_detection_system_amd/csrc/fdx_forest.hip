@@ -653,9 +653,10 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
     const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
-    int32_t *__restrict__ nan_flag, RankTab rt) {
+    int32_t *__restrict__ nan_flag, RankTab rt, uint4 *__restrict__ feat) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     constexpr int W = 3, nf = 15;
+    static_assert(sizeof(fdx_feature_row) == 80, "5 x 16-byte stores per feature record");
     __shared__ float s_e[kMaxRankSamples];  // Eytzinger sample tables (RankTab::etab)
     __shared__ uint16_t s_itab[16 * kIntTab];
     for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
@@ -749,11 +750,13 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
         bool nan = v[0] != v[0];
         uint16_t rq[W];
         bool rat_ok[W];
+        double cavg[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const int32_t c = cur.c[w];
             count(3 + 2 * w, c);
-            v[4 + 2 * w] = zval((val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w], mean, scale, 4 + 2 * w);
+            cavg[w] = (val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w];
+            v[4 + 2 * w] = zval(cavg[w], mean, scale, 4 + 2 * w);
             nan |= v[4 + 2 * w] != v[4 + 2 * w];
             const int64_t tw = cur.tw[w];
             const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
@@ -844,6 +847,22 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                 nan |= v[fr_] != v[fr_];
             }
         }
+        if (feat && live) {  // the featurized row, at its input row (uniform branch on feat)
+            int32_t tn[W];
+            double rk[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                tn[w] = term_nb(cur.tw[w]);
+                rk[w] = term_risk(cur.tw[w]);
+            }
+            auto u32 = [](double d, int h) { return (uint32_t)((uint64_t)__double_as_longlong(d) >> (32 * h)); };
+            uint4 *dst = feat + (int64_t)cur.r * 5;
+            dst[0] = make_uint4((uint32_t)cur.c[0], (uint32_t)cur.c[1], (uint32_t)cur.c[2], (uint32_t)tn[0]);
+            dst[1] = make_uint4((uint32_t)tn[1], (uint32_t)tn[2], u32(cavg[0], 0), u32(cavg[0], 1));
+            dst[2] = make_uint4(u32(cavg[1], 0), u32(cavg[1], 1), u32(cavg[2], 0), u32(cavg[2], 1));
+            dst[3] = make_uint4(u32(rk[0], 0), u32(rk[0], 1), u32(rk[1], 0), u32(rk[1], 1));
+            dst[4] = make_uint4(u32(rk[2], 0), u32(rk[2], 1), (uint32_t)we | (uint32_t)ni << 8, 0u);
+        }
         if (live && nan) *nan_flag = 1;
         need &= (1u << nf) - 1u;
         if (live && need) rank_row_global(v, rt, q, need);  // table overflows (rare): full lower_bound in HBM
@@ -882,6 +901,8 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
+    {1024, 1, 8, 1, 3, 2},   // 5: compact v2, 8 chains
+    {1024, 1, 10, 1, 3, 2},  // 6: compact v2, 10 chains
 };
 // (Round 3 also measured v1 with 6 / 8 / 9 chains, compact v2 with 10 chains and register
 // ranks -- the lane's rank row in 8 VGPRs, one ds_read per step: 16.3 vs 7.6 ms -- and removed
@@ -1306,6 +1327,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         last = 0;
     }
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
+    static_assert(BLOCK % 64 == 0, "whole waves (the u16 plane swizzle)");
     constexpr int K = R * G;
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
@@ -1325,9 +1347,15 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     __syncthreads();
     const uint8_t *ml = mleft + node_base;
     const bool any_nan = *nan_flag != 0;  // uniform
+    // u16 planes: a dword holds two rows' ranks; the lane of row slot 2i + h within its wave is
+    // i + 32h, so the two halves of a dword are read by lanes l and l + 32 -- different LDS lane
+    // groups -- and the 32 lanes of a group read 32 different banks whatever features they test
+    // (natural order put rows 2i, 2i+1 in one group: a 2-way conflict whenever their features
+    // differ).  u32 planes are conflict-free in natural order.
+    const int pslot = P16 ? ((tid & ~63) | ((tid & 31) << 1) | ((tid >> 5) & 1)) : tid;
     uint32_t lrow[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + tid) * (P16 ? 2 : 4));
+    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + pslot) * (P16 ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R], q2[R], q3[R];
@@ -1414,14 +1442,14 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                                               q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
                     for (int f = 0; f < 32; ++f)
-                        s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)((w16[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
+                        s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w16[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
                 } else {
                     const uint32_t w8[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
 #pragma unroll
                     for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
                         const uint32_t u = (w8[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
                         if (P16)
-                            s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
+                            s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)u;
                         else
                             s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
                     }
@@ -1484,14 +1512,14 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                                         q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
                 for (int f = 0; f < 32; ++f)
-                    s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)((w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
+                    s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
             } else {
                 const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
 #pragma unroll
                 for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
                     const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
                     if (P16)
-                        s_x16[f * kPlaneRows + r * BLOCK + tid] = (uint16_t)u;
+                        s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)u;
                     else
                         s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
                 }
@@ -2449,6 +2477,8 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
+                case 5: FDX_LAUNCH_RANK(1024, 1, 8, 3, 2); break;
+                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 3, 2); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
             }
 #undef FDX_LAUNCH_RANK
@@ -2573,6 +2603,17 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                                           const int32_t *cust_nb_d, const double *cust_avg_d,
                                           const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                           const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
+    return fdx_forest_prepare_grouped_rows(F, n, n_windows, flags_mode, cust_val_is_sum, cust_ts_d, cust_amount_d,
+                                           cust_nb_d, cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, nullptr, ws,
+                                           ws_bytes, stream);
+}
+
+extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
+                                               int32_t cust_val_is_sum, const int64_t *cust_ts_d,
+                                               const double *cust_amount_d, const int32_t *cust_nb_d,
+                                               const double *cust_avg_d, const int32_t *cust_perm_d,
+                                               const int32_t *term_inv_d, const int64_t *term_rec_d,
+                                               fdx_feature_row *rows_out_d, void *ws, size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
     FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
                 "the fused scoring rows need the v1 row format (one slot per feature)");
@@ -2597,10 +2638,11 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
     if (rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat && rt.etab) {
         hipLaunchKernelGGL(k_zfill_grouped_w3, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
                            cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,
-                           F->mean_d, F->scale_d, (void *)z, flag, rt);
+                           F->mean_d, F->scale_d, (void *)z, flag, rt, reinterpret_cast<uint4 *>(rows_out_d));
         FDX_LAUNCHED("k_zfill_grouped_w3");
         return FDX_OK;
     }
+    FDX_REQUIRE(!rows_out_d, "feature rows: n_windows = 3, compact terminal records and the rank layout only");
     FDX_PREP(k_zfill_grouped, dim3(grid), st, cust_ts_d, cust_amount_d, cust_nb_d, cust_avg_d, cust_perm_d,
              term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum, F->mean_d, F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill_grouped");

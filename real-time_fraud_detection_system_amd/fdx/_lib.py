@@ -142,6 +142,8 @@ SIGNATURES = {
     "fdx_forest_traverse": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),
     "fdx_forest_prepare_features": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_forest_prepare_grouped": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_sz, P]),
+    "fdx_forest_prepare_grouped_rows": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, P, c_sz,
+                                                       P]),
     "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
     "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
     "fdx_forest_get_variant": (ctypes.c_int, [P, P]),

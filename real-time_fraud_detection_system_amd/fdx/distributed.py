@@ -261,7 +261,7 @@ class ShardedPipeline:
         return X[:, : p.n_features]
 
     def run(self, ts, customer, terminal, amount, fraud, proba, ws, events=None, n_customers_local: int | None = None,
-            mark=None, stats=None):
+            mark=None, stats=None, rows_out=None):
         """featurize + score this rank's rows: the single-GPU scoring path (interleaved
         customer layout, FraudPipeline.run_fused) for the customer half; the terminal half
         comes back from the owners as packed count records in send order.  mark(stage, stream)
@@ -323,7 +323,7 @@ class ShardedPipeline:
         sinv.record_stream(main)
         ws = p._forest_ws(lay.n_slots, ws, ts.device)
         ops.forest_prepare_grouped(p.forest, p.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, sinv, back, ws,
-                                   n=lay.n_slots, val_is_sum=True)
+                                   n=lay.n_slots, val_is_sum=True, rows_out=rows_out)
         mk("assemble_rows", main)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import time
-from typing import Sequence
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -677,16 +677,40 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
-                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_compact: bool = False):
+                           ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_compact: bool = False,
+                           rows_out: Optional[torch.Tensor] = None):
     """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
-    term_compact: term_rec is terminal_windows_compact's array."""
+    term_compact: term_rec is terminal_windows_compact's array; rows_out: feature_rows(n_rows)
+    -- the featurized table (fdx_feature_row per input row) written by the same pass."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
     opts = (1 if val_is_sum else 0) | (4 if term_compact else 0)
-    check(_lib.load().fdx_forest_prepare_grouped(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
-                                                 _ptr(camt), _ptr(cnb),
-                                                 _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec), _ptr(ws),
-                                                 ws.numel(), _s(stream)), "fdx_forest_prepare_grouped")
+    if rows_out is not None and (rows_out.dtype != torch.uint8 or rows_out.dim() != 2 or rows_out.shape[1] != 80
+                                 or not rows_out.is_contiguous()):
+        raise ValueError("rows_out must be feature_rows(n_rows): contiguous uint8 [n_rows, 80]")
+    check(_lib.load().fdx_forest_prepare_grouped_rows(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
+                                                      _ptr(camt), _ptr(cnb),
+                                                      _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec),
+                                                      _ptr(rows_out), _ptr(ws), ws.numel(), _s(stream)),
+          "fdx_forest_prepare_grouped_rows")
+
+
+# fdx_feature_row (include/fdx.h): the featurized table's compact record, 80 bytes per transaction
+FEATURE_ROW_BYTES = 80
+
+
+def feature_rows(n_rows: int, device) -> torch.Tensor:
+    """An uninitialised [n_rows, 80] uint8 buffer of fdx_feature_row records."""
+    return torch.empty((int(n_rows), FEATURE_ROW_BYTES), dtype=torch.uint8, device=device)
+
+
+def feature_row_columns(rows: torch.Tensor) -> dict:
+    """Views of the fdx_feature_row fields (no copy): cust_nb / term_nb int32 [n, 3],
+    cust_avg / term_risk float64 [n, 3], weekend / night uint8 [n]."""
+    i32 = rows.view(torch.int32)  # [n, 20]
+    f64 = rows.view(torch.float64)  # [n, 10]
+    return {"cust_nb": i32[:, 0:3], "term_nb": i32[:, 3:6], "cust_avg": f64[:, 3:6], "term_risk": f64[:, 6:9],
+            "weekend": rows[:, 72], "night": rows[:, 73]}
 
 
 def forest_traverse_perm(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, out_perm: torch.Tensor,

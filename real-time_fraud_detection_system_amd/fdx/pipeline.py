@@ -126,7 +126,7 @@ class FraudPipeline:
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
                   proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, mark=None,
-                  validate: bool = True, overlap: bool = True):
+                  validate: bool = True, overlap: bool = True, rows_out: Optional[torch.Tensor] = None):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
@@ -142,10 +142,14 @@ class FraudPipeline:
         records a HIP event there).  validate: the customer / terminal ids must lie in
         [0, n_customers) / [0, n_terminals) (counted on the device, read once everything is
         enqueued -- no extra stall).  overlap=False runs everything on the caller's stream
-        (bench.py's isolated per-stage timings)."""
+        (bench.py's isolated per-stage timings).  rows_out (ops.feature_rows(n)): the
+        featurized table -- one fdx_feature_row per transaction in input row order, the 14
+        feature columns the reference's featurization writes -- from the same assembly pass."""
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         caller = stream or torch.cuda.current_stream()
+        if rows_out is not None and (rows_out.shape[0] < ts_ns.numel() or rows_out.device != ts_ns.device):
+            raise ValueError("rows_out must hold ops.feature_rows(n) on the inputs' device")
         if ts_ns.numel() == 0:  # an empty table: nothing to score
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
@@ -159,7 +163,8 @@ class FraudPipeline:
         side = self._side if overlap else caller
         if main is not caller:
             main.wait_stream(caller)
-            for t in (ts_ns, customer, terminal, amount, fraud, proba) + ((ws,) if ws is not None else ()):
+            for t in (ts_ns, customer, terminal, amount, fraud, proba) + ((ws,) if ws is not None else ()) + \
+                ((rows_out,) if rows_out is not None else ()):
                 t.record_stream(main)
         with torch.cuda.stream(main):
             mk("start", main)
@@ -225,7 +230,8 @@ class FraudPipeline:
             trec.record_stream(main)
             ws = self._forest_ws(lay.n_slots, ws, amount.device)
             ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                       ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact)
+                                       ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact,
+                                       rows_out=rows_out)
             mk("assemble_rows", main)
             ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
             mk("forest_traverse", main)
