@@ -136,10 +136,11 @@ def parse():
     ap.add_argument("--wide-records", action="store_true",
                     help="terminal count records in the 24-byte form (FraudPipeline(compact_records=False); "
                          "default: the 16-byte compact form)")
-    ap.add_argument("--no-emit-features", dest="emit_features", action="store_false",
-                    help="do not write the featurized table (default: every step writes the 14 feature columns "
-                         "per transaction as fdx_feature_row records in input row order, SURVEY.md §8(d)'s compact "
-                         "form, besides scoring)")
+    ap.add_argument("--emit-features", choices=("slot", "input", "none"), default="slot",
+                    help="the featurized table every step writes besides scoring: the 14 feature columns per "
+                         "transaction in SURVEY.md §8(d)'s compact form + the row index, as columns by scoring slot "
+                         "(default, coalesced: ops.FeatureTable) or as 80-byte records by input row (one random "
+                         "write per row: ops.FeatureRecords); none: scores only")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
@@ -408,7 +409,10 @@ def main():
     pipe = FraudPipeline(forest=forest, avg_mode=args.avg_mode, compact_records=not args.wide_records)
     ws = ops.workspace(forest.workspace_size(n_local * 11 // 10), dev)  # scoring slots incl. layout padding
     proba = torch.empty(n_local, dtype=torch.float64, device=dev)
-    rows_out = ops.feature_rows(n_local, dev) if args.emit_features else None  # the featurized table
+    emit = args.emit_features != "none"
+    # the featurized table: one record per scoring slot (incl. the layout's padding) or per row
+    rows_out = None if not emit else (ops.FeatureTable(n_local * 11 // 10, dev) if args.emit_features == "slot"
+                                      else ops.FeatureRecords(n_local, dev))
     marks_all = []   # per timed step: {stage: (start event, end event)}
     trav = []        # per timed step: (start, end) of the forest traversal
     shard_stats = {}  # the exchange's split sizes / bytes per peer (N > 1)
@@ -531,7 +535,7 @@ def main():
                    "parallelism": f"customer-sharded x{world}" + (" (RCCL all-to-all re-key)" if world > 1 else ""),
                    "model": "bench_assets/rf100_d20.npz (sklearn RandomForest, config-1 features)",
                    "customer_averages": args.avg_mode,
-                   "features_emitted": bool(args.emit_features)},
+                   "features_emitted": args.emit_features},
         "roofline": {"kernel": "k_forest_rank", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(max(fk)) if fk else None, "traffic_unit": "HBM bytes per launch (PMC)",
@@ -581,7 +585,7 @@ def main():
                           "pmc_traffic_bytes": round(u["pmc"]) if u["pmc_ok"] and pmc else None,
                           "traffic_over_alg": round(u["pmc"] / alg, 2) if u["pmc_ok"] and pmc else None})
         step_ms = sum(r["ms_in_step"] for r in table)
-        e2e_b = E2E_IN + E2E_PROBA + (E2E_FEATURES if args.emit_features else 0)
+        e2e_b = E2E_IN + E2E_PROBA + (E2E_FEATURES if emit else 0)
         e2e = e2e_b * n_local / (dt / args.steps) / 1e9
         out["kernels"] = {"per_stage": table, "per_unit": krows, "stage_sum_ms": round(step_ms, 3),
                           "streams": "rekey_terminal + terminal_windows run on a side stream, concurrently with the "
@@ -592,10 +596,11 @@ def main():
                                      f"above {ISOLATED_MAX_OVER_IN_STEP}x the in-step time is rejected "
                                      "(ms_isolated_rejected) and ms falls back to ms_in_step",
                           "end_to_end": {"alg_bytes_per_tx": e2e_b, "achieved_GBs": round(e2e, 1),
-                                         "time": "ms_per_step", "features_emitted": bool(args.emit_features),
+                                         "time": "ms_per_step", "features_emitted": args.emit_features,
                                          "bytes": f"raw columns in {E2E_IN} + proba out {E2E_PROBA}"
-                                                  + (f" + feature columns out {E2E_FEATURES}" if args.emit_features
-                                                     else " (featurized table not written: --no-emit-features)")
+                                                  + (f" + feature columns out {E2E_FEATURES} (by "
+                                                     f"{args.emit_features}, with the row index)" if emit
+                                                     else " (featurized table not written: --emit-features none)")
                                                   + f"; SURVEY.md §8(d)'s fused ideal is {ALG['end-to-end']}",
                                          "frac": round(e2e / HBM_PEAK_GBS, 4)},
                           "note": "ms_in_step = HIP events around each stage on its stream, median over the timed steps; "

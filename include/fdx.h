@@ -482,28 +482,43 @@ int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, 
                                const int64_t *term_rec_d, void *workspace_d, size_t workspace_bytes,
                                void *stream);
 /* The featurized table the reference writes (feature_transformation.ipynb:2890-2905; columns
- * added at :613-622 and :1509-1520), one 80-byte record per transaction in INPUT row order,
- * in the compact form of SURVEY §8(d): window counts as int32 (pandas holds the same integers
- * as float64), averages / risks float64 bit-equal to the reference's, the two flags as bytes.
- * Windows in windows_days order (1, 7, 30 for the reference). */
+ * added at :613-622 and :1509-1520): one 80-byte record per transaction in the compact form of
+ * SURVEY §8(d) -- window counts as int32 (pandas holds the same integers as float64),
+ * averages / risks float64 bit-equal to the reference's, the two flags as bytes -- plus the
+ * transaction's input row.  Windows in windows_days order (1, 7, 30 for the reference). */
 typedef struct fdx_feature_row {
     int32_t cust_nb[3];     /* CUSTOMER_ID_NB_TX_{w}DAY_WINDOW          */
     int32_t term_nb[3];     /* TERMINAL_ID_NB_TX_{w}DAY_WINDOW          */
     double cust_avg[3];     /* CUSTOMER_ID_AVG_AMOUNT_{w}DAY_WINDOW     */
     double term_risk[3];    /* TERMINAL_ID_RISK_{w}DAY_WINDOW           */
     uint8_t weekend, night; /* TX_DURING_WEEKEND, TX_DURING_NIGHT       */
-    uint8_t pad[6];
+    uint8_t pad[2];
+    int32_t row;            /* input row of the transaction (-1: a padding slot's record) */
 } fdx_feature_row;
-/* fdx_forest_prepare_grouped that also writes the featurized table: rows_out_d[r] for every
- * transaction r = cust_perm_d[i] >= 0 (padding slots write nothing), the same values the
- * scoring row is built from (n_windows = 3, compact terminal records, the rank layout; other
- * shapes: FDX_E_UNSUPPORTED).  rows_out_d NULL = fdx_forest_prepare_grouped. */
+/* rows_order of fdx_forest_prepare_grouped_rows */
+#define FDX_ROWS_INPUT_ORDER 1 /* out_d = fdx_feature_row records, out_d[r] = input row r (time order,
+                                  as the reference's table after its sort_values('TX_DATETIME')):
+                                  one random 80-byte write per row (rows >= out_cap: not written) */
+#define FDX_ROWS_SLOT_ORDER 2  /* out_d = the same fields as COLUMNS, by scoring slot i < n (padding
+                                  slots: row -1, zero features), each column written coalesced:
+                                  FDX_FEATURE_COL(c, cap) bytes into out_d, cap = rows per column */
+/* Column c of the slot-order table (a buffer of FDX_FEATURE_TABLE_BYTES(cap) bytes, cap >= n,
+ * cap % 64 == 0): 0-2 cust_nb[w] int32, 3-5 term_nb[w] int32, 6-8 cust_avg[w] float64,
+ * 9-11 term_risk[w] float64, 12 row int32, 13 flags uint8[2] per slot (weekend, night). */
+#define FDX_FEATURE_COL(c, cap)                                                                  \
+    ((c) < 6 ? (int64_t)(c) * 4 * (cap) : (c) < 12 ? (int64_t)24 * (cap) + ((c) - 6) * (int64_t)8 * (cap) \
+                                       : (c) == 12 ? (int64_t)72 * (cap) : (int64_t)76 * (cap))
+#define FDX_FEATURE_TABLE_BYTES(cap) ((int64_t)78 * (cap))
+/* fdx_forest_prepare_grouped that also writes the featurized table, in rows_order, with the
+ * same values the scoring row is built from (n_windows = 3 and the rank layout; other shapes:
+ * FDX_E_UNSUPPORTED).  out_d NULL = fdx_forest_prepare_grouped; out_cap = records (input order)
+ * or rows per column (slot order) the buffer holds. */
 int fdx_forest_prepare_grouped_rows(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
                                     int32_t cust_val_is_sum, const int64_t *cust_ts_d,
                                     const double *cust_amount_d, const int32_t *cust_nb_d,
                                     const double *cust_avg_d, const int32_t *cust_perm_d,
-                                    const int32_t *term_inv_d, const int64_t *term_rec_d,
-                                    fdx_feature_row *rows_out_d, void *workspace_d, size_t workspace_bytes,
+                                    const int32_t *term_inv_d, const int64_t *term_rec_d, void *out_d,
+                                    int64_t out_cap, int32_t rows_order, void *workspace_d, size_t workspace_bytes,
                                     void *stream);
 /* fdx_forest_traverse writing proba_d[out_perm_d[row]] (and leaf rows likewise). */
 int fdx_forest_traverse_perm(fdx_forest forest, int64_t n, double *proba_d, const int32_t *out_perm_d,

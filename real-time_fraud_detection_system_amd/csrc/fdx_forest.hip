@@ -648,12 +648,17 @@ struct PrepRow {
 #ifndef FDX_ZFILL_WAVES
 #define FDX_ZFILL_WAVES 4
 #endif
+// EMIT: the featurized table besides the rank rows (fdx_forest_prepare_grouped_rows): 0 = none,
+// FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
+// input row / at its slot, stored as soon as the row's values are loaded (the record's registers
+// die before the rank search; kept to the end, 15 VGPRs spilled)
+template <int EMIT>
 __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
     const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
-    int32_t *__restrict__ nan_flag, RankTab rt, uint4 *__restrict__ feat) {
+    int32_t *__restrict__ nan_flag, RankTab rt, char *__restrict__ feat, int64_t fcap) {
     constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     constexpr int W = 3, nf = 15;
     static_assert(sizeof(fdx_feature_row) == 80, "5 x 16-byte stores per feature record");
@@ -748,15 +753,50 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
         q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
         v[0] = zval(cur.a, mean, scale, 0);
         bool nan = v[0] != v[0];
+        if constexpr (EMIT != 0) {
+            // the featurized row: a record at its input row (one random 80-byte write), or the
+            // columns at its slot (consecutive lanes, consecutive elements: every store of a wave
+            // is whole lines; an 80-byte record per slot, 5 strided 16-byte stores, measured
+            // +0.62 ms at config 2; padding slots: row -1, zero features)
+            if (i < n && (EMIT == FDX_ROWS_SLOT_ORDER || (live && (uint64_t)cur.r < (uint64_t)fcap))) {
+                auto u32 = [](double d, int h) { return (uint32_t)((uint64_t)__double_as_longlong(d) >> (32 * h)); };
+                uint32_t c[W], tn[W];
+                double avg[W], rk[W];
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    c[w] = live ? (uint32_t)cur.c[w] : 0u;
+                    avg[w] = !live ? 0.0 : (val_is_sum & 1) ? cur.cv[w] / (double)cur.c[w] : cur.cv[w];
+                    tn[w] = live ? (uint32_t)term_nb(cur.tw[w]) : 0u;
+                    rk[w] = live ? term_risk(cur.tw[w]) : 0.0;
+                }
+                const uint32_t fl = live ? ((uint32_t)we | (uint32_t)ni << 8) : 0u;
+                if constexpr (EMIT == FDX_ROWS_SLOT_ORDER) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(w, fcap))[i] = c[w];
+                        reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(3 + w, fcap))[i] = tn[w];
+                        reinterpret_cast<double *>(feat + FDX_FEATURE_COL(6 + w, fcap))[i] = avg[w];
+                        reinterpret_cast<double *>(feat + FDX_FEATURE_COL(9 + w, fcap))[i] = rk[w];
+                    }
+                    reinterpret_cast<int32_t *>(feat + FDX_FEATURE_COL(12, fcap))[i] = live ? cur.r : -1;
+                    reinterpret_cast<uint16_t *>(feat + FDX_FEATURE_COL(13, fcap))[i] = (uint16_t)fl;
+                } else {
+                    uint4 *dst = reinterpret_cast<uint4 *>(feat) + (int64_t)cur.r * 5;
+                    dst[0] = make_uint4(c[0], c[1], c[2], tn[0]);
+                    dst[1] = make_uint4(tn[1], tn[2], u32(avg[0], 0), u32(avg[0], 1));
+                    dst[2] = make_uint4(u32(avg[1], 0), u32(avg[1], 1), u32(avg[2], 0), u32(avg[2], 1));
+                    dst[3] = make_uint4(u32(rk[0], 0), u32(rk[0], 1), u32(rk[1], 0), u32(rk[1], 1));
+                    dst[4] = make_uint4(u32(rk[2], 0), u32(rk[2], 1), fl, (uint32_t)cur.r);
+                }
+            }
+        }
         uint16_t rq[W];
         bool rat_ok[W];
-        double cavg[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const int32_t c = cur.c[w];
             count(3 + 2 * w, c);
-            cavg[w] = (val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w];
-            v[4 + 2 * w] = zval(cavg[w], mean, scale, 4 + 2 * w);
+            v[4 + 2 * w] = zval((val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w], mean, scale, 4 + 2 * w);
             nan |= v[4 + 2 * w] != v[4 + 2 * w];
             const int64_t tw = cur.tw[w];
             const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
@@ -846,22 +886,6 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                 need |= 1u << fr_;
                 nan |= v[fr_] != v[fr_];
             }
-        }
-        if (feat && live) {  // the featurized row, at its input row (uniform branch on feat)
-            int32_t tn[W];
-            double rk[W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                tn[w] = term_nb(cur.tw[w]);
-                rk[w] = term_risk(cur.tw[w]);
-            }
-            auto u32 = [](double d, int h) { return (uint32_t)((uint64_t)__double_as_longlong(d) >> (32 * h)); };
-            uint4 *dst = feat + (int64_t)cur.r * 5;
-            dst[0] = make_uint4((uint32_t)cur.c[0], (uint32_t)cur.c[1], (uint32_t)cur.c[2], (uint32_t)tn[0]);
-            dst[1] = make_uint4((uint32_t)tn[1], (uint32_t)tn[2], u32(cavg[0], 0), u32(cavg[0], 1));
-            dst[2] = make_uint4(u32(cavg[1], 0), u32(cavg[1], 1), u32(cavg[2], 0), u32(cavg[2], 1));
-            dst[3] = make_uint4(u32(rk[0], 0), u32(rk[0], 1), u32(rk[1], 0), u32(rk[1], 1));
-            dst[4] = make_uint4(u32(rk[2], 0), u32(rk[2], 1), (uint32_t)we | (uint32_t)ni << 8, 0u);
         }
         if (live && nan) *nan_flag = 1;
         need &= (1u << nf) - 1u;
@@ -1086,14 +1110,33 @@ constexpr uint32_t kOffMask = (P16 == 2 || P16 == 3) ? 0x7FFu : 0xFFFu;
 template <int P16>
 constexpr uint32_t kNodeB = P16 == 3 ? 32768u : kRankNodeB;
 
+// Compact planes (P16 = 3) are read a DWORD at a time: the lane's u16 rank is the low half
+// (lanes 0-31 of the wave) or the high half (lanes 32-63) of the dword it shares with lane
+// l +- 32 (the plane swizzle in k_forest_rank), and d = (x << sh) + S with sh = 16 / 0 puts it
+// in bits 31:16 either way.  For the high half the other row's rank (<= 0x7FFF) stays in bits
+// 15:0, where it adds to S's low half (slot << 11 | offset <= 0x7FFF) without a carry into bit 16:
+// d < 0 iff r <= k as before, and d >= S's low half >= offset when r > k, so med3(d, 1, offset)
+// steps exactly as with the u16 read (which measured ~27 % slower per tree than the u32 planes'
+// ds_read_b32: r04d forest trace, 70 vs 55 us per tree).
+template <int P16>
+__device__ __forceinline__ uint32_t plane_shift() {
+    return P16 == 3 && (threadIdx.x & 32) ? 0u : 16u;
+}
+template <int P16>
+__device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
+    return P16 == 3 ? lds32(lds, addr) : (P16 ? lds16(lds, addr) : lds32(lds, addr));
+}
+
 template <bool NAN_AWARE, int P16, int K>
 __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                           uint32_t (&nd)[K], const uint8_t *__restrict__ mleft) {
+    const uint32_t sh = plane_shift<P16>();
     uint32_t x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-        x[k] = P16 ? lds16(lds, (nd[k] & kSlotMask<P16>) | lane_base[k])
-                   : lds32(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+    for (int k = 0; k < K; ++k) {
+        x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+        if (P16 == 3) x[k] = (x[k] >> (16u - sh)) & 0xFFFFu;  // this lane's half
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint32_t st;
@@ -1130,10 +1173,6 @@ __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane
 // with sched_barrier, so every chain has its next LDS read in flight while the others
 // compute (the default schedule clusters all K reads of a phase behind all K updates, and
 // a wave's outstanding reads drain to zero twice per step).
-template <int P16>
-__device__ __forceinline__ uint32_t rank_x(const char *lds, uint32_t addr) {
-    return P16 ? lds16(lds, addr) : lds32(lds, addr);
-}
 // PW > 1: chains in groups of PW, the node reads of a group issued in reverse chain order
 // and its feature reads in forward order, so the first use in each group waits for the
 // group's last-issued read and one s_waitcnt covers the whole group (LDS reads of a wave
@@ -1144,6 +1183,7 @@ template <int P16, int K, int PW>
 __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                               uint32_t (&nd)[K], int depth, int pre = 0) {
     auto fetch_x = [&](int k) -> uint32_t { return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]); };
+    const uint32_t sh = plane_shift<P16>();
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
@@ -1154,7 +1194,7 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
             for (int j = PW - 1; j >= 0; --j) {
                 const int k = g + j;
                 if (k < K) {
-                    const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
+                    const int32_t d = P16 ? (int32_t)((x[k] << (P16 == 3 ? sh : 16u)) + nd[k]) : (int32_t)(x[k] - nd[k]);
                     uint32_t st, pn;  // pa += med3(d, 1, off) << 2, kept as 2 VALU on the byte address
                     // (a separate output: a read-write operand made the compiler copy pa first)
                     asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %4"
@@ -1355,7 +1395,8 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const int pslot = P16 ? ((tid & ~63) | ((tid & 31) << 1) | ((tid >> 5) & 1)) : tid;
     uint32_t lrow[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) lrow[r] = (uint32_t)((r * BLOCK + pslot) * (P16 ? 2 : 4));
+    for (int r = 0; r < R; ++r)  // compact planes: the byte address of the dword holding the lane's u16
+        lrow[r] = (uint32_t)(P16 == 3 ? ((r * BLOCK + pslot) & ~1) * 2 : (r * BLOCK + pslot) * (P16 ? 2 : 4));
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R], q2[R], q3[R];
@@ -2604,17 +2645,24 @@ extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_win
                                           const int32_t *cust_perm_d, const int32_t *term_inv_d,
                                           const int64_t *term_rec_d, void *ws, size_t ws_bytes, void *stream) {
     return fdx_forest_prepare_grouped_rows(F, n, n_windows, flags_mode, cust_val_is_sum, cust_ts_d, cust_amount_d,
-                                           cust_nb_d, cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, nullptr, ws,
-                                           ws_bytes, stream);
+                                           cust_nb_d, cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, nullptr, 0, 0,
+                                           ws, ws_bytes, stream);
 }
 
 extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
                                                int32_t cust_val_is_sum, const int64_t *cust_ts_d,
                                                const double *cust_amount_d, const int32_t *cust_nb_d,
                                                const double *cust_avg_d, const int32_t *cust_perm_d,
-                                               const int32_t *term_inv_d, const int64_t *term_rec_d,
-                                               fdx_feature_row *rows_out_d, void *ws, size_t ws_bytes, void *stream) {
+                                               const int32_t *term_inv_d, const int64_t *term_rec_d, void *rows_out_d,
+                                               int64_t out_cap, int32_t rows_order, void *ws, size_t ws_bytes,
+                                               void *stream) {
     FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(!rows_out_d || rows_order == FDX_ROWS_INPUT_ORDER || rows_order == FDX_ROWS_SLOT_ORDER,
+                "rows_order must be FDX_ROWS_INPUT_ORDER or FDX_ROWS_SLOT_ORDER");
+    FDX_REQUIRE(!rows_out_d || rows_order != FDX_ROWS_SLOT_ORDER || (out_cap >= n && out_cap % 64 == 0),
+                "slot-order feature table: out_cap %lld must be >= n = %lld and a multiple of 64",
+                (long long)out_cap, (long long)n);
+    FDX_REQUIRE(!rows_out_d || ((uintptr_t)rows_out_d & 15) == 0, "feature output must be 16-byte aligned");
     FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
                 "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
@@ -2636,9 +2684,17 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
     const unsigned grid = stream_grid(n, 256);
     const RankTab rt = rank_tab(F);
     if (rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat && rt.etab) {
-        hipLaunchKernelGGL(k_zfill_grouped_w3, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,
-                           cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,
-                           F->mean_d, F->scale_d, (void *)z, flag, rt, reinterpret_cast<uint4 *>(rows_out_d));
+#define FDX_ZFILL_W3(E)                                                                                          \
+    hipLaunchKernelGGL(k_zfill_grouped_w3<E>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,   \
+                       cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum, F->mean_d, \
+                       F->scale_d, (void *)z, flag, rt, reinterpret_cast<char *>(rows_out_d), out_cap)
+        if (!rows_out_d)
+            FDX_ZFILL_W3(0);
+        else if (rows_order == FDX_ROWS_SLOT_ORDER)
+            FDX_ZFILL_W3(FDX_ROWS_SLOT_ORDER);
+        else
+            FDX_ZFILL_W3(FDX_ROWS_INPUT_ORDER);
+#undef FDX_ZFILL_W3
         FDX_LAUNCHED("k_zfill_grouped_w3");
         return FDX_OK;
     }

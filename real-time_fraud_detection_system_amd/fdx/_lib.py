@@ -16,6 +16,8 @@ FDX_OK = 0
 FDX_E_UNSUPPORTED = -3
 FDX_FLAGS_NOTEBOOK = 0
 FDX_FLAGS_SPARK = 1
+FDX_ROWS_INPUT_ORDER = 1  # fdx_forest_prepare_grouped_rows: the featurized table by input row
+FDX_ROWS_SLOT_ORDER = 2   # ... by scoring slot (coalesced; each record carries its row)
 FDX_KEY_MOD, FDX_KEY_DIV, FDX_KEY_SUB = 0, 1, 2
 MAX_WINDOWS = 8
 MAX_FEATURES = 32
@@ -142,8 +144,8 @@ SIGNATURES = {
     "fdx_forest_traverse": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),
     "fdx_forest_prepare_features": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_forest_prepare_grouped": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_sz, P]),
-    "fdx_forest_prepare_grouped_rows": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, P, c_sz,
-                                                       P]),
+    "fdx_forest_prepare_grouped_rows": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_i64,
+                                                       c_i32, P, c_sz, P]),
     "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
     "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
     "fdx_forest_get_variant": (ctypes.c_int, [P, P]),

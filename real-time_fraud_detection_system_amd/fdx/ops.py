@@ -678,39 +678,64 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
 
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
                            ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_compact: bool = False,
-                           rows_out: Optional[torch.Tensor] = None):
+                           rows_out=None):
     """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
-    term_compact: term_rec is terminal_windows_compact's array; rows_out: feature_rows(n_rows)
-    -- the featurized table (fdx_feature_row per input row) written by the same pass."""
+    term_compact: term_rec is terminal_windows_compact's array; rows_out: the featurized table
+    written by the same pass -- a FeatureRecords (by input row) or a FeatureTable (columns by
+    scoring slot, capacity >= n)."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
     opts = (1 if val_is_sum else 0) | (4 if term_compact else 0)
-    if rows_out is not None and (rows_out.dtype != torch.uint8 or rows_out.dim() != 2 or rows_out.shape[1] != 80
-                                 or not rows_out.is_contiguous()):
-        raise ValueError("rows_out must be feature_rows(n_rows): contiguous uint8 [n_rows, 80]")
+    out, cap, order = None, 0, 0
+    if rows_out is not None:
+        if not isinstance(rows_out, (FeatureRecords, FeatureTable)):
+            raise TypeError("rows_out must be a FeatureRecords or a FeatureTable")
+        if isinstance(rows_out, FeatureTable) and rows_out.cap < n:
+            raise ValueError(f"the feature table holds {rows_out.cap} slots < {n}")
+        out, cap, order = rows_out.buf, rows_out.cap, rows_out.order
     check(_lib.load().fdx_forest_prepare_grouped_rows(forest._h, n, W, int(flags_mode), opts, _ptr(cts),
                                                       _ptr(camt), _ptr(cnb),
                                                       _ptr(cavg), _ptr(cperm), _ptr(term_inv), _ptr(term_rec),
-                                                      _ptr(rows_out), _ptr(ws), ws.numel(), _s(stream)),
+                                                      _ptr(out), cap, order, _ptr(ws), ws.numel(), _s(stream)),
           "fdx_forest_prepare_grouped_rows")
 
 
-# fdx_feature_row (include/fdx.h): the featurized table's compact record, 80 bytes per transaction
-FEATURE_ROW_BYTES = 80
+class FeatureRecords:
+    """The featurized table by INPUT row: fdx_feature_row records (include/fdx.h), 80 bytes each
+    -- the 14 feature columns of the reference's table in SURVEY.md §8(d)'s compact form plus
+    the row index; record r = transaction r (time order).  columns(): views, no copy."""
+    order = _lib.FDX_ROWS_INPUT_ORDER
+    BYTES = 80
+
+    def __init__(self, n_rows: int, device):
+        self.cap = int(n_rows)
+        self.buf = torch.empty((self.cap, self.BYTES), dtype=torch.uint8, device=device)
+
+    def columns(self) -> dict:
+        i32, f64 = self.buf.view(torch.int32), self.buf.view(torch.float64)
+        return {"cust_nb": i32[:, 0:3].T, "term_nb": i32[:, 3:6].T, "cust_avg": f64[:, 3:6].T,
+                "term_risk": f64[:, 6:9].T, "weekend": self.buf[:, 72], "night": self.buf[:, 73], "row": i32[:, 19]}
 
 
-def feature_rows(n_rows: int, device) -> torch.Tensor:
-    """An uninitialised [n_rows, 80] uint8 buffer of fdx_feature_row records."""
-    return torch.empty((int(n_rows), FEATURE_ROW_BYTES), dtype=torch.uint8, device=device)
+class FeatureTable:
+    """The featurized table by SCORING SLOT, as columns (FDX_FEATURE_COL layout of include/fdx.h,
+    one buffer): each column written coalesced by the assembly pass; slot i holds the
+    transaction `row[i]` (-1 for the interleaved layout's padding slots, whose features are
+    zero).  cap = slots per column (a multiple of 64, >= the layout's slot count)."""
+    order = _lib.FDX_ROWS_SLOT_ORDER
 
+    def __init__(self, cap_slots: int, device):
+        self.cap = (int(cap_slots) + 63) // 64 * 64
+        self.buf = torch.empty(78 * self.cap, dtype=torch.uint8, device=device)
 
-def feature_row_columns(rows: torch.Tensor) -> dict:
-    """Views of the fdx_feature_row fields (no copy): cust_nb / term_nb int32 [n, 3],
-    cust_avg / term_risk float64 [n, 3], weekend / night uint8 [n]."""
-    i32 = rows.view(torch.int32)  # [n, 20]
-    f64 = rows.view(torch.float64)  # [n, 10]
-    return {"cust_nb": i32[:, 0:3], "term_nb": i32[:, 3:6], "cust_avg": f64[:, 3:6], "term_risk": f64[:, 6:9],
-            "weekend": rows[:, 72], "night": rows[:, 73]}
+    def columns(self, n_slots: int = None) -> dict:
+        m, c = (self.cap if n_slots is None else int(n_slots)), self.cap
+        i32 = self.buf[: 24 * c].view(torch.int32).view(6, c)
+        f64 = self.buf[24 * c: 72 * c].view(torch.float64).view(6, c)
+        row = self.buf[72 * c: 76 * c].view(torch.int32)
+        fl = self.buf[76 * c: 78 * c].view(c, 2)
+        return {"cust_nb": i32[0:3, :m], "term_nb": i32[3:6, :m], "cust_avg": f64[0:3, :m], "term_risk": f64[3:6, :m],
+                "weekend": fl[:m, 0], "night": fl[:m, 1], "row": row[:m]}
 
 
 def forest_traverse_perm(forest: "Forest", n: int, ws: torch.Tensor, out: torch.Tensor, out_perm: torch.Tensor,

@@ -126,7 +126,7 @@ class FraudPipeline:
 
     def run_fused(self, ts_ns, customer, terminal, amount, fraud, n_customers, n_terminals,
                   proba: torch.Tensor, ws: Optional[torch.Tensor] = None, stream=None, mark=None,
-                  validate: bool = True, overlap: bool = True, rows_out: Optional[torch.Tensor] = None):
+                  validate: bool = True, overlap: bool = True, rows_out=None):
         """The scoring path of bench.py: no float64 feature matrix.  The customer half is
         computed in the interleaved (lane-major) layout and the scoring rows follow that
         layout (customer features already in place, the terminal half one count record per
@@ -142,14 +142,18 @@ class FraudPipeline:
         records a HIP event there).  validate: the customer / terminal ids must lie in
         [0, n_customers) / [0, n_terminals) (counted on the device, read once everything is
         enqueued -- no extra stall).  overlap=False runs everything on the caller's stream
-        (bench.py's isolated per-stage timings).  rows_out (ops.feature_rows(n)): the
-        featurized table -- one fdx_feature_row per transaction in input row order, the 14
-        feature columns the reference's featurization writes -- from the same assembly pass."""
+        (bench.py's isolated per-stage timings).  rows_out: the featurized table -- the 14
+        feature columns the reference's featurization writes, with each transaction's input
+        row -- from the same assembly pass: an ops.FeatureRecords(n) (one record per input row,
+        time order: one random 80-byte write per row) or an ops.FeatureTable (columns by
+        scoring slot, written coalesced; capacity >= self.last_slots, which a caller can size
+        as n * 11 // 10 -- the layout pads < 1 %; padding slots' rows are -1)."""
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         caller = stream or torch.cuda.current_stream()
-        if rows_out is not None and (rows_out.shape[0] < ts_ns.numel() or rows_out.device != ts_ns.device):
-            raise ValueError("rows_out must hold ops.feature_rows(n) on the inputs' device")
+        if rows_out is not None and (rows_out.buf.device != ts_ns.device or
+                                     (isinstance(rows_out, ops.FeatureRecords) and rows_out.cap < ts_ns.numel())):
+            raise ValueError("rows_out must be an ops.FeatureRecords(n) / ops.FeatureTable on the inputs' device")
         if ts_ns.numel() == 0:  # an empty table: nothing to score
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
@@ -164,7 +168,7 @@ class FraudPipeline:
         if main is not caller:
             main.wait_stream(caller)
             for t in (ts_ns, customer, terminal, amount, fraud, proba) + ((ws,) if ws is not None else ()) + \
-                ((rows_out,) if rows_out is not None else ()):
+                ((rows_out.buf,) if rows_out is not None else ()):
                 t.record_stream(main)
         with torch.cuda.stream(main):
             mk("start", main)

@@ -120,32 +120,44 @@ def test_config1_scoring_fused_vs_f64_vs_oracle(dev, config1, model):
         assert len(np.unique(fused)) >= 3
 
 
-def test_config1_featurized_table_rows(dev, config1):
+@pytest.mark.parametrize("order", ["input", "slot"])
+def test_config1_featurized_table_rows(dev, config1, order):
     """run_fused(rows_out=...): the featurized table the reference writes
     (feature_transformation.ipynb:2890-2905) from the scoring path's own assembly pass -- one
-    fdx_feature_row per transaction in input row order -- equal to the C oracle on every
-    feature of every row (counts as exact integers, averages / risks bit for bit, flags), and
-    the scores unchanged by emitting it."""
+    fdx_feature_row per transaction, by input row or by scoring slot (each record carrying its
+    row) -- equal to the C oracle on every feature of every row (counts as exact integers,
+    averages / risks bit for bit, flags), and the scores unchanged by emitting it."""
     g, d, Xo = config1
     arrays, mean, scale = _load("rf100_d20")
     pipe = FraudPipeline(forest=ops.Forest(arrays, 15, mean, scale))
     n = len(d["ts"])
     args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 5_000, 10_000)
-    rows = ops.feature_rows(n, dev)
-    rows.fill_(0xAB)
+    rows = ops.FeatureTable(n * 11 // 10, dev) if order == "slot" else ops.FeatureRecords(n, dev)
+    rows.buf.fill_(0xAB)
     p_rows = torch.empty(n, dtype=torch.float64, device=dev)
     pipe.run_fused(*args, p_rows, rows_out=rows)
     p_plain = torch.empty(n, dtype=torch.float64, device=dev)
     pipe.run_fused(*args, p_plain)
     assert torch.equal(p_rows, p_plain)
-    col = {k: v.cpu().numpy() for k, v in ops.feature_row_columns(rows).items()}
+    if order == "slot":  # slots 0..n_slots-1: every row exactly once, padding slots row -1 and zero
+        m = pipe.last_slots
+        assert n <= m <= rows.cap
+        col = {k: v.cpu().numpy() for k, v in rows.columns(m).items()}
+        real = col["row"] >= 0
+        assert real.sum() == n and not col["cust_nb"][:, ~real].any() and not col["term_risk"][:, ~real].any()
+        assert not col["weekend"][~real].any() and not col["night"][~real].any()
+        o = np.argsort(col["row"][real], kind="stable")
+        col = {k: (v[..., real][..., o]) for k, v in col.items()}
+    else:
+        col = {k: v.cpu().numpy() for k, v in rows.columns().items()}
+    np.testing.assert_array_equal(col["row"], np.arange(n, dtype=np.int32))
     np.testing.assert_array_equal(col["weekend"], Xo[:, 1].astype(np.uint8))
     np.testing.assert_array_equal(col["night"], Xo[:, 2].astype(np.uint8))
     for w in range(3):
-        np.testing.assert_array_equal(col["cust_nb"][:, w], Xo[:, 3 + 2 * w].astype(np.int32))
-        np.testing.assert_array_equal(col["cust_avg"][:, w].view(np.int64), Xo[:, 4 + 2 * w].view(np.int64))
-        np.testing.assert_array_equal(col["term_nb"][:, w], Xo[:, 9 + 2 * w].astype(np.int32))
-        np.testing.assert_array_equal(col["term_risk"][:, w].view(np.int64), Xo[:, 10 + 2 * w].view(np.int64))
-    assert not rows[:, 74:].any()  # padding zeroed
+        np.testing.assert_array_equal(col["cust_nb"][w], Xo[:, 3 + 2 * w].astype(np.int32))
+        np.testing.assert_array_equal(col["cust_avg"][w].view(np.int64), Xo[:, 4 + 2 * w].view(np.int64))
+        np.testing.assert_array_equal(col["term_nb"][w], Xo[:, 9 + 2 * w].astype(np.int32))
+        np.testing.assert_array_equal(col["term_risk"][w].view(np.int64), Xo[:, 10 + 2 * w].view(np.int64))
+    small = ops.FeatureTable(64, dev) if order == "slot" else ops.FeatureRecords(n - 1, dev)
     with pytest.raises(ValueError):
-        pipe.run_fused(*args, p_rows, rows_out=rows[: n - 1])
+        pipe.run_fused(*args, p_rows, rows_out=small)

@@ -9,6 +9,7 @@
 #   forest[=<bench_forest args>] bench_forest.py (configs[2])
 #   stream[=<bench_stream args>] bench_stream.py (configs[4])
 #   py=<script args>             python3 <script args> (a study script)
+#   tracepy=<script args>        rocprofv3 kernel trace + stats of python3 <script args> -> <tag>_tracepy_<n>/
 set -eu
 TAG=${1:?tag}
 shift
@@ -39,6 +40,10 @@ for st in "$@"; do
             -- python3 bench.py ${arg:---steps 5 --warmup 2 --no-cpu-baseline} > $O/trace_$n.log 2>&1 \
             || { echo "trace failed"; tail -20 $O/trace_$n.log; exit 1; }
         echo "trace $n ok" ;;
+    tracepy)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tracepy_$n \
+            -- python3 $arg > $O/tracepy_$n.log 2>&1 || { echo "tracepy failed"; tail -20 $O/tracepy_$n.log; exit 1; }
+        tail -3 $O/tracepy_$n.log ;;
     pmc)
         ctr=${arg%%@*}
         bargs="--steps 2 --warmup 1 --no-cpu-baseline --isolated-steps 0"
