@@ -61,7 +61,8 @@ STAGES = [
     ("rekey_customer", "K2", [("k_radix_hist<unsigned int, 8>", 2), ("k_radix_scatter<unsigned int, 8, 2>", 2)]),
     ("customer_layout", "K1-cust", [("k_interleave<true, true>", 1)]),
     ("customer_walk", "K1-cust", [("k_customer_walk", 1)]),
-    ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 2), ("k_radix_scatter<unsigned int, 9, 1>", 2)]),
+    ("rekey_terminal", "K2", [("k_radix_hist<unsigned int, 9>", 1), ("k_radix_scatter<unsigned int, 9, 1>", 1),
+                              ("k_radix_scatter<unsigned int, 8, 1>", 1)]),  # 17-bit ids: a 9- and an 8-bit pass
     ("terminal_windows", "K1-term", [("k_terminal_short<3>", 1), ("k_terminal_g<false, 1024>", 1)]),
     ("assemble_rows", "K3", [("k_zfill_grouped_w3", 1)]),
     ("forest_traverse", "K3", [("k_forest_rank", "chunks")]),
@@ -71,7 +72,8 @@ EXCHANGE_STAGES = [
     ("exchange_splits", "xGMI", [("k_key_map", 1), ("k_radix_hist", 1), ("k_radix_scatter", 1)]),
     ("exchange_pack", "xGMI", [("k_exchange_pack", 1)]),
     ("exchange_rows", "xGMI", []),
-    ("owner_windows", "K1-term", [("k_exchange_unpack", 1), ("k_radix_scatter<unsigned int, 9, 1>", 2),
+    ("owner_windows", "K1-term", [("k_exchange_unpack", 1), ("k_radix_scatter<unsigned int, 9, 1>", 1),
+                                  ("k_radix_scatter<unsigned int, 8, 1>", 1),
                                   ("k_terminal_g<true>", 1)]),
     ("exchange_back", "xGMI", []),
 ]

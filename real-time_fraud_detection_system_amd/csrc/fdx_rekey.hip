@@ -587,9 +587,12 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
                const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr, uint64_t key_limit = 0,
                int32_t *bad = nullptr) {
     const int64_t tiles = ceil_div(n, kTile);
-    // 9-bit digits when they need fewer passes than 8-bit ones (17- and 18-bit keys: 2, not 3)
-    const int dbits = ((bits + 8) / 9 < (bits + kRadixBits - 1) / kRadixBits) ? 9 : kRadixBits;
-    const int passes = (bits + dbits - 1) / dbits;
+    // 9-bit digits only where they save a pass (17- and 18-bit keys: 2 passes, not 3), and then
+    // only as many as the key needs: 17 bits = 9 + 8 -- an 8-bit pass writes runs of ~16 keys
+    // per digit and 4,096-key tile (a 9-bit pass ~8: twice the partial lines)
+    const int p8 = (bits + kRadixBits - 1) / kRadixBits, p9 = (bits + 8) / 9;
+    const int passes = std::min(p8, p9);
+    const int n9 = p9 < p8 ? std::max(0, bits - kRadixBits * passes) : 0;  // leading 9-bit passes
     const K *kin = keys;
     const uint32_t *vin = nullptr;  // identity on the first pass
     const uint64_t *pin[2] = {pw > 0 ? pay_in[0] : nullptr, pw > 1 ? pay_in[1] : nullptr};
@@ -606,7 +609,8 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         return FDX_OK;
     }
     for (int p = 0; p < passes; ++p) {
-        const int shift = p * dbits;
+        const int dbits = p < n9 ? 9 : kRadixBits;
+        const int shift = p < n9 ? 9 * p : 9 * n9 + kRadixBits * (p - n9);
         const bool last = p == passes - 1;
         K *kout = (p & 1) ? w.k1 : w.k0;
         if (last && keys_out) kout = keys_out;
