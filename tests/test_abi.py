@@ -120,3 +120,58 @@ def test_threshold_round_down_edge_cases():
     expect = np.stack([(cand.astype(np.float64) <= t) for t in thr], axis=1)  # left leaf = node 1
     np.testing.assert_array_equal(leaves == 1, expect)
     _ = _lib
+
+
+def test_feature_table_layouts_match_the_header():
+    """The featurized table's two layouts (include/fdx.h): the 80-byte fdx_feature_row record
+    (FeatureRecords' views) and the slot-order columns at FDX_FEATURE_COL(c, cap)
+    (FeatureTable's views) -- checked on CPU tensors by writing through the C layout and
+    reading through the Python views."""
+    import torch
+
+    from fdx import ops
+
+    class Row(ctypes.Structure):  # the header's struct, field for field
+        _fields_ = [("cust_nb", ctypes.c_int32 * 3), ("term_nb", ctypes.c_int32 * 3),
+                    ("cust_avg", ctypes.c_double * 3), ("term_risk", ctypes.c_double * 3),
+                    ("weekend", ctypes.c_uint8), ("night", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 2),
+                    ("row", ctypes.c_int32)]
+
+    assert ctypes.sizeof(Row) == ops.FeatureRecords.BYTES == 80
+    rec = ops.FeatureRecords(3, "cpu")
+    for r in range(3):
+        x = Row((ctypes.c_int32 * 3)(r, r + 1, r + 2), (ctypes.c_int32 * 3)(10 + r, 11, 12),
+                (ctypes.c_double * 3)(0.5 + r, 1.5, 2.5), (ctypes.c_double * 3)(0.25, 0.125 * r, 1.0),
+                r % 2, 1, (ctypes.c_uint8 * 2)(0, 0), 100 + r)
+        rec.buf[r] = torch.frombuffer(bytearray(bytes(x)), dtype=torch.uint8)
+    c = rec.columns()
+    assert c["cust_nb"][:, 2].tolist() == [2, 3, 4] and c["term_nb"][0].tolist() == [10, 11, 12]
+    assert c["cust_avg"][0].tolist() == [0.5, 1.5, 2.5] and c["term_risk"][1].tolist() == [0.0, 0.125, 0.25]
+    assert c["weekend"].tolist() == [0, 1, 0] and c["night"].tolist() == [1, 1, 1]
+    assert c["row"].tolist() == [100, 101, 102]
+
+    def col(c_, cap):  # FDX_FEATURE_COL of include/fdx.h
+        return c_ * 4 * cap if c_ < 6 else (24 * cap + (c_ - 6) * 8 * cap if c_ < 12 else
+                                            (72 * cap if c_ == 12 else 76 * cap))
+
+    src = open(HEADER).read()
+    assert "#define FDX_FEATURE_TABLE_BYTES(cap) ((int64_t)78 * (cap))" in src
+    t = ops.FeatureTable(100, "cpu")
+    cap = t.cap
+    assert cap % 64 == 0 and cap >= 100 and t.buf.numel() == 78 * cap
+    raw = t.buf.numpy()
+    for w in range(3):
+        raw[col(w, cap):col(w, cap) + 4 * cap].view(np.int32)[:] = np.arange(cap) + 1000 * w
+        raw[col(3 + w, cap):col(3 + w, cap) + 4 * cap].view(np.int32)[:] = -np.arange(cap) - w
+        raw[col(6 + w, cap):col(6 + w, cap) + 8 * cap].view(np.float64)[:] = np.arange(cap) / 8 + w
+        raw[col(9 + w, cap):col(9 + w, cap) + 8 * cap].view(np.float64)[:] = np.arange(cap) / 16 - w
+    raw[col(12, cap):col(12, cap) + 4 * cap].view(np.int32)[:] = np.arange(cap) * 3
+    raw[col(13, cap):col(13, cap) + 2 * cap].reshape(cap, 2)[:] = np.stack([np.arange(cap) % 2, 1 - np.arange(cap) % 2], 1)
+    c = t.columns(70)
+    for w in range(3):
+        assert c["cust_nb"][w].tolist() == list(range(1000 * w, 1000 * w + 70))
+        assert c["term_nb"][w].tolist() == [-i - w for i in range(70)]
+        assert c["cust_avg"][w].tolist() == [i / 8 + w for i in range(70)]
+        assert c["term_risk"][w].tolist() == [i / 16 - w for i in range(70)]
+    assert c["row"].tolist() == [3 * i for i in range(70)]
+    assert c["weekend"].tolist() == [i % 2 for i in range(70)] and c["night"].tolist() == [1 - i % 2 for i in range(70)]
