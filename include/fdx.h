@@ -436,8 +436,7 @@ int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *
  *   1 = rank layout v1, 1,024 threads x 10 trees per lane (the default when the forest fits v1),
  *   2 = rank layout v2, 32 threshold slots (the default for forests v1 cannot hold),
  *   3 = v2 nodes over 16 compact u16 planes (every feature in one slot),
- *   4 = rank layout v2 with 10 trees per lane,
- *   5, 6 = as 3 with 8 / 10 trees per lane.
+ *   4 = rank layout v2 with 10 trees per lane.
  * Variants > 0 need <= 15 features (the rank rows' 16th slot is the v1 sentinel) and the
  * rank layout (FDX_E_UNSUPPORTED otherwise; a
  * refused call leaves the forest's node format, variant and chunks as they were).

@@ -1183,8 +1183,6 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 8, 3, 2); break;
-                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 3, 2); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
             }
 #undef FDX_LAUNCH_RANK

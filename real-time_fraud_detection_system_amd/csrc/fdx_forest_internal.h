@@ -143,9 +143,9 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
-    {1024, 1, 8, 1, 3, 2},   // 5: compact v2, 8 chains
-    {1024, 1, 10, 1, 3, 2},  // 6: compact v2, 10 chains
 };
+// (Round 4 measured compact v2 with 8 / 10 chains as well -- 7.27 ms against 6.91 for variant 1,
+// the extra depth of its jump nodes, profiles/r04e_forest_launches.txt -- and removed them.)
 // (Round 3 also measured v1 with 6 / 8 / 9 chains, compact v2 with 10 chains and register
 // ranks -- the lane's rank row in 8 VGPRs, one ds_read per step: 16.3 vs 7.6 ms -- and removed
 // them; DESIGN.md §4 keeps their numbers.)
