@@ -820,9 +820,12 @@ __global__ void __launch_bounds__(64) k_customer_walk_ev(
     static_assert((kRing & (kRing - 1)) == 0 && kRing % kChunk == 0, "power-of-two ring of whole chunks");
     constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;
     constexpr int kRingEl = kRing * S_MAX;
+    // FDX_WALK_EVENT == 2: each add stores its row's outputs straight to global memory (no LDS
+    // staging of the outputs: 12 KiB less LDS per wave, stores scattered over the lanes' rows)
+    constexpr bool kDirect = FDX_WALK_EVENT == 2;
     __shared__ double r_amt[kRingEl];
     __shared__ int32_t s_st[kChunk * kWave];   // row j's window start of lane l at [j * 64 + l]; then its NB
-    __shared__ double s_val[kChunk * kWave];   // row j's output value of lane l
+    __shared__ double s_val[kDirect ? 1 : kChunk * kWave];   // row j's output value of lane l
     const int lane = threadIdx.x;
     const int64_t g = blockIdx.x / P;
     const int h = (int)(blockIdx.x % P);
@@ -925,9 +928,14 @@ __global__ void __launch_bounds__(64) k_customer_walk_ev(
                     }
                 }
                 if (add) {
-                    s_st[j * kWave + lane] = nobs;
-                    s_val[j * kWave + lane] = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum)
-                                                        : __builtin_nan("");
+                    const double ov = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
+                    if constexpr (kDirect) {
+                        nb[(int64_t)t * S] = nobs;
+                        sm[(int64_t)t * S] = ov;
+                    } else {
+                        s_st[j * kWave + lane] = nobs;
+                        s_val[j * kWave + lane] = ov;
+                    }
                     tail = st;
                     ++j;
                     if (j < jn) st = s_st[j * kWave + lane];
@@ -939,11 +947,13 @@ __global__ void __launch_bounds__(64) k_customer_walk_ev(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if constexpr (!kDirect) {
 #pragma unroll
-        for (int jj = 0; jj < kChunk; ++jj) {
-            if (t0 + jj < L) {
-                nb[(int64_t)(t0 + jj) * S] = s_st[jj * kWave + lane];
-                sm[(int64_t)(t0 + jj) * S] = s_val[jj * kWave + lane];
+            for (int jj = 0; jj < kChunk; ++jj) {
+                if (t0 + jj < L) {
+                    nb[(int64_t)(t0 + jj) * S] = s_st[jj * kWave + lane];
+                    sm[(int64_t)(t0 + jj) * S] = s_val[jj * kWave + lane];
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
