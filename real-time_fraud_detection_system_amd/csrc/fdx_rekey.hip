@@ -123,82 +123,14 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_apply(const uint32_t *in, i
 
 int64_t scan_partials_count(int64_t m) { return ceil_div(m, kScanChunk); }
 
-// Single-pass form (compile-time A/B: FDX_SCAN_1PASS): one launch instead of three -- chained
-// scan with decoupled look-back (Merrill & Garland).  A block takes the next chunk by ticket
-// (dispatch order: every smaller chunk is held by a block already running, so the look-back
-// always ends), publishes its aggregate, looks back to the nearest inclusive prefix, publishes
-// its own.  A status word holds flag and value in one 8-byte relaxed agent-scope atomic (its
-// own payload: no separate bytes to order across XCDs, MI355X_MICROARCH.md hand-off table);
-// the status array and ticket are zeroed by one memset before the launch.
-#ifndef FDX_SCAN_1PASS
-#define FDX_SCAN_1PASS 0
-#endif
-constexpr uint64_t kScanAgg = 1ull << 62, kScanPre = 2ull << 62;
-__global__ void __launch_bounds__(kScanBlock) k_scan_1pass(uint32_t *data, int64_t m,
-                                                            unsigned long long *__restrict__ status,
-                                                            unsigned int *__restrict__ ticket) {
-    __shared__ uint32_t s_chunk, s_prefix;
-    if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t c = s_chunk;
-    const int64_t base = c * kScanChunk + (int64_t)threadIdx.x * kScanItems;
-    uint32_t v[kScanItems];
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        v[k] = base + k < m ? data[base + k] : 0u;
-        s += v[k];
-    }
-    uint32_t tot;
-    uint32_t ex = block_excl_scan(s, &tot);
-    if (threadIdx.x == 0) {
-        uint32_t pre = 0;
-        if (c == 0) {
-            __hip_atomic_store(&status[0], kScanPre | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&status[c], kScanAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = c - 1;; --j) {
-                unsigned long long w;
-                do {
-                    w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } while ((w >> 62) == 0);
-                pre += (uint32_t)w;
-                if ((w >> 62) == 2) break;
-            }
-            __hip_atomic_store(&status[c], kScanPre | (uint32_t)(pre + tot), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_prefix = pre;
-    }
-    __syncthreads();
-    ex += s_prefix;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        if (base + k < m) data[base + k] = ex;
-        ex += v[k];
-    }
-}
-
-// scratch words of exclusive_scan (uint32): the three-kernel form's partials, or the
-// single-pass form's 8-byte status words + ticket
-int64_t scan_scratch_words(int64_t m) {
-    const int64_t P = scan_partials_count(m);
-    return std::max<int64_t>(P + 1, 2 * (P + 2));
-}
+// scratch words of exclusive_scan (uint32): the partials.  (Round 4 measured a single-launch
+// decoupled look-back scan in their place: bit-identical and no faster in the re-keys -- 0.591 /
+// 0.513 vs 0.555 / 0.504 ms alone, profiles/r04h_bench*.json -- and removed it.)
+int64_t scan_scratch_words(int64_t m) { return scan_partials_count(m) + 1; }
 
 int exclusive_scan(uint32_t *data, int64_t m, uint32_t *part, hipStream_t st) {
     if (m == 0) return FDX_OK;
     const int64_t P = scan_partials_count(m);
-    if (FDX_SCAN_1PASS) {
-        // status words 8-byte aligned inside the scratch
-        uint32_t *al = reinterpret_cast<uint32_t *>((reinterpret_cast<uintptr_t>(part) + 7) & ~(uintptr_t)7);
-        auto *status = reinterpret_cast<unsigned long long *>(al);
-        auto *ticket = reinterpret_cast<unsigned int *>(status + P);
-        FDX_HIP(hipMemsetAsync(status, 0, sizeof(unsigned long long) * (size_t)P + sizeof(unsigned int), st));
-        hipLaunchKernelGGL(k_scan_1pass, dim3((unsigned)P), dim3(kScanBlock), 0, st, data, m, status, ticket);
-        FDX_LAUNCHED("k_scan_1pass");
-        return FDX_OK;
-    }
     hipLaunchKernelGGL(k_scan_partials, dim3((unsigned)P), dim3(kScanBlock), 0, st, data, m, part);
     FDX_LAUNCHED("k_scan_partials");
     hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(kScanBlock), 0, st, part, P);

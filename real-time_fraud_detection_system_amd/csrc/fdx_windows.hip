@@ -797,171 +797,6 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     }
 }
 
-// k_customer_walk in EVENT form (compile-time A/B: FDX_WALK_EVENT).  The row-synchronous walk
-// above runs, for every row, as many removal sub-iterations as its busiest lane needs (6.5 per
-// row at config 2 where a lane needs ~1).  Here each lane runs its own event sequence -- for
-// row t: the removals of rows [tail, start(t)), then the add of row t (or, when start(t) >= t,
-// pandas' re-initialisation and the add) -- one event per wave iteration, so a chunk takes as
-// many iterations as its busiest LANE has events, not the sum over rows of per-row maxima.
-// The same float64 operations in the same order per lane (remove: y = -a - c_rem, add:
-// y = v - c_add; t = sum + y; c = (t - sum) - y; sum = t), so the outputs are bit-identical.
-// Per chunk the lane's 16 window starts are staged in LDS (a lane reads the start of ITS
-// current row) and the outputs go back through LDS (the count over the consumed start), then
-// leave as the row-synchronous kernel's coalesced stores.
-#ifndef FDX_WALK_EVENT
-#define FDX_WALK_EVENT 0
-#endif
-template <int S_MAX, int kRing, int P>
-__global__ void __launch_bounds__(64) k_customer_walk_ev(
-    const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
-    const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
-    int32_t *__restrict__ nb_out, double *__restrict__ sum_out, const int32_t *__restrict__ starts,
-    int32_t lg_min = 0, int32_t lg_max = INT32_MAX) {
-    static_assert((kRing & (kRing - 1)) == 0 && kRing % kChunk == 0, "power-of-two ring of whole chunks");
-    constexpr int kPer = (kChunk * S_MAX + kWave - 1) / kWave;
-    constexpr int kRingEl = kRing * S_MAX;
-    // FDX_WALK_EVENT == 2: each add stores its row's outputs straight to global memory (no LDS
-    // staging of the outputs: 12 KiB less LDS per wave, stores scattered over the lanes' rows)
-    constexpr bool kDirect = FDX_WALK_EVENT == 2;
-    __shared__ double r_amt[kRingEl];
-    __shared__ int32_t s_st[kChunk * kWave];   // row j's window start of lane l at [j * 64 + l]; then its NB
-    __shared__ double s_val[kDirect ? 1 : kChunk * kWave];   // row j's output value of lane l
-    const int lane = threadIdx.x;
-    const int64_t g = blockIdx.x / P;
-    const int h = (int)(blockIdx.x % P);
-    const int Sh = (S + P - 1) / P, seg0 = h * Sh;
-    const int64_t s0 = sorder[g * S];
-    const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
-    if (Lg < lg_min || Lg >= lg_max) return;
-    if (seg0 >= S || g * S + seg0 >= n_seg) return;
-    const int Sw = min(Sh, (int)min<int64_t>(S - seg0, n_seg - g * S - seg0));
-    const int64_t sw0 = sorder[g * S + seg0];
-    const int32_t Lw = (int32_t)(seg_off[sw0 + 1] - seg_off[sw0]);
-    const int l = lane / n_win, wi = lane - l * n_win;
-    const bool active = l < Sw;
-    const int64_t s = active ? sorder[g * S + seg0 + l] : 0;
-    const int32_t L = active ? (int32_t)(seg_off[s + 1] - seg_off[s]) : 0;
-    const int64_t gbase = goff[g];
-    const double *g_amt = iamt + gbase + seg0 + l;
-    int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + seg0 + l;
-    double *sm = sum_out + (int64_t)wi * n_slots + gbase + seg0 + l;
-    int32_t e_src[kPer], e_ring[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const int e = lane + j * kWave;
-        const int tt = e / Sw, ll = e - tt * Sw;
-        e_src[j] = tt * S + ll;
-        e_ring[j] = tt * S_MAX + ll;
-    }
-    double pam[kPer];
-    int32_t pst[kChunk];
-    auto fetch = [&](int32_t t0) {
-        const int n_el = min(kChunk, Lw - t0) * Sw;
-        const int64_t src0 = gbase + (int64_t)t0 * S + seg0;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int e = lane + j * kWave;
-            if (e < n_el) pam[j] = iamt[src0 + e_src[j]];
-        }
-        if (starts) {
-            const int32_t *sp = starts + (int64_t)wi * n_slots + gbase + (int64_t)(seg0 + l) * Lg + t0;
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j)
-                if (t0 + j < L) pst[j] = sp[j];
-        } else {
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j)
-                if (t0 + j < L) pst[j] = nb[(int64_t)(t0 + j) * S];
-        }
-    };
-    double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
-    int32_t nobs = 0, nsame = 0, tail = 0;
-    if (Lw > 0) fetch(0);
-    for (int32_t t0 = 0; t0 < Lw; t0 += kChunk) {
-        // commit the chunk's amounts to the ring and its starts to LDS (registers of the prefetch)
-        {
-            const int n_el = min(kChunk, Lw - t0) * Sw;
-            const int ring0 = (t0 & (kRing - 1)) * S_MAX;
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-                const int e = lane + j * kWave;
-                if (e < n_el) r_amt[ring0 + e_ring[j]] = pam[j];
-            }
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j) s_st[j * kWave + lane] = pst[j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (t0 + kChunk < Lw) fetch(t0 + kChunk);  // in flight while this chunk is walked
-        const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
-        const int32_t jn = max(0, min(kChunk, L - t0));  // this lane's rows in the chunk
-        int32_t j = 0;
-        int32_t st = jn > 0 ? s_st[lane] : 0;
-        while (__any(j < jn)) {
-            if (j < jn) {
-                const int32_t t = t0 + j;
-                const bool reset = st >= t;
-                const bool add = reset || tail >= st;
-                const int32_t row = add ? t : tail;
-                double a;
-                if (row < oldest)  // a removal older than the ring (rare): from global memory
-                    a = g_amt[(int64_t)row * S];
-                else
-                    a = r_amt[(row & (kRing - 1)) * S_MAX + l];
-                if (reset) {  // start[i] >= end[i-1] (or i == 0): pandas re-initialises
-                    sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = a;
-                }
-                if (a == a) {  // Kahan add (c_add) or remove (c_rem)
-                    const double y = (add ? a : -a) - (add ? c_add : c_rem);
-                    const double tt = sum + y;
-                    const double cn = (tt - sum) - y;
-                    sum = tt;
-                    if (add) {
-                        c_add = cn;
-                        nobs += 1;
-                        nsame = (a == prev) ? nsame + 1 : 1;
-                        prev = a;
-                    } else {
-                        c_rem = cn;
-                        nobs -= 1;
-                    }
-                }
-                if (add) {
-                    const double ov = nobs >= 1 ? ((nsame >= nobs) ? prev * (double)nobs : sum) : __builtin_nan("");
-                    if constexpr (kDirect) {
-                        nb[(int64_t)t * S] = nobs;
-                        sm[(int64_t)t * S] = ov;
-                    } else {
-                        s_st[j * kWave + lane] = nobs;
-                        s_val[j * kWave + lane] = ov;
-                    }
-                    tail = st;
-                    ++j;
-                    if (j < jn) st = s_st[j * kWave + lane];
-                } else {
-                    ++tail;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if constexpr (!kDirect) {
-#pragma unroll
-            for (int jj = 0; jj < kChunk; ++jj) {
-                if (t0 + jj < L) {
-                    nb[(int64_t)(t0 + jj) * S] = s_st[jj * kWave + lane];
-                    sm[(int64_t)(t0 + jj) * S] = s_val[jj * kWave + lane];
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-
 // ------------------------------------------------ customer windows, scan mode
 // The averages from float64 prefix sums instead of pandas' sequential Kahan add/remove
 // recurrence: fully parallel, one wave per segment.  Counts are exact; sums agree with pandas
@@ -2119,8 +1954,7 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     // blocks per CU); the class boundary is kWalkSplitRows.
     constexpr int split = kWalkSplitRows;
 #define FDX_WALK(SM, RING, P, STREAM, LO, HI)                                                                 \
-    hipLaunchKernelGGL((FDX_WALK_EVENT ? k_customer_walk_ev<SM, RING, P> : k_customer_walk<SM, RING, P>),        \
-                       dim3((unsigned)(n_groups * (P))), dim3(64), 0, STREAM,                                   \
+    hipLaunchKernelGGL((k_customer_walk<SM, RING, P>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, STREAM,  \
                        iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, \
                        LO, HI);                                                                                \
     FDX_LAUNCHED("k_customer_walk")
