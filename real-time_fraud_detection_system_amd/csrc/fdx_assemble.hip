@@ -265,6 +265,32 @@ __global__ void __launch_bounds__(256) k_scale(const double *__restrict__ X, int
     }
 }
 
+// The weekend / night flags of a nanosecond timestamp, with the floor divisions of pandas'
+// dt accessors (feature_transformation.ipynb's is_weekend / is_night; fraud_detection.py's
+// dayofweek / hour for FDX_FLAGS_SPARK).  floor(t / 1 day) = floor(floor(t / 1 s) / 86,400 s) and
+// the hour likewise, so one 64-bit division to whole seconds, then 32-bit day / hour / weekday
+// arithmetic while the seconds fit (1901-2038), the 64-bit form otherwise: the same values.
+__device__ __forceinline__ void day_flags(int64_t t, int32_t flags_mode, bool &we, bool &ni) {
+    int64_t sec = t / 1000000000LL;
+    if (sec * 1000000000LL != t && t < 0) --sec;
+    int32_t hour, wd;
+    if (sec >= INT32_MIN && sec <= INT32_MAX) {
+        const int32_t s32 = (int32_t)sec;
+        int32_t day = s32 / 86400;
+        if (day * 86400 != s32 && s32 < 0) --day;
+        hour = (s32 - day * 86400) / 3600;
+        wd = (day + 3) % 7;
+    } else {
+        int64_t day = sec / 86400;
+        if (day * 86400 != sec && sec < 0) --day;
+        hour = (int32_t)((sec - day * 86400) / 3600);
+        wd = (int32_t)((day + 3) % 7);
+    }
+    if (wd < 0) wd += 7;
+    we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
+    ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+}
+
 __device__ __forceinline__ float zval(double x, const double *mean, const double *scale, int f) {
     if (mean) x = x - mean[f];
     if (scale) x = x / scale[f];
@@ -346,7 +372,6 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     const int64_t *__restrict__ term_rec, int64_t n, int32_t W, int32_t flags_mode, int32_t val_is_sum,
     const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
     int32_t *__restrict__ nan_flag, RankTab rt) {
-    constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     const int nf = 3 + 4 * W;
     __shared__ float s_smp[RANK ? kMaxRankSamples : 1];
     __shared__ uint16_t s_itab[RANK ? 16 * kIntTab : 1];
@@ -372,14 +397,8 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
             }
             continue;
         }
-        const int64_t t = cts[i];
-        int64_t day = t / kDay;
-        if (t % kDay != 0 && t < 0) --day;
-        const int64_t hour = (t - day * kDay) / kHour;
-        int64_t wd = (day + 3) % 7;
-        if (wd < 0) wd += 7;
-        const bool we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
-        const bool ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+        bool we, ni;
+        day_flags(cts[i], flags_mode, we, ni);
         if constexpr (RANK) {
             // flags and window counts: integer rank table; amount, averages and risks: search
             uint32_t q[16];
@@ -502,7 +521,8 @@ struct PrepRow {
     double a;
     int32_t c[3];
     double cv[3];
-    int64_t tw[3];
+    int64_t tw[3];  // the terminal count words: the wide record, or the compact one decoded (decode_tw)
+    longlong2 raw;  // the compact record as loaded (decoded when the row is consumed)
     int32_t r;
 };
 
@@ -516,14 +536,35 @@ struct PrepRow {
 // FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
 // input row / at its slot, stored as soon as the row's values are loaded (the record's registers
 // die before the rank search; kept to the end, 15 VGPRs spilled)
-template <int EMIT>
+// Loads of the NEXT row are issued at the top of each iteration and consumed one iteration
+// later; nothing in that load phase may wait on a load (a wait covers every older load, the
+// prefetch included: with the compact record's overflow branch and a runtime term_inv select
+// in it, the r03 kernel waited twice per row on HBM round trips -- vmcnt(0) -- before doing the
+// current row).  So the record is loaded raw and decoded when consumed (COMPACT), and the
+// term_inv indirection (TINV, the multi-GPU reply records) runs one more iteration ahead.
+template <bool COMPACT>
+__device__ __forceinline__ void decode_tw(const int64_t *rec, PrepRow &L) {
+    if constexpr (COMPACT) {
+        if (L.raw.x < 0) {  // a count past 2^21 - 1: its full record in the overflow area (rare)
+            const int64_t *wide = rec + (L.raw.x & INT64_MAX);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) L.tw[w] = wide[w];
+        } else {
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+                L.tw[w] = term_word((int32_t)((L.raw.x >> (kCompactBits * w)) & kCompactMax),
+                                    (int32_t)((L.raw.y >> (kCompactBits * w)) & kCompactMax));
+        }
+    }
+}
+
+template <int EMIT, bool COMPACT, bool TINV, int ORD>
 __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
     const double *__restrict__ mean, const double *__restrict__ scale, void *__restrict__ z,
     int32_t *__restrict__ nan_flag, RankTab rt, char *__restrict__ feat, int64_t fcap) {
-    constexpr int64_t kDay = 86400LL * 1000000000LL, kHour = 3600LL * 1000000000LL;
     constexpr int W = 3, nf = 15;
     static_assert(sizeof(fdx_feature_row) == 80, "5 x 16-byte stores per feature record");
     __shared__ float s_e[kMaxRankSamples];  // Eytzinger sample tables (RankTab::etab)
@@ -533,48 +574,40 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     __syncthreads();
     const int e_lmax = max(max(rt.elev[0], rt.elev[1]), max(rt.elev[2], rt.elev[3]));
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const bool rec16 = ((uintptr_t)term_rec & 15) == 0;  // uniform
     auto row_of = [&](int64_t j) -> int32_t { return j < n ? (cust_perm ? cust_perm[j] : (int32_t)j) : -1; };
-    auto load = [&](int64_t j, int32_t r, PrepRow &L) {
+    auto rec_of = [&](int32_t r) -> int64_t { return TINV ? (r >= 0 ? (int64_t)term_inv[r] : -1) : (int64_t)r; };
+    // issues every load of slot j (row r, record q) and waits on none of them
+    auto load = [&](int64_t j, int32_t r, int64_t q, PrepRow &L) {
         L.r = r;
-        if (j >= n || r < 0) {  // defined values: every lane runs the row arithmetic (quad rounds)
+        const bool ok = j < n && r >= 0;
+        const int64_t jj = ok ? j : 0, qq = ok ? q : 0;  // defined values: every lane runs the row arithmetic
+        L.t = cts[jj];
+        L.a = camt[jj];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            L.c[w] = cnb[(int64_t)w * n + jj];
+            L.cv[w] = cval[(int64_t)w * n + jj];
+        }
+        if constexpr (COMPACT) {
+            L.raw = *reinterpret_cast<const longlong2 *>(term_rec + 2 * ((ORD & 16) ? (int64_t)(threadIdx.x & 63) : qq));
+        } else {
+#pragma unroll
+            for (int w = 0; w < W; ++w) L.tw[w] = term_rec[qq * W + w];
+        }
+    };
+    auto settle = [&](int64_t j, PrepRow &L) {  // the consume side: dummies for dead lanes, decode
+        if (!(j < n && L.r >= 0)) {
             L.t = 0;
             L.a = 0.0;
+            L.raw = make_longlong2(0, 0);
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 L.c[w] = 1;
                 L.cv[w] = 0.0;
                 L.tw[w] = 0;
             }
-            return;
         }
-        L.t = cts[j];
-        L.a = camt[j];
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            L.c[w] = cnb[(int64_t)w * n + j];
-            L.cv[w] = cval[(int64_t)w * n + j];
-        }
-        const int64_t q_ = term_inv ? term_inv[r] : r;
-        const int64_t *src = term_rec + q_ * W;
-        if (val_is_sum & 4) {
-            compact_load(term_rec, q_, L.tw);
-        } else if (rec16) {  // the 24-byte record in two loads (16-byte aligned pair first or second)
-            if ((q_ & 1) == 0) {
-                const longlong2 p = *reinterpret_cast<const longlong2 *>(src);
-                L.tw[0] = p.x;
-                L.tw[1] = p.y;
-                L.tw[2] = src[2];
-            } else {
-                const longlong2 p = *reinterpret_cast<const longlong2 *>(src + 1);
-                L.tw[0] = src[0];
-                L.tw[1] = p.x;
-                L.tw[2] = p.y;
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < W; ++w) L.tw[w] = src[w];
-        }
+        decode_tw<COMPACT>(term_rec, L);
     };
     // wave-uniform loop (stride and the wave's first slot are multiples of 64): every lane of a
     // wave runs each iteration, so the quads of k_seg_count_quad stay whole; lanes past n and
@@ -582,21 +615,25 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     const int lane = threadIdx.x & (kWave - 1);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     PrepRow cur;
-    load(i, row_of(i), cur);
-    int32_t r_next = row_of(i + stride);
+    {
+        const int32_t r0 = row_of(i);
+        load(i, r0, rec_of(r0), cur);
+    }
+    int32_t r1 = row_of(i + stride), r2 = row_of(i + 2 * stride);  // slots one and two ahead
+    int64_t q1 = rec_of(r1);
     for (; i - lane < n; i += stride) {
         PrepRow nxt;
-        load(i + stride, r_next, nxt);  // next row's loads in flight during this row
-        r_next = row_of(i + 2 * stride);
+        auto prefetch = [&]() {
+            load(i + stride, r1, q1, nxt);  // next row's loads in flight during this row
+            q1 = rec_of(r2);                // (r2 arrived during the previous row)
+            r1 = r2;
+            r2 = row_of(i + 3 * stride);
+        };
+        if constexpr ((ORD & 3) == 0) prefetch();
+        settle(i, cur);
         const bool live = i < n && cur.r >= 0;
-        const int64_t t = cur.t;
-        int64_t day = t / kDay;
-        if (t % kDay != 0 && t < 0) --day;
-        const int64_t hour = (t - day * kDay) / kHour;
-        int64_t wd = (day + 3) % 7;
-        if (wd < 0) wd += 7;
-        const bool we = flags_mode == FDX_FLAGS_NOTEBOOK ? wd >= 5 : (((wd + 1) % 7) + 1) >= 5;
-        const bool ni = flags_mode == FDX_FLAGS_NOTEBOOK ? hour <= 6 : hour >= 20;
+        bool we, ni;
+        day_flags(cur.t, flags_mode, we, ni);
         float v[16];
         uint32_t q[16];
 #pragma unroll
@@ -617,7 +654,7 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
         q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
         v[0] = zval(cur.a, mean, scale, 0);
         bool nan = v[0] != v[0];
-        if constexpr (EMIT != 0) {
+        auto emit = [&]() {
             // the featurized row: a record at its input row (one random 80-byte write), or the
             // columns at its slot (consecutive lanes, consecutive elements: every store of a wave
             // is whole lines; an 80-byte record per slot, 5 strided 16-byte stores, measured
@@ -653,7 +690,8 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                     dst[4] = make_uint4(u32(rk[2], 0), u32(rk[2], 1), fl, (uint32_t)cur.r);
                 }
             }
-        }
+        };
+        if constexpr (EMIT != 0 && (ORD & 3) < 2) emit();
         uint16_t rq[W];
         bool rat_ok[W];
 #pragma unroll
@@ -668,12 +706,12 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
             const int fr_ = 4 + 2 * W + 2 * w;
             rat_ok[w] = tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb;
             // unconditional read (index clamped to 0 when the table does not apply)
-            rq[w] = rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
+            rq[w] = (ORD & 8) ? (uint16_t)tnb : rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
         }
         // two-level search of the 4 continuous features: the Eytzinger descent over the LDS
         // samples (cs = #samples < v: k - 2^L after L levels), then all 4 segments at once
         int32_t ek[4] = {1, 1, 1, 1};
-        for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
+        for (int l = 0; l < ((ORD & 32) ? 0 : e_lmax); ++l) {  // uniform trip count
 #pragma unroll
             for (int s = 0; s < 4; ++s)
                 if (l < rt.elev[s]) ek[s] = 2 * ek[s] + (s_e[rt.eoff[s] + ek[s]] < v[kW3Search[s]] ? 1 : 0);
@@ -700,7 +738,7 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                     const int f = kW3Search[s];
                     const int32_t si = quad_bcast<K>(sidx[s]);
                     vk[s] = __int_as_float(quad_bcast<K>(__float_as_int(v[f])));
-                    w4[s] = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)si * 16)[qj];
+                    w4[s] = (ORD & 4) ? make_float4(vk[s], vk[s], vk[s], vk[s]) : reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)si * 16)[qj];
                 }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -710,10 +748,44 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                     kc[s] = qj == K ? c : kc[s];
                 }
             };
-            round(std::integral_constant<int, 0>{});
-            round(std::integral_constant<int, 1>{});
-            round(std::integral_constant<int, 2>{});
-            round(std::integral_constant<int, 3>{});
+            if constexpr ((ORD & 3) == 0) {
+                round(std::integral_constant<int, 0>{});
+                round(std::integral_constant<int, 1>{});
+                round(std::integral_constant<int, 2>{});
+                round(std::integral_constant<int, 3>{});
+            } else {
+                // the 16 segment loads first, then the next row's loads: waiting on a segment
+                // (vmcnt counts in issue order) then never waits on the next row's HBM reads
+                float4 w4[4][4];
+                auto issue = [&](auto kk) {
+                    constexpr int K = decltype(kk)::value;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const int32_t si = quad_bcast<K>(sidx[s]);
+                        w4[K][s] = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[kW3Search[s]] + (int64_t)si * 16)[qj];
+                    }
+                };
+                auto consume = [&](auto kk) {
+                    constexpr int K = decltype(kk)::value;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const float vk = __int_as_float(quad_bcast<K>(__float_as_int(v[kW3Search[s]])));
+                        uint32_t c = (uint32_t)(w4[K][s].x < vk) + (uint32_t)(w4[K][s].y < vk) +
+                                     (uint32_t)(w4[K][s].z < vk) + (uint32_t)(w4[K][s].w < vk);
+                        c = quad_sum(c);
+                        kc[s] = qj == K ? c : kc[s];
+                    }
+                };
+                issue(std::integral_constant<int, 0>{});
+                issue(std::integral_constant<int, 1>{});
+                issue(std::integral_constant<int, 2>{});
+                issue(std::integral_constant<int, 3>{});
+                prefetch();
+                consume(std::integral_constant<int, 0>{});
+                consume(std::integral_constant<int, 1>{});
+                consume(std::integral_constant<int, 2>{});
+                consume(std::integral_constant<int, 3>{});
+            }
         } else {
             float4 sg[4][4];
 #pragma unroll
@@ -762,11 +834,21 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
             dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
                           : make_uint4(0, 0, 0, 0);
         }
+        if constexpr (EMIT != 0 && (ORD & 3) == 2) emit();
         cur = nxt;
     }
 }
 
 }  // namespace
+
+// study switch FDX_ZFILL_ORDER (tools/zfill_ab.py; results of 4..60 are NOT the features): 1, 2 =
+// k_zfill_grouped_w3 with the next row's loads issued after the segment loads (2: the feature
+// record stored last); 4 / 8 / 16 / 32 = without the segment loads / the ratio-table loads / the
+// term-record gather (one line per wave) / the LDS sample descent; 60 = without all four
+static int zfill_order() {
+    const char *e = getenv("FDX_ZFILL_ORDER");
+    return e ? atoi(e) : 0;
+}
 
 RankTab rank_tab(const fdx_forest_s *F) {
     RankTab rt;
@@ -955,16 +1037,33 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
     const unsigned grid = stream_grid(n, 256);
     const RankTab rt = rank_tab(F);
     if (rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat && rt.etab) {
-#define FDX_ZFILL_W3(E)                                                                                          \
-    hipLaunchKernelGGL(k_zfill_grouped_w3<E>, dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d, cust_nb_d,   \
-                       cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum, F->mean_d, \
-                       F->scale_d, (void *)z, flag, rt, reinterpret_cast<char *>(rows_out_d), out_cap)
+#define FDX_ZFILL_W3(E, C, T, O)                                                                                  \
+    hipLaunchKernelGGL((k_zfill_grouped_w3<E, C, T, O>), dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d,     \
+                       cust_nb_d, cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,   \
+                       F->mean_d, F->scale_d, (void *)z, flag, rt, reinterpret_cast<char *>(rows_out_d), out_cap)
+#define FDX_ZFILL_W3_E(E)                                                                                         \
+    do {                                                                                                          \
+        if (cust_val_is_sum & 4) {                                                                                \
+            if (term_inv_d) FDX_ZFILL_W3(E, true, true, 0);                                                       \
+            else if (zfill_order() == 1) FDX_ZFILL_W3(E, true, false, 1);                                         \
+            else if (zfill_order() == 2) FDX_ZFILL_W3(E, true, false, 2);                                         \
+            else if (zfill_order() == 4) FDX_ZFILL_W3(E, true, false, 4);                                         \
+            else if (zfill_order() == 8) FDX_ZFILL_W3(E, true, false, 8);                                         \
+            else if (zfill_order() == 16) FDX_ZFILL_W3(E, true, false, 16);                                       \
+            else if (zfill_order() == 32) FDX_ZFILL_W3(E, true, false, 32);                                       \
+            else if (zfill_order() == 60) FDX_ZFILL_W3(E, true, false, 60);                                       \
+            else FDX_ZFILL_W3(E, true, false, 0);                                                                 \
+        } else {                                                                                                  \
+            if (term_inv_d) FDX_ZFILL_W3(E, false, true, 0); else FDX_ZFILL_W3(E, false, false, 0);               \
+        }                                                                                                         \
+    } while (0)
         if (!rows_out_d)
-            FDX_ZFILL_W3(0);
+            FDX_ZFILL_W3_E(0);
         else if (rows_order == FDX_ROWS_SLOT_ORDER)
-            FDX_ZFILL_W3(FDX_ROWS_SLOT_ORDER);
+            FDX_ZFILL_W3_E(FDX_ROWS_SLOT_ORDER);
         else
-            FDX_ZFILL_W3(FDX_ROWS_INPUT_ORDER);
+            FDX_ZFILL_W3_E(FDX_ROWS_INPUT_ORDER);
+#undef FDX_ZFILL_W3_E
 #undef FDX_ZFILL_W3
         FDX_LAUNCHED("k_zfill_grouped_w3");
         return FDX_OK;
