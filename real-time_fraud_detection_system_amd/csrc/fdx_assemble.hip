@@ -489,32 +489,22 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
     }
 }
 
-// k_zfill_grouped for the reference's layout (W = 3, rank rows, ratio table, 16-float search
-// segments), restructured for memory-level parallelism.  The general kernel is bound by
+// k_zfill_grouped for the reference's layout (W = 3, rank rows, ratio table, the four searched
+// features' S-trees), restructured for memory-level parallelism.  The general kernel is bound by
 // dependent round trips per row at 3 waves/SIMD (cust_perm -> term record -> ratio table;
 // amount/average -> one search segment per feature, each behind its own branch).  Here the
 // next row's loads (scoring-order columns + its term record, whose row index is fetched two
 // rows ahead) are in flight while the current row is ranked, and the current row's four
 // segment reads and three ratio-table reads are issued together, unconditionally (clamped
-// addresses; the host pads useg by one segment), so a row costs about one round trip.
-// Results are bit-identical to k_zfill_grouped<16, true> (same arithmetic, same fallbacks).
-// A/B switch (compile time): k_zfill_grouped_w3's segment counts by lane quads (1) or per lane (0)
-#ifndef FDX_ZFILL_QUAD
-#define FDX_ZFILL_QUAD 1
-#endif
-constexpr bool kZfillQuad = FDX_ZFILL_QUAD != 0;
-
-// lane K of each quad of lanes, to all 4 (DPP quad_perm broadcast; every lane of the wave active)
-template <int K>
-__device__ __forceinline__ int32_t quad_bcast(int32_t x) {
-    return __builtin_amdgcn_update_dpp(0, x, K * 0x55, 0xF, 0xF, false);
-}
-// the sum over each quad of lanes, in all 4 (DPP quad_perm [1,0,3,2] then [2,3,0,1])
-__device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
-    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)c, 0xB1, 0xF, 0xF, false);
-    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)c, 0x4E, 0xF, 0xF, false);
-    return c;
-}
+// addresses; the host pads useg by one segment).
+// Search of the four continuous features (amount, the three averages): the descent of an
+// S-tree in LDS -- every kW3Gap-th threshold in 8-key nodes, two ds_read_b128 per level, 4
+// levels for <= 6,560 samples (the r03 form: an Eytzinger descent over every 16th threshold, 11
+// dependent ds_read_b32 levels, then 64-byte segments read by lane quads) -- then one 16-byte
+// read of the kW3Gap thresholds the sample count leaves.  One 1,024-thread block per CU (the
+// trees take ~100 KiB of LDS).  Results are bit-identical to k_zfill_grouped<16, true> (same
+// arithmetic, same fallbacks).
+constexpr int kW3Block = 1024;
 
 struct PrepRow {
     int64_t t;
@@ -526,12 +516,6 @@ struct PrepRow {
     int32_t r;
 };
 
-// A/B switch (compile time): minimum waves per SIMD the compiler must fit k_zfill_grouped_w3's
-// registers to (0: the compiler's choice, 156 VGPRs / 3 waves; 4: 128 VGPRs, assembly 1.02-1.09 -> 0.985 ms
-// alone, profiles/r03af_zfill_waves_ab.txt)
-#ifndef FDX_ZFILL_WAVES
-#define FDX_ZFILL_WAVES 4
-#endif
 // EMIT: the featurized table besides the rank rows (fdx_forest_prepare_grouped_rows): 0 = none,
 // FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
 // input row / at its slot, stored as soon as the row's values are loaded (the record's registers
@@ -558,8 +542,8 @@ __device__ __forceinline__ void decode_tw(const int64_t *rec, PrepRow &L) {
     }
 }
 
-template <int EMIT, bool COMPACT, bool TINV, int ORD>
-__global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
+template <int EMIT, bool COMPACT, bool TINV>
+__global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
     const int64_t *__restrict__ cts, const double *__restrict__ camt, const int32_t *__restrict__ cnb,
     const double *__restrict__ cval, const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv,
     const int64_t *__restrict__ term_rec, int64_t n, int32_t flags_mode, int32_t val_is_sum,
@@ -567,10 +551,11 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     int32_t *__restrict__ nan_flag, RankTab rt, char *__restrict__ feat, int64_t fcap) {
     constexpr int W = 3, nf = 15;
     static_assert(sizeof(fdx_feature_row) == 80, "5 x 16-byte stores per feature record");
-    __shared__ float s_e[kMaxRankSamples];  // Eytzinger sample tables (RankTab::etab)
+    __shared__ __align__(16) float s_t[kW3TreeFloats];  // the S-trees (RankTab::etab)
     __shared__ uint16_t s_itab[16 * kIntTab];
     for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
-    for (int e = threadIdx.x; e < rt.n_etab; e += blockDim.x) s_e[e] = rt.etab[e];
+    for (int e = threadIdx.x; e < rt.n_etab / 4; e += blockDim.x)
+        reinterpret_cast<float4 *>(s_t)[e] = reinterpret_cast<const float4 *>(rt.etab)[e];
     __syncthreads();
     const int e_lmax = max(max(rt.elev[0], rt.elev[1]), max(rt.elev[2], rt.elev[3]));
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -589,7 +574,7 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
             L.cv[w] = cval[(int64_t)w * n + jj];
         }
         if constexpr (COMPACT) {
-            L.raw = *reinterpret_cast<const longlong2 *>(term_rec + 2 * ((ORD & 16) ? (int64_t)(threadIdx.x & 63) : qq));
+            L.raw = *reinterpret_cast<const longlong2 *>(term_rec + 2 * qq);
         } else {
 #pragma unroll
             for (int w = 0; w < W; ++w) L.tw[w] = term_rec[qq * W + w];
@@ -623,13 +608,10 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
     int64_t q1 = rec_of(r1);
     for (; i - lane < n; i += stride) {
         PrepRow nxt;
-        auto prefetch = [&]() {
-            load(i + stride, r1, q1, nxt);  // next row's loads in flight during this row
-            q1 = rec_of(r2);                // (r2 arrived during the previous row)
-            r1 = r2;
-            r2 = row_of(i + 3 * stride);
-        };
-        if constexpr ((ORD & 3) == 0) prefetch();
+        load(i + stride, r1, q1, nxt);  // next row's loads in flight during this row
+        q1 = rec_of(r2);                // (r2 arrived during the previous row)
+        r1 = r2;
+        r2 = row_of(i + 3 * stride);
         settle(i, cur);
         const bool live = i < n && cur.r >= 0;
         bool we, ni;
@@ -691,7 +673,7 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
                 }
             }
         };
-        if constexpr (EMIT != 0 && (ORD & 3) < 2) emit();
+        if constexpr (EMIT != 0) emit();
         uint16_t rq[W];
         bool rat_ok[W];
 #pragma unroll
@@ -706,110 +688,42 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
             const int fr_ = 4 + 2 * W + 2 * w;
             rat_ok[w] = tnb >= 0 && tnb < kRatN && tfr >= 0 && tfr <= tnb;
             // unconditional read (index clamped to 0 when the table does not apply)
-            rq[w] = (ORD & 8) ? (uint16_t)tnb : rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
+            rq[w] = rt.rat[rat_ok[w] ? ((int64_t)fr_ * kRatN + tnb) * kRatN + tfr : 0];
         }
-        // two-level search of the 4 continuous features: the Eytzinger descent over the LDS
-        // samples (cs = #samples < v: k - 2^L after L levels), then all 4 segments at once
-        int32_t ek[4] = {1, 1, 1, 1};
-        for (int l = 0; l < ((ORD & 32) ? 0 : e_lmax); ++l) {  // uniform trip count
+        // the 4 continuous features: S-tree descents (cs = #samples < v: the digits c of the
+        // levels in base 9), then the kW3Gap thresholds of the segment the count leaves
+        int32_t ek[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
+        for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (l < rt.elev[s]) {
+                    const float4 *nd = reinterpret_cast<const float4 *>(s_t) + 2 * (rt.eoff[s] + ek[s]);
+                    const float4 a = nd[0], b = nd[1];
+                    const float x = v[kW3Search[s]];
+                    const int32_t c = (int32_t)(a.x < x) + (int32_t)(a.y < x) + (int32_t)(a.z < x) + (int32_t)(a.w < x) +
+                                      (int32_t)(b.x < x) + (int32_t)(b.y < x) + (int32_t)(b.z < x) + (int32_t)(b.w < x);
+                    cs[s] = cs[s] * 9 + c;
+                    ek[s] = ek[s] * 9 + 1 + c;
+                }
+            }
+        }
+        uint32_t kc[4];
+        {
+            float4 sg[4];
 #pragma unroll
             for (int s = 0; s < 4; ++s)
-                if (l < rt.elev[s]) ek[s] = 2 * ek[s] + (s_e[rt.eoff[s] + ek[s]] < v[kW3Search[s]] ? 1 : 0);
-        }
-        int32_t cs[4];
-        uint32_t kc[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) cs[s] = ek[s] - (1 << rt.elev[s]);
-        if constexpr (kZfillQuad) {
-            // a quad of lanes per segment: round K loads lane K's 64-byte segment as 4 x 16 B
-            // (lane j of the quad: bytes 16j..16j+15), so each load instruction touches 16 lines
-            // instead of 64 -- the address unit serves a gather line by line -- and the quad sums
-            // its 4 partial counts (DPP); lane K keeps round K's count
-            const int qj = lane & 3;
-            int32_t sidx[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) sidx[s] = max(cs[s] - 1, 0);
-            auto round = [&](auto kk) {
-                constexpr int K = decltype(kk)::value;
-                float4 w4[4];
-                float vk[4];
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int f = kW3Search[s];
-                    const int32_t si = quad_bcast<K>(sidx[s]);
-                    vk[s] = __int_as_float(quad_bcast<K>(__float_as_int(v[f])));
-                    w4[s] = (ORD & 4) ? make_float4(vk[s], vk[s], vk[s], vk[s]) : reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)si * 16)[qj];
-                }
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    uint32_t c = (uint32_t)(w4[s].x < vk[s]) + (uint32_t)(w4[s].y < vk[s]) +
-                                 (uint32_t)(w4[s].z < vk[s]) + (uint32_t)(w4[s].w < vk[s]);
-                    c = quad_sum(c);
-                    kc[s] = qj == K ? c : kc[s];
-                }
-            };
-            if constexpr ((ORD & 3) == 0) {
-                round(std::integral_constant<int, 0>{});
-                round(std::integral_constant<int, 1>{});
-                round(std::integral_constant<int, 2>{});
-                round(std::integral_constant<int, 3>{});
-            } else {
-                // the 16 segment loads first, then the next row's loads: waiting on a segment
-                // (vmcnt counts in issue order) then never waits on the next row's HBM reads
-                float4 w4[4][4];
-                auto issue = [&](auto kk) {
-                    constexpr int K = decltype(kk)::value;
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const int32_t si = quad_bcast<K>(sidx[s]);
-                        w4[K][s] = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[kW3Search[s]] + (int64_t)si * 16)[qj];
-                    }
-                };
-                auto consume = [&](auto kk) {
-                    constexpr int K = decltype(kk)::value;
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const float vk = __int_as_float(quad_bcast<K>(__float_as_int(v[kW3Search[s]])));
-                        uint32_t c = (uint32_t)(w4[K][s].x < vk) + (uint32_t)(w4[K][s].y < vk) +
-                                     (uint32_t)(w4[K][s].z < vk) + (uint32_t)(w4[K][s].w < vk);
-                        c = quad_sum(c);
-                        kc[s] = qj == K ? c : kc[s];
-                    }
-                };
-                issue(std::integral_constant<int, 0>{});
-                issue(std::integral_constant<int, 1>{});
-                issue(std::integral_constant<int, 2>{});
-                issue(std::integral_constant<int, 3>{});
-                prefetch();
-                consume(std::integral_constant<int, 0>{});
-                consume(std::integral_constant<int, 1>{});
-                consume(std::integral_constant<int, 2>{});
-                consume(std::integral_constant<int, 3>{});
-            }
-        } else {
-            float4 sg[4][4];
+                sg[s] = *reinterpret_cast<const float4 *>(rt.useg + rt.uoff[kW3Search[s]] +
+                                                          (int64_t)max(cs[s] - 1, 0) * kW3Gap);
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const int f = kW3Search[s];
-                const float4 *p = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)max(cs[s] - 1, 0) * 16);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) sg[s][k] = p[k];
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int f = kW3Search[s];
-                uint32_t k = 0;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    k += (uint32_t)(sg[s][e].x < v[f]) + (uint32_t)(sg[s][e].y < v[f]) +
-                         (uint32_t)(sg[s][e].z < v[f]) + (uint32_t)(sg[s][e].w < v[f]);
-                kc[s] = k;
+                const float x = v[kW3Search[s]];
+                kc[s] = (uint32_t)(sg[s].x < x) + (uint32_t)(sg[s].y < x) + (uint32_t)(sg[s].z < x) + (uint32_t)(sg[s].w < x);
             }
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int f = kW3Search[s];
-            const uint32_t r = cs[s] > 0 ? (uint32_t)(cs[s] - 1) * 16u + kc[s] : 0u;
+            const uint32_t r = cs[s] > 0 ? (uint32_t)(cs[s] - 1) * kW3Gap + kc[s] : 0u;
             q[f] = v[f] != v[f] ? 0xFFFFu : r;
         }
 #pragma unroll
@@ -834,20 +748,18 @@ __global__ void __launch_bounds__(256, FDX_ZFILL_WAVES) k_zfill_grouped_w3(
             dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
                           : make_uint4(0, 0, 0, 0);
         }
-        if constexpr (EMIT != 0 && (ORD & 3) == 2) emit();
         cur = nxt;
     }
 }
 
 }  // namespace
 
-// study switch FDX_ZFILL_ORDER (tools/zfill_ab.py; results of 4..60 are NOT the features): 1, 2 =
-// k_zfill_grouped_w3 with the next row's loads issued after the segment loads (2: the feature
-// record stored last); 4 / 8 / 16 / 32 = without the segment loads / the ratio-table loads / the
-// term-record gather (one line per wave) / the LDS sample descent; 60 = without all four
-static int zfill_order() {
-    const char *e = getenv("FDX_ZFILL_ORDER");
-    return e ? atoi(e) : 0;
+// compute units of the current device (grid of the one-block-per-CU kernels)
+static int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 256;
+    return cus > 0 ? cus : 256;
 }
 
 RankTab rank_tab(const fdx_forest_s *F) {
@@ -1036,27 +948,20 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     const unsigned grid = stream_grid(n, 256);
     const RankTab rt = rank_tab(F);
-    if (rank_mode(F) && n_windows == 3 && F->rseg == 16 && rt.rat && rt.etab) {
-#define FDX_ZFILL_W3(E, C, T, O)                                                                                  \
-    hipLaunchKernelGGL((k_zfill_grouped_w3<E, C, T, O>), dim3(grid), dim3(256), 0, st, cust_ts_d, cust_amount_d,     \
+    if (rank_mode(F) && n_windows == 3 && rt.rat && rt.etab) {
+#define FDX_ZFILL_W3(E, C, T)                                                                                     \
+    hipLaunchKernelGGL((k_zfill_grouped_w3<E, C, T>), dim3(grid_w3), dim3(kW3Block), 0, st, cust_ts_d, cust_amount_d, \
                        cust_nb_d, cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, cust_val_is_sum,   \
                        F->mean_d, F->scale_d, (void *)z, flag, rt, reinterpret_cast<char *>(rows_out_d), out_cap)
 #define FDX_ZFILL_W3_E(E)                                                                                         \
     do {                                                                                                          \
         if (cust_val_is_sum & 4) {                                                                                \
-            if (term_inv_d) FDX_ZFILL_W3(E, true, true, 0);                                                       \
-            else if (zfill_order() == 1) FDX_ZFILL_W3(E, true, false, 1);                                         \
-            else if (zfill_order() == 2) FDX_ZFILL_W3(E, true, false, 2);                                         \
-            else if (zfill_order() == 4) FDX_ZFILL_W3(E, true, false, 4);                                         \
-            else if (zfill_order() == 8) FDX_ZFILL_W3(E, true, false, 8);                                         \
-            else if (zfill_order() == 16) FDX_ZFILL_W3(E, true, false, 16);                                       \
-            else if (zfill_order() == 32) FDX_ZFILL_W3(E, true, false, 32);                                       \
-            else if (zfill_order() == 60) FDX_ZFILL_W3(E, true, false, 60);                                       \
-            else FDX_ZFILL_W3(E, true, false, 0);                                                                 \
+            if (term_inv_d) FDX_ZFILL_W3(E, true, true); else FDX_ZFILL_W3(E, true, false);                       \
         } else {                                                                                                  \
-            if (term_inv_d) FDX_ZFILL_W3(E, false, true, 0); else FDX_ZFILL_W3(E, false, false, 0);               \
+            if (term_inv_d) FDX_ZFILL_W3(E, false, true); else FDX_ZFILL_W3(E, false, false);                     \
         }                                                                                                         \
     } while (0)
+        const unsigned grid_w3 = stream_grid(n, kW3Block, device_cus());
         if (!rows_out_d)
             FDX_ZFILL_W3_E(0);
         else if (rows_order == FDX_ROWS_SLOT_ORDER)

@@ -443,6 +443,58 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
+// A/B switch (compile time): the u32 row planes written by ds_write_addtid_b32 (1) or ds_write_b32 (0)
+#ifndef FDX_STAGE_ADDTID
+#define FDX_STAGE_ADDTID 1
+#endif
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// The 15 u32 plane words of row slot r * BLOCK + tid (rank << 16, NaN 0xFFFFFFFF).  With
+// ds_write_addtid_b32 (address = M0 + offset + 4 * lane; no address VGPR) a store moves 4 B per
+// lane in 2 LDS cycles, half of ds_write_b32's 4: the planes are re-staged for every 1,024-row
+// tile, 15 stores per lane against ~220 walk reads.  The kernel's code uses M0 nowhere else.
+template <int BLOCK>
+__device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uint32_t (&w)[8]) {
+    uint32_t x[15];
+#pragma unroll
+    for (int f = 0; f < 15; ++f) {
+        const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
+        x[f] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+    }
+#if FDX_STAGE_ADDTID
+    static_assert(14 * kRankPlaneRows * 4 < 65536, "plane offsets fit the 16-bit instruction offset");
+    const uint32_t b = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(lds_u32 *)(s_x + r * BLOCK + (threadIdx.x & ~63u)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 1\n\t"  // M0 write -> LDS add-TID: wait states (without them the first store used the old M0)
+        "ds_write_addtid_b32 %1\n\t"
+        "ds_write_addtid_b32 %2 offset:4096\n\t"
+        "ds_write_addtid_b32 %3 offset:8192\n\t"
+        "ds_write_addtid_b32 %4 offset:12288\n\t"
+        "ds_write_addtid_b32 %5 offset:16384\n\t"
+        "ds_write_addtid_b32 %6 offset:20480\n\t"
+        "ds_write_addtid_b32 %7 offset:24576\n\t"
+        "ds_write_addtid_b32 %8 offset:28672\n\t"
+        "ds_write_addtid_b32 %9 offset:32768\n\t"
+        "ds_write_addtid_b32 %10 offset:36864\n\t"
+        "ds_write_addtid_b32 %11 offset:40960\n\t"
+        "ds_write_addtid_b32 %12 offset:45056\n\t"
+        "ds_write_addtid_b32 %13 offset:49152\n\t"
+        "ds_write_addtid_b32 %14 offset:53248\n\t"
+        "ds_write_addtid_b32 %15 offset:57344"
+        :
+        : "s"(b), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+          "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14])
+        : "memory", "m0");
+#pragma clang diagnostic pop
+#else
+#pragma unroll
+    for (int f = 0; f < 15; ++f) s_x[f * kRankPlaneRows + r * BLOCK + threadIdx.x] = x[f];
+#endif
+}
+
 template <int BLOCK, int R, int G, int P16, int PIPE>
 __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
@@ -586,13 +638,12 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                         s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w16[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
                 } else {
                     const uint32_t w8[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
+                    if constexpr (P16 == 0) {
+                        stage_planes_u32<BLOCK>(s_x, r, w8);
+                    } else {
 #pragma unroll
-                    for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
-                        const uint32_t u = (w8[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                        if (P16)
-                            s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)u;
-                        else
-                            s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+                        for (int f = 0; f < 16; ++f)
+                            s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w8[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
                     }
                 }
                 a[r] = pacc[r];
@@ -656,13 +707,12 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                     s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
             } else {
                 const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
+                if constexpr (P16 == 0) {
+                    stage_planes_u32<BLOCK>(s_x, r, w);
+                } else {
 #pragma unroll
-                for (int f = 0; f < (P16 == 3 ? 16 : 15); ++f) {
-                    const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-                    if (P16)
-                        s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)u;
-                    else
-                        s_x[f * kRankPlaneRows + r * BLOCK + tid] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+                    for (int f = 0; f < 16; ++f)
+                        s_x16[f * kPlaneRows + r * BLOCK + pslot] = (uint16_t)((w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu);
                 }
             }
             a[r] = pacc[r];
@@ -897,32 +947,40 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
         for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
     }
     F->rnsmp = (int32_t)smp.size();
-    // Eytzinger tables of the searched features of k_zfill_grouped_w3 (15-feature forests with
-    // 16-float segments): samples padded with +inf to 2^L - 1, laid out in BFS order
+    // S-trees of the searched features of k_zfill_grouped_w3 (RankTab::etab; 15-feature
+    // forests with the v1 row format): every kW3Gap-th threshold, 8 keys per node, filled in
+    // in-order (= sorted order), +inf past the samples
     std::vector<float> etab;
     F->rnetab = 0;
-    if (F->n_features == 15 && seg == 16 && (!v2 || F->rank_identity)) {
+    if (F->n_features == 15 && seg % kW3Gap == 0 && (!v2 || F->rank_identity)) {
         for (int s = 0; s < 4; ++s) {
             const int f = kW3Search[s];
-            const int32_t ns = F->rscnt[f];
+            const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, kW3Gap);
+            const float *thr = RL.thr.data() + RL.thr_off[f];
             int L = 0;
-            while (((int64_t)1 << L) - 1 < ns) ++L;
-            const int32_t m = (1 << L) - 1;
-            F->reoff[s] = (int32_t)etab.size();
+            int64_t keys = 0;  // 9^L - 1
+            while (keys < ns) {
+                ++L;
+                keys = keys * 9 + 8;
+            }
+            const int64_t nn = keys / 8;
+            F->reoff[s] = (int32_t)(etab.size() / 8);
             F->relev[s] = L;
-            std::vector<float> e((size_t)m + 1, INFINITY);  // e[0] unused
+            std::vector<float> t((size_t)keys, INFINITY);
             int32_t i = 0;
-            std::function<void(int32_t)> fill = [&](int32_t k) {  // in-order walk = sorted order
-                if (k > m) return;
-                fill(2 * k);
-                e[(size_t)k] = i < ns ? smp[(size_t)(F->rsoff[f] + i)] : INFINITY;
-                ++i;
-                fill(2 * k + 1);
+            std::function<void(int64_t)> fill = [&](int64_t k) {  // in-order walk = sorted order
+                if (k >= nn) return;
+                for (int j = 0; j < 8; ++j) {
+                    fill(9 * k + 1 + j);
+                    t[(size_t)(8 * k + j)] = i < ns ? thr[(size_t)i * kW3Gap] : INFINITY;
+                    ++i;
+                }
+                fill(9 * k + 9);
             };
-            fill(1);
-            etab.insert(etab.end(), e.begin(), e.end());
+            fill(0);
+            etab.insert(etab.end(), t.begin(), t.end());
         }
-        if (etab.size() > (size_t)kMaxRankSamples) etab.clear();  // over the LDS budget: generic kernel
+        if (etab.size() > (size_t)kW3TreeFloats) etab.clear();  // over the LDS budget: generic kernel
         F->rnetab = (int32_t)etab.size();
     }
     // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every

@@ -112,17 +112,19 @@ struct RankTab {
     // rat[(f * kRatN + nb) * kRatN + fr] = rank of the scaled ratio fr / nb (0 when nb == 0,
     // the reference's fillna(0)) for nb < kRatN: the terminal risks are such ratios
     const uint16_t *rat;
-    // Eytzinger form of the segment samples of the reference layout's searched features
-    // (kW3Search: amount + the three averages), for k_zfill_grouped_w3: feature kW3Search[s]'s
-    // samples padded with +inf to 2^elev[s] - 1 entries, BFS order, entry k (1-based) at
-    // etab[eoff[s] + k].  A lane's descent reads level d from a window of 2^d consecutive words,
-    // so the first levels are bank-conflict free (the sorted table's binary search puts every
-    // probe of a level on one bank: stride n / 2^d).  NULL when the tables exceed the LDS budget.
+    // S-trees of the reference layout's searched features (kW3Search: amount + the three
+    // averages), for k_zfill_grouped_w3: feature kW3Search[s]'s every kW3Gap-th threshold as a
+    // complete 9-ary tree of elev[s] levels, 8 keys per node (32 B; node k's children are
+    // 9k+1..9k+9; keys padded with +inf), keys in in-order = sorted order, so the digits of a
+    // descent (keys of the node < v) spell #samples < v in base 9; node k of feature s at
+    // etab[8 * (eoff[s] + k)].  NULL when the trees exceed the LDS budget (kW3TreeFloats).
     const float *etab;
     int32_t eoff[4], elev[4], n_etab;
 };
 constexpr int kW3Search[4] = {0, 4, 6, 8};  // TX_AMOUNT, CUSTOMER_ID_AVG_AMOUNT_{1,7,30}DAY_WINDOW
 constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
+constexpr int kW3Gap = 4;              // thresholds per S-tree sample (one 16-byte segment read)
+constexpr int kW3TreeFloats = 28672;   // LDS budget of the S-trees (112 KiB)
 constexpr int kIntTab = 256;           // integer rank table entries per feature (8 KiB in LDS)
 constexpr int kRatN = 128;             // ratio rank table: nb, fr < kRatN (32 KiB per feature, global)
 
