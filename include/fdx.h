@@ -403,6 +403,15 @@ int fdx_forest_pack_rank2(const fdx_forest_desc *desc, int32_t version, uint32_t
                           double *leaf_value_out, uint8_t *missing_left_out, int32_t *root_out, int32_t *depth_out,
                           float *thr_out, int32_t *thr_off_out /* [33] */, int32_t *slot_feat_out /* [32] */,
                           int32_t *slot_base_out /* [32] */);
+/* Host form of the fused row assembly's search tables (tests; fdx_forest_prepare_grouped*):
+ * for a 15-feature forest, every 4th v1-layout threshold of features 0, 4, 6, 8 (amount and the
+ * three customer averages) as a complete 9-ary tree of 8-key nodes, keys in in-order (= sorted)
+ * order, +inf padded.  Feature s's node k (children 9k+1..9k+9) is trees_out[8*(eoff_out[s]+k)
+ * ...+7]; elev_out[s] levels.  A descent that goes to child c = #keys < v at every level
+ * counts the samples < v in base 9.  trees_out may be NULL (sizes only); *n_floats = 0 when
+ * the trees exceed the kernel's LDS budget (the generic prepare kernel is used then). */
+int fdx_forest_search_trees(const fdx_forest_desc *desc, float *trees_out, int64_t cap, int64_t *n_floats,
+                            int32_t *eoff_out /* [4] */, int32_t *elev_out /* [4] */);
 /* *layout = 0 (wide 8-byte nodes), 1 (rank v1, the default when the forest fits it), 2 (rank
  * v2) or 3 (rank v2 with one slot per feature: v1 row format, compact 32 KiB row planes);
  * *n_slots = rank slots.  fdx_forest_set_variant rebuilds the rank layout in the other node

@@ -516,6 +516,14 @@ struct PrepRow {
     int32_t r;
 };
 
+// A/B switches (compile time): the feature table stored after the rank row (FDX_EMIT_LATE), by
+// nontemporal stores (FDX_EMIT_NT)
+#ifndef FDX_EMIT_LATE
+#define FDX_EMIT_LATE 0
+#endif
+#ifndef FDX_EMIT_NT
+#define FDX_EMIT_NT 0
+#endif
 // EMIT: the featurized table besides the rank rows (fdx_forest_prepare_grouped_rows): 0 = none,
 // FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
 // input row / at its slot, stored as soon as the row's values are loaded (the record's registers
@@ -636,6 +644,13 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
         q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
         v[0] = zval(cur.a, mean, scale, 0);
         bool nan = v[0] != v[0];
+        auto fst = [](auto *p, auto v) {  // feature-table store (FDX_EMIT_NT: nontemporal, the step never reads it)
+#if FDX_EMIT_NT
+            __builtin_nontemporal_store(v, p);
+#else
+            *p = v;
+#endif
+        };
         auto emit = [&]() {
             // the featurized row: a record at its input row (one random 80-byte write), or the
             // columns at its slot (consecutive lanes, consecutive elements: every store of a wave
@@ -656,13 +671,13 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                 if constexpr (EMIT == FDX_ROWS_SLOT_ORDER) {
 #pragma unroll
                     for (int w = 0; w < W; ++w) {
-                        reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(w, fcap))[i] = c[w];
-                        reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(3 + w, fcap))[i] = tn[w];
-                        reinterpret_cast<double *>(feat + FDX_FEATURE_COL(6 + w, fcap))[i] = avg[w];
-                        reinterpret_cast<double *>(feat + FDX_FEATURE_COL(9 + w, fcap))[i] = rk[w];
+                        fst(reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(w, fcap)) + i, c[w]);
+                        fst(reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(3 + w, fcap)) + i, tn[w]);
+                        fst(reinterpret_cast<double *>(feat + FDX_FEATURE_COL(6 + w, fcap)) + i, avg[w]);
+                        fst(reinterpret_cast<double *>(feat + FDX_FEATURE_COL(9 + w, fcap)) + i, rk[w]);
                     }
-                    reinterpret_cast<int32_t *>(feat + FDX_FEATURE_COL(12, fcap))[i] = live ? cur.r : -1;
-                    reinterpret_cast<uint16_t *>(feat + FDX_FEATURE_COL(13, fcap))[i] = (uint16_t)fl;
+                    fst(reinterpret_cast<int32_t *>(feat + FDX_FEATURE_COL(12, fcap)) + i, live ? cur.r : -1);
+                    fst(reinterpret_cast<uint16_t *>(feat + FDX_FEATURE_COL(13, fcap)) + i, (uint16_t)fl);
                 } else {
                     uint4 *dst = reinterpret_cast<uint4 *>(feat) + (int64_t)cur.r * 5;
                     dst[0] = make_uint4(c[0], c[1], c[2], tn[0]);
@@ -673,7 +688,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                 }
             }
         };
-        if constexpr (EMIT != 0) emit();
+        if constexpr (EMIT != 0 && !FDX_EMIT_LATE) emit();
         uint16_t rq[W];
         bool rat_ok[W];
 #pragma unroll
@@ -748,6 +763,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
                           : make_uint4(0, 0, 0, 0);
         }
+        if constexpr (EMIT != 0 && FDX_EMIT_LATE) emit();
         cur = nxt;
     }
 }

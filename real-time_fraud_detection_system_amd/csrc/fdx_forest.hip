@@ -948,39 +948,11 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
     }
     F->rnsmp = (int32_t)smp.size();
     // S-trees of the searched features of k_zfill_grouped_w3 (RankTab::etab; 15-feature
-    // forests with the v1 row format): every kW3Gap-th threshold, 8 keys per node, filled in
-    // in-order (= sorted order), +inf past the samples
+    // forests with the v1 row format, build_search_trees)
     std::vector<float> etab;
     F->rnetab = 0;
     if (F->n_features == 15 && seg % kW3Gap == 0 && (!v2 || F->rank_identity)) {
-        for (int s = 0; s < 4; ++s) {
-            const int f = kW3Search[s];
-            const int32_t c = F->rthr_cnt[f], ns = (int32_t)ceil_div(c, kW3Gap);
-            const float *thr = RL.thr.data() + RL.thr_off[f];
-            int L = 0;
-            int64_t keys = 0;  // 9^L - 1
-            while (keys < ns) {
-                ++L;
-                keys = keys * 9 + 8;
-            }
-            const int64_t nn = keys / 8;
-            F->reoff[s] = (int32_t)(etab.size() / 8);
-            F->relev[s] = L;
-            std::vector<float> t((size_t)keys, INFINITY);
-            int32_t i = 0;
-            std::function<void(int64_t)> fill = [&](int64_t k) {  // in-order walk = sorted order
-                if (k >= nn) return;
-                for (int j = 0; j < 8; ++j) {
-                    fill(9 * k + 1 + j);
-                    t[(size_t)(8 * k + j)] = i < ns ? thr[(size_t)i * kW3Gap] : INFINITY;
-                    ++i;
-                }
-                fill(9 * k + 9);
-            };
-            fill(0);
-            etab.insert(etab.end(), t.begin(), t.end());
-        }
-        if (etab.size() > (size_t)kW3TreeFloats) etab.clear();  // over the LDS budget: generic kernel
+        build_search_trees(RL, etab, F->reoff, F->relev);
         F->rnetab = (int32_t)etab.size();
     }
     // one whole +inf segment past the end: k_zfill_grouped_w3 reads a segment of every

@@ -188,6 +188,10 @@ struct RankLayout {
     int32_t n_slots = 0, slot_feat[32] = {}, slot_base[32] = {};
 };
 constexpr int64_t kSlotSpan = 32767;  // thresholds per rank-layout-v2 slot (build_rank_layout)
+// The S-trees of k_zfill_grouped_w3 (RankTab::etab) over a v1 rank layout's thresholds of the
+// kW3Search features: trees (floats, 8 per node), eoff (node offset) and elev (levels) per
+// searched feature.  Empty when they exceed kW3TreeFloats.
+void build_search_trees(const RankLayout &L, std::vector<float> &trees, int32_t eoff[4], int32_t elev[4]);
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
                       RankLayout &L, bool v2 = false);

@@ -4,6 +4,8 @@
 // and the 4-byte rank layouts v1 / v2 (fdx_forest.hip's "Rank layout" comment).  Host code only.
 #include "fdx_forest_internal.h"
 
+#include <functional>
+
 namespace fdx {
 
 float round_down_f32(double t) {
@@ -284,6 +286,41 @@ extern "C" int fdx_forest_pack(const fdx_forest_desc *d, uint64_t *nodes_out, in
     return FDX_OK;
 }
 
+// Every kW3Gap-th threshold of each searched feature as a complete 9-ary tree of 8-key nodes
+// (node k's children 9k+1..9k+9), keys filled by an in-order walk (= sorted order), +inf past
+// the samples: a descent's digits (keys of the node < v) spell #samples < v in base 9.
+void fdx::build_search_trees(const RankLayout &L, std::vector<float> &trees, int32_t eoff[4], int32_t elev[4]) {
+    trees.clear();
+    for (int s = 0; s < 4; ++s) {
+        const int f = kW3Search[s];
+        const int32_t c = L.thr_off[f + 1] - L.thr_off[f], ns = (c + kW3Gap - 1) / kW3Gap;
+        const float *thr = L.thr.data() + L.thr_off[f];
+        int lv = 0;
+        int64_t keys = 0;  // 9^lv - 1
+        while (keys < ns) {
+            ++lv;
+            keys = keys * 9 + 8;
+        }
+        const int64_t nn = keys / 8;
+        eoff[s] = (int32_t)(trees.size() / 8);
+        elev[s] = lv;
+        std::vector<float> t((size_t)keys, INFINITY);
+        int32_t i = 0;
+        std::function<void(int64_t)> fill = [&](int64_t k) {
+            if (k >= nn) return;
+            for (int j = 0; j < 8; ++j) {
+                fill(9 * k + 1 + j);
+                t[(size_t)(8 * k + j)] = i < ns ? thr[(size_t)i * kW3Gap] : INFINITY;
+                ++i;
+            }
+            fill(9 * k + 9);
+        };
+        fill(0);
+        trees.insert(trees.end(), t.begin(), t.end());
+    }
+    if (trees.size() > (size_t)kW3TreeFloats) trees.clear();  // over the LDS budget
+}
+
 static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL, int version = 1) {
     std::vector<uint64_t> packed;
     std::vector<int32_t> orig, root, depth;
@@ -367,3 +404,22 @@ extern "C" int fdx_forest_pack_rank(const fdx_forest_desc *d, uint32_t *nodes_ou
     return FDX_OK;
 }
 
+// Host form of the row assembly's search tables (tests): the S-trees of a 15-feature forest's
+// v1 rank layout.  trees_out may be NULL (sizes only); *n_floats = 0 when none are built.
+extern "C" int fdx_forest_search_trees(const fdx_forest_desc *d, float *trees_out, int64_t cap, int64_t *n_floats,
+                                       int32_t *eoff_out, int32_t *elev_out) {
+    FDX_REQUIRE(d && n_floats && eoff_out && elev_out, "null argument");
+    FDX_REQUIRE(d->n_features == 15, "the assembly's search tables serve 15-feature forests");
+    RankLayout RL;
+    int rc = rank_layout_host(d, RL);
+    if (rc) return rc;
+    std::vector<float> trees;
+    build_search_trees(RL, trees, eoff_out, elev_out);
+    *n_floats = (int64_t)trees.size();
+    if (trees_out) {
+        FDX_REQUIRE(cap >= (int64_t)trees.size(), "trees_out holds %lld floats, %lld needed", (long long)cap,
+                    (long long)trees.size());
+        memcpy(trees_out, trees.data(), 4 * trees.size());
+    }
+    return FDX_OK;
+}

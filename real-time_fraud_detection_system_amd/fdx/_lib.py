@@ -131,6 +131,7 @@ SIGNATURES = {
     "fdx_forest_pack_rank": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, P, P, P, P, P, P, P]),
     "fdx_forest_rank_layout_size2": (ctypes.c_int, [ctypes.POINTER(ForestDesc), c_i32, P, P, P]),
     "fdx_forest_pack_rank2": (ctypes.c_int, [ctypes.POINTER(ForestDesc), c_i32, P, P, P, P, P, P, P, P, P, P]),
+    "fdx_forest_search_trees": (ctypes.c_int, [ctypes.POINTER(ForestDesc), P, c_i64, P, P, P]),
     "fdx_forest_layout": (ctypes.c_int, [P, P, P]),
     "fdx_forest_destroy": (ctypes.c_int, [P]),
     "fdx_synth_workspace_size": (c_sz, [ctypes.POINTER(SynthDesc), c_i64]),

@@ -4,6 +4,7 @@ and probabilities bit for bit (golden vectors from sklearn, and the C oracle of
 sklearn's Tree._apply_dense for random forests -- incl. trees large enough to need
 jump nodes, and NaN rows routed by missing_go_to_left)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -270,3 +271,52 @@ def test_rank_layout_v2_deployed_model():
     sel = np.arange(0, len(z["test_X"]), 16)
     proba, _ = walk_rank_v2(R, _z32(z["test_X"][sel], z["mean"], z["scale"]))
     np.testing.assert_array_equal(proba, z["test_proba1"][sel])
+
+
+def _search_trees(a):
+    from fdx import _lib
+
+    L = _lib.load()
+    d, keep = _desc(a, 15)
+    nf = ctypes.c_int64()
+    eoff, elev = (ctypes.c_int32 * 4)(), (ctypes.c_int32 * 4)()
+    assert L.fdx_forest_search_trees(ctypes.byref(d), None, 0, ctypes.byref(nf), eoff, elev) == 0
+    trees = np.zeros(max(nf.value, 1), np.float32)
+    assert L.fdx_forest_search_trees(ctypes.byref(d), trees.ctypes.data, trees.size, ctypes.byref(nf), eoff,
+                                     elev) == 0
+    return trees[: nf.value], list(eoff), list(elev)
+
+
+@pytest.mark.parametrize("which", ["bench", "random"])
+def test_search_trees_count_samples(which):
+    """k_zfill_grouped_w3's search tables (fdx_forest_search_trees, the same host builder the
+    forest object uploads): descending each searched feature's S-tree and counting the 4
+    thresholds of the segment it leaves gives lower_bound over the feature's thresholds (the
+    rank the forest walk compares), for every threshold, its float32 neighbours, random and
+    extreme values."""
+    if which == "bench":
+        z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench_assets",
+                                 "rf100_d20.npz"))
+        a = {k: z[k] for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    else:
+        a = random_forest(np.random.default_rng(5), n_trees=12, depth=12)
+    trees, eoff, elev = _search_trees(a)
+    assert trees.size > 0
+    packed = pack_rank(a)
+    thr_all, thr_off = packed["thr"], packed["thr_off"]
+    rng = np.random.default_rng(11)
+    for s, f in enumerate((0, 4, 6, 8)):
+        thr = thr_all[thr_off[f]:thr_off[f + 1]].astype(np.float32)
+        v = np.concatenate([thr, np.nextafter(thr, np.float32(np.inf)), np.nextafter(thr, np.float32(-np.inf)),
+                            rng.normal(0, 3, 5000).astype(np.float32),
+                            np.array([-3e38, 3e38, np.inf, -np.inf], np.float32)]).astype(np.float32)
+        ek = np.zeros(v.size, np.int64)
+        cs = np.zeros(v.size, np.int64)
+        for _ in range(elev[s]):
+            nd = trees.reshape(-1, 8)[eoff[s] + ek]
+            c = (nd < v[:, None]).sum(1)
+            cs, ek = cs * 9 + c, ek * 9 + 1 + c
+        useg = np.concatenate([thr, np.full(16, np.inf, np.float32)])
+        seg = useg[(np.maximum(cs - 1, 0) * 4)[:, None] + np.arange(4)]
+        rank = np.where(cs > 0, (cs - 1) * 4 + (seg < v[:, None]).sum(1), 0)
+        np.testing.assert_array_equal(rank, np.searchsorted(thr, v, side="left"))
