@@ -522,7 +522,7 @@ struct PrepRow {
 #define FDX_EMIT_LATE 0
 #endif
 #ifndef FDX_EMIT_NT
-#define FDX_EMIT_NT 0
+#define FDX_EMIT_NT 1
 #endif
 // EMIT: the featurized table besides the rank rows (fdx_forest_prepare_grouped_rows): 0 = none,
 // FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
