@@ -516,10 +516,14 @@ struct PrepRow {
     int32_t r;
 };
 
-// A/B switches (compile time): the feature table stored after the rank row (FDX_EMIT_LATE), by
-// nontemporal stores (FDX_EMIT_NT)
-#ifndef FDX_EMIT_LATE
-#define FDX_EMIT_LATE 0
+// A/B switches (compile time): where the feature table is stored (FDX_EMIT_POS: 0 = right after
+// the row's loads, 1 = behind the segment / ratio loads, 2 = after the rank row), by nontemporal
+// stores (FDX_EMIT_NT); the first row iteration peeled (FDX_ZFILL_PEEL)
+#ifndef FDX_EMIT_POS
+#define FDX_EMIT_POS 1
+#endif
+#ifndef FDX_ZFILL_PEEL
+#define FDX_ZFILL_PEEL 1
 #endif
 #ifndef FDX_EMIT_NT
 #define FDX_EMIT_NT 1
@@ -541,6 +545,10 @@ __device__ __forceinline__ void decode_tw(const int64_t *rec, PrepRow &L) {
             const int64_t *wide = rec + (L.raw.x & INT64_MAX);
 #pragma unroll
             for (int w = 0; w < 3; ++w) L.tw[w] = wide[w];
+            // waited for inside the branch: a wait after it (taken or not) would cover every
+            // load and store in flight, the next row's loads and the previous row's stores
+#pragma unroll
+            for (int w = 0; w < 3; ++w) asm volatile("" ::"v"(L.tw[w]));
         } else {
 #pragma unroll
             for (int w = 0; w < 3; ++w)
@@ -614,13 +622,18 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
     }
     int32_t r1 = row_of(i + stride), r2 = row_of(i + 2 * stride);  // slots one and two ahead
     int64_t q1 = rec_of(r1);
-    for (; i - lane < n; i += stride) {
+    // one row per call; the loop below runs it with its first iteration peeled (FDX_ZFILL_PEEL), so
+    // that the loop header is reached only in the steady state: entered straight from the
+    // prologue, whose last memory operations are the first row's loads, the header's merged wait
+    // state forced s_waitcnt vmcnt(0) there -- every iteration then waited for the previous row's
+    // stores to complete
+    auto row_iter = [&]() {
+        settle(i, cur);
         PrepRow nxt;
         load(i + stride, r1, q1, nxt);  // next row's loads in flight during this row
         q1 = rec_of(r2);                // (r2 arrived during the previous row)
         r1 = r2;
         r2 = row_of(i + 3 * stride);
-        settle(i, cur);
         const bool live = i < n && cur.r >= 0;
         bool we, ni;
         day_flags(cur.t, flags_mode, we, ni);
@@ -656,7 +669,9 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             // columns at its slot (consecutive lanes, consecutive elements: every store of a wave
             // is whole lines; an 80-byte record per slot, 5 strided 16-byte stores, measured
             // +0.62 ms at config 2; padding slots: row -1, zero features)
-            if (i < n && (EMIT == FDX_ROWS_SLOT_ORDER || (live && (uint64_t)cur.r < (uint64_t)fcap))) {
+            // (slot order: every lane stores, i < round_up(n, 64) <= fcap -- no branch, so that
+            // no wait behind it has to assume the stores were skipped)
+            if (EMIT == FDX_ROWS_SLOT_ORDER || (i < n && live && (uint64_t)cur.r < (uint64_t)fcap)) {
                 auto u32 = [](double d, int h) { return (uint32_t)((uint64_t)__double_as_longlong(d) >> (32 * h)); };
                 uint32_t c[W], tn[W];
                 double avg[W], rk[W];
@@ -688,7 +703,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                 }
             }
         };
-        if constexpr (EMIT != 0 && !FDX_EMIT_LATE) emit();
+        if constexpr (EMIT != 0 && FDX_EMIT_POS == 0) emit();
         uint16_t rq[W];
         bool rat_ok[W];
 #pragma unroll
@@ -729,6 +744,9 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             for (int s = 0; s < 4; ++s)
                 sg[s] = *reinterpret_cast<const float4 *>(rt.useg + rt.uoff[kW3Search[s]] +
                                                           (int64_t)max(cs[s] - 1, 0) * kW3Gap);
+            // (stores issued behind the segment and ratio loads: waiting for those loads does
+            // not wait for the stores -- vmcnt counts stores, in issue order)
+            if constexpr (EMIT != 0 && FDX_EMIT_POS == 1) emit();
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const float x = v[kW3Search[s]];
@@ -763,9 +781,16 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
                           : make_uint4(0, 0, 0, 0);
         }
-        if constexpr (EMIT != 0 && FDX_EMIT_LATE) emit();
+        if constexpr (EMIT != 0 && FDX_EMIT_POS == 2) emit();
         cur = nxt;
+    };
+#if FDX_ZFILL_PEEL
+    if (i - lane < n) {
+        row_iter();
+        i += stride;
     }
+#endif
+    for (; i - lane < n; i += stride) row_iter();
 }
 
 }  // namespace
