@@ -655,7 +655,12 @@ __global__ void __launch_bounds__(64) k_customer_ring(
 // the amounts ride in the LDS ring (8 B per row), so more waves fit per CU.
 // starts: segment-contiguous (k_interleave<true>); nullptr = in nb_out, slot layout, overwritten
 // by the counts.
-template <int S_MAX, int kRing, int P>
+// BUF: the per-row outputs stored by raw buffer stores, a lane past its segment's end given an
+// out-of-range offset (the store is dropped) instead of a branch: behind a branch around stores,
+// the next chunk's wait for its prefetched amounts had to assume the stores were skipped and
+// waited for them too (vmcnt counts stores).  Needs the outputs within 2^31 bytes (the host picks).
+typedef unsigned int fdx_u32x2 __attribute__((ext_vector_type(2)));
+template <int S_MAX, int kRing, int P, bool BUF>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
@@ -686,6 +691,9 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     const double *g_amt = iamt + gbase + seg0 + l;  // row t of this lane's segment: g_amt[t * S]
     int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + seg0 + l;
     double *sm = sum_out + (int64_t)wi * n_slots + gbase + seg0 + l;
+    const int32_t n_out = (int32_t)min<int64_t>((int64_t)n_win * n_slots, INT32_MAX / 8);
+    const __amdgpu_buffer_rsrc_t rnb = __builtin_amdgcn_make_buffer_rsrc(nb_out, (short)0, n_out * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsm = __builtin_amdgcn_make_buffer_rsrc(sum_out, (short)0, n_out * 8, 0x00020000);
     // chunk element e = lane + j * 64 of this wave's Sw segments: row e / Sw, segment e % Sw --
     // the same for every chunk, so its slot offset and ring position are computed once
     int32_t e_src[kPer], e_ring[kPer];
@@ -702,15 +710,14 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         const int n_el = min(kChunk, Lw - t0) * Sw;
         const int64_t src0 = gbase + (int64_t)t0 * S + seg0;
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
+        for (int j = 0; j < kPer; ++j) {  // (no branch: a conditional load's register merge waits for it)
             const int e = lane + j * kWave;
-            if (e < n_el) pam[j] = iamt[src0 + e_src[j]];
+            pam[j] = iamt[src0 + (e < n_el ? e_src[j] : 0)];  // src0 is a slot of this wave's longest segment
         }
         if (starts) {
-            const int32_t *sp = starts + (int64_t)wi * n_slots + gbase + (int64_t)(seg0 + l) * Lg + t0;
+            const int32_t *sp = t0 < L ? starts + (int64_t)wi * n_slots + gbase + (int64_t)(seg0 + l) * Lg + t0 : starts;
 #pragma unroll
-            for (int j = 0; j < kChunk; ++j)
-                if (t0 + j < L) pst[j] = sp[j];
+            for (int j = 0; j < kChunk; ++j) pst[j] = sp[t0 + j < L ? j : 0];
         } else {
 #pragma unroll
             for (int j = 0; j < kChunk; ++j)
@@ -721,9 +728,9 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         const int n_el = min(kChunk, Lw - t0) * Sw;
         const int ring0 = (t0 & (kRing - 1)) * S_MAX;
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int e = lane + j * kWave;
-            if (e < n_el) r_amt[ring0 + e_ring[j]] = pam[j];
+        for (int j = 0; j < kPer; ++j) {  // elements past the chunk go to the lane's miss slot (scratch):
+            const int e = lane + j * kWave;  // past the chunk, a ring row may still hold a live older row
+            r_amt[e < n_el ? ring0 + e_ring[j] : kRing * S_MAX + lane] = pam[j];
         }
     };
     double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
@@ -780,11 +787,23 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if constexpr (BUF) {
+            const uint32_t o0 = (uint32_t)((int64_t)wi * n_slots + gbase + seg0 + l);  // element index of row 0
 #pragma unroll
-        for (int j = 0; j < kChunk; ++j) {
-            if (t0 + j < L) {
-                nb[(int64_t)(t0 + j) * S] = onb[j];
-                sm[(int64_t)(t0 + j) * S] = oval[j];
+            for (int j = 0; j < kChunk; ++j) {
+                const bool ok = t0 + j < L;
+                const uint32_t el = o0 + (uint32_t)(t0 + j) * (uint32_t)S;
+                __builtin_amdgcn_raw_buffer_store_b32(onb[j], rnb, ok ? (int)(el * 4u) : (int)0x80000000, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fdx_u32x2, oval[j]), rsm,
+                                                      ok ? (int)(el * 8u) : (int)0x80000000, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) {
+                if (t0 + j < L) {
+                    nb[(int64_t)(t0 + j) * S] = onb[j];
+                    sm[(int64_t)(t0 + j) * S] = oval[j];
+                }
             }
         }
     };
@@ -1953,10 +1972,17 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     // ring on a forked stream, concurrently with the rest on the 128-row ring (twice the
     // blocks per CU); the class boundary is kWalkSplitRows.
     constexpr int split = kWalkSplitRows;
+    // buffer stores while the outputs fit 2^31 bytes (raw buffer offsets are 32-bit)
+    const bool buf = (int64_t)n_windows * n_slots * 8 < (int64_t)INT32_MAX / 8 * 8;
 #define FDX_WALK(SM, RING, P, STREAM, LO, HI)                                                                 \
-    hipLaunchKernelGGL((k_customer_walk<SM, RING, P>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, STREAM,  \
-                       iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, starts_d, \
-                       LO, HI);                                                                                \
+    if (buf)                                                                                                  \
+        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, true>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
+                           STREAM, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, \
+                           starts_d, LO, HI);                                                                  \
+    else                                                                                                      \
+        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, false>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
+                           STREAM, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, \
+                           starts_d, LO, HI);                                                                  \
     FDX_LAUNCHED("k_customer_walk")
 #if FDX_WALK_SINGLE
     (void)split;
