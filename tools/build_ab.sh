@@ -1,5 +1,5 @@
 # Build an A/B variant of libfdx.so with extra compile-time defines (every source recompiled):
-#   bash tools/build_ab.sh NAME "-DFDX_WALK_LP=2 -DFDX_RADIX_XCD=1"  ->  tools/ab/libfdx_NAME.so
+#   bash tools/build_ab.sh NAME "-DFDX_WALK_LP=2 -DFDX_EMIT_NT=0"  ->  tools/ab/libfdx_NAME.so
 set -eu
 NAME=$1; DEFS=$2
 C=real-time_fraud_detection_system_amd/csrc

@@ -1,8 +1,8 @@
 """Time the one-launch customer layout plan alone (fdx_customer_layout_plan_async on the
 config-2 segment offsets: 50k customers, lengths from the GPU generator), 50 launches after a
-warm-up, HIP events on one stream; prints one JSON line.  Study builds of the kernel that stop
-after phase k (tools/build_ab.sh -DFDX_STUDY_PLAN_STOP=k) attribute its time:
-    python tools/with_lib.py tools/ab/libfdx_plan1.so tools/plan_probe.py
+warm-up, HIP events on one stream; prints one JSON line.  (Round 3 attributed its time with
+study builds stopping after each phase -- profiles/r03ao_plan_phases.txt; that switch is gone.)
+    python tools/plan_probe.py
 """
 import json
 import os
