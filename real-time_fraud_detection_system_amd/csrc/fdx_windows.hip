@@ -435,8 +435,19 @@ __global__ void __launch_bounds__(256) k_interleave(
             const int64_t *gts = GROUPED ? ts + seg_off[sg] : its + base + ls;
             const int64_t gstride = GROUPED ? 1 : S;
             const bool in_lds = L <= kStartLds;
-            if (in_lds)
-                for (int64_t t = lane; t < L; t += kWave) lts[t] = __builtin_nontemporal_load(gts + t * gstride);
+            if (in_lds && L > 0) {  // (an empty segment: nothing to stage or search)
+                // the whole staged segment in one trip: every lane's 16 loads issued before its
+                // first LDS store (a rolled loop waited on each load in turn: 0.41 -> 0.37 ms
+                // alone at config 2, profiles/r04wxy_interleave_ab.txt); a row past the end
+                // re-reads and re-stores the last row (the same value to the same word)
+                constexpr int UF = kStartLds / kWave;
+                int64_t v[UF];
+#pragma unroll
+                for (int j = 0; j < UF; ++j)
+                    v[j] = __builtin_nontemporal_load(gts + (int64_t)min(lane + j * kWave, (int32_t)L - 1) * gstride);
+#pragma unroll
+                for (int j = 0; j < UF; ++j) lts[min(lane + j * kWave, (int32_t)L - 1)] = v[j];
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

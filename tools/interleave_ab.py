@@ -1,0 +1,51 @@
+"""A/B probe for the customer layout fill (k_interleave<true, true>): config-2 rows (50k
+customers, 183 days) -> payload re-key -> one-launch plan, then
+fdx_customer_layout_fill_starts_grouped timed alone (--reps); prints the time and a digest of
+the slots (its / iamt / irow) and the window starts so that builds of libfdx.so with different
+fill shapes (tools/build_ab.sh, tools/with_lib.py) can be compared bit for bit.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "real-time_fraud_detection_system_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+
+    from fdx import ops, synth
+
+    dev = torch.device("cuda", 0)
+    g = synth.generate_device(50_000, 100_000, 183, seed=1234, device=dev)
+    perm, seg, gts, gamt = ops.rekey_payload(g["customer"], 50_000, g["ts"], g["amount"])
+    plan = ops.customer_layout_plan(seg, 3)
+    days = (1, 7, 30)
+    lay = ops.customer_layout_fill(plan, seg, perm, gts, gamt, days)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(args.reps):
+        ops.customer_layout_fill(plan, seg, perm, gts, gamt, days)
+    b.record()
+    torch.cuda.synchronize()
+    m = lay.n_slots
+    w = torch.arange(1, m + 1, device=dev, dtype=torch.int64)
+    real = lay.irow[:m] >= 0
+    dig = {
+        "irow": int((lay.irow[:m].to(torch.int64) * w).sum().item()),
+        "its": int((lay.its[:m][real] % 1_000_003).sum().item()),
+        "iamt_bits": int((lay.iamt[:m][real].view(torch.int64) % 1_000_003).sum().item()),
+        "starts": [int((lay.starts[k * m:(k + 1) * m][real].to(torch.int64) * w[real]).sum().item()) for k in range(3)],
+    }
+    print(json.dumps({"lib": os.path.basename(__import__("fdx")._lib.LIB_PATH),
+                      "fill_ms": round(a.elapsed_time(b) / args.reps, 4), "n_slots": m, "digest": dig}))
+
+
+if __name__ == "__main__":
+    main()
