@@ -382,7 +382,68 @@ __global__ void __launch_bounds__(256) k_interleave(
     const int64_t s0 = sorder[g * S];
     const int64_t Lg = seg_off[s0 + 1] - seg_off[s0];
     const int64_t base = goff[g];
-    if (tt < rows_per_iter) {
+    if constexpr (STARTS && GROUPED) {
+        // a tile = R rows of each of the group's S segments (R * S <= 1024 slots): loaded along
+        // the segments (R consecutive rows each: whole lines, not the row-at-a-time form's 12
+        // rows of 21 segments per wave load), transposed through LDS (the start phase's staging
+        // arrays, free until then), written as R * S consecutive slots (0.371 -> 0.342 ms alone
+        // at config 2, bit-equal, profiles/r04wxy_interleave_ab.txt)
+        __shared__ int64_t s_sb[kWave];
+        __shared__ int32_t s_sl[kWave];
+        if ((int)threadIdx.x < S) {
+            const int64_t si = g * S + threadIdx.x;
+            const int64_t sx = si < n_seg ? sorder[si] : -1;
+            s_sb[threadIdx.x] = sx >= 0 ? seg_off[sx] : 0;
+            s_sl[threadIdx.x] = sx >= 0 ? (int32_t)(seg_off[sx + 1] - seg_off[sx]) : 0;
+        }
+        __syncthreads();
+        int64_t *x_ts = s_ts[0];
+        double *x_am = reinterpret_cast<double *>(s_ts[1]);
+        int32_t *x_rw = reinterpret_cast<int32_t *>(s_ts[2]);
+        const int R = kStartLds / S, TS = R * S;
+        const uint32_t r_inv = ((1u << 20) + (uint32_t)R - 1) / (uint32_t)R;  // e / R = e * r_inv >> 20 (e * R < 2^20)
+        constexpr int E = kStartLds / 256;
+        for (int64_t t0 = 0; t0 < Lg; t0 += R) {
+            int64_t vts[E];
+            double vam[E];
+            int32_t vr[E], xi[E];
+            bool okv[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int e = j * 256 + (int)threadIdx.x;
+                const bool valid = e < TS;
+                const int ls = valid ? (int)(((uint32_t)e * r_inv) >> 20) : 0;
+                const int r = e - ls * R;
+                const int64_t t = t0 + r;
+                const bool ok = valid && t < s_sl[ls];
+                const int64_t k = ok ? s_sb[ls] + t : 0;  // row 0 stands in (n >= 1 here)
+                vr[j] = cperm[k];
+                vts[j] = ts[k];
+                vam[j] = amount[k];
+                okv[j] = ok;
+                xi[j] = valid ? r * S + ls : e;  // (past TS: padding words, never read)
+            }
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                x_ts[xi[j]] = okv[j] ? vts[j] : 0;
+                x_am[xi[j]] = okv[j] ? vam[j] : 0.0;
+                x_rw[xi[j]] = okv[j] ? vr[j] : -1;
+            }
+            __syncthreads();
+            const int64_t lim = min<int64_t>(R, Lg - t0) * S;
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int e = j * 256 + (int)threadIdx.x;
+                if (e < lim) {
+                    const int64_t slot = base + t0 * S + e;
+                    its[slot] = x_ts[e];
+                    iamt[slot] = x_am[e];
+                    irow[slot] = x_rw[e];
+                }
+            }
+            __syncthreads();
+        }
+    } else if (tt < rows_per_iter) {
         const int64_t si = g * S + l;
         const int64_t s = si < n_seg ? sorder[si] : -1;
         const int64_t b = s >= 0 ? seg_off[s] : 0;
