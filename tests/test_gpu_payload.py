@@ -7,7 +7,9 @@ streams = the gathered columns, for 1 / 2 / 3 radix passes and tile-edge sizes.
 fdx_terminal_windows_grouped: records / columns against the C oracle, incl. segments longer
 than the 1,024-row LDS stage (a hot terminal, O(L log L) path with the prefix scratch),
 segments of several time-sorted runs (the multi-GPU owner side) and more runs than the per-run
-search handles.  fdx_customer_layout_starts_grouped: identical layout to the gathering form."""
+search handles.  fdx_customer_layout_starts_grouped: identical layout to the gathering form,
+its tiled copy for 1 / 2 / 4 windows (empty customers, a hot one past the start stage) and its
+window starts against numpy's searchsorted."""
 import numpy as np
 import pytest
 import torch
@@ -118,6 +120,45 @@ def test_customer_layout_grouped_equals_gathering_form(dev):
     valid = (a.irow[: a.n_slots] >= 0).cpu().numpy()
     for x, y in zip(ops.customer_windows_walk(a, cseg), ops.customer_windows_walk(b, cseg)):
         np.testing.assert_array_equal(x.cpu().numpy()[:, valid], y.cpu().numpy()[:, valid])
+
+
+@pytest.mark.parametrize("days", [(1,), (1, 7), (1, 7, 30, 60)])
+def test_customer_layout_grouped_tiles_and_starts(dev, days):
+    """The grouped fill's tiled copy (R = 1,024 / S rows of each of a group's S = 64 / W
+    segments per tile) equals the gathering form's row-at-a-time copy for 1 / 2 / 4 windows,
+    with empty customers and a hot one longer than the 1,024-row start stage; every window
+    start equals numpy's searchsorted over the customer's time-sorted rows (first row with
+    ts > ts_t - window: the variable-window start of `feature_transformation.ipynb:613-614`)."""
+    rng = np.random.default_rng(len(days))
+    n, n_cust = 40_000, 700
+    ts = np.sort(rng.integers(0, 90 * 86_400, n)) * 10**9  # the table in time order
+    cust = rng.integers(0, 600, n)  # customers 600..699 have no rows
+    cust[rng.choice(n, 1_500, replace=False)] = 5
+    amt = np.round(rng.random(n) * 100, 2)
+    perm, seg, gts, gamt = ops.rekey_payload(T(cust, torch.int32, dev), n_cust, T(ts, torch.int64, dev),
+                                             T(amt, torch.float64, dev))
+    W = len(days)
+    a = ops.customer_layout(seg, perm, T(ts, torch.int64, dev), T(amt, torch.float64, dev), W, windows_days=days)
+    b = ops.customer_layout(seg, perm, gts, gamt, W, windows_days=days, grouped=True)
+    m = b.n_slots
+    assert a.n_slots == m
+    for k in ("its", "iamt", "irow"):
+        assert torch.equal(getattr(a, k)[:m], getattr(b, k)[:m]), k
+    seg_np, gts_np = seg.cpu().numpy(), gts.cpu().numpy()
+    sorder, goff, st = b.sorder.cpu().numpy(), b.goff.cpu().numpy(), b.starts.cpu().numpy()
+    S = 64 // W
+    checked = 0
+    for g in range(len(goff) - 1):
+        segs = sorder[g * S:min((g + 1) * S, n_cust)]
+        Lg = seg_np[segs[0] + 1] - seg_np[segs[0]]
+        for l, s in enumerate(segs):
+            tss = gts_np[seg_np[s]:seg_np[s + 1]]
+            for w, d in enumerate(days):
+                exp = np.searchsorted(tss, tss - d * DAY, side="right")
+                o = w * m + goff[g] + l * Lg
+                np.testing.assert_array_equal(st[o:o + len(tss)], exp)
+            checked += len(tss)
+    assert checked == n
 
 
 def test_fused_pipeline_hot_terminal_matches_oracle(dev, golden):
