@@ -75,7 +75,7 @@ def _bit_length(c):
     return bl
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--customers", type=int, default=1_000_000)
@@ -91,7 +91,15 @@ def parse():
                     help="timed batches arrive as Debezium wire columns (decimal bytes, us timestamps, Kafka "
                          "timestamps, 2%% stale duplicate updates): device decode + dedup + compact + score "
                          "(StreamScorer.score_cdc; world 1)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def rank_shard(args, world: int, rank: int):
+    """configs[4]'s key state over the ranks: rank r owns the contiguous customer ids
+    [r * n_c, (r + 1) * n_c) (n_c = customers // world) and all terminals (terminal t is owned
+    by t % world for the exchange).  Returns (n_c, customer_base, n_terminals)."""
+    n_c = args.customers // world
+    return n_c, rank * n_c, args.terminals
 
 
 def main():
@@ -118,8 +126,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    n_c = args.customers // world
-    base = rank * n_c
+    n_c, base, _ = rank_shard(args, world, rank)
     t_gen = time.perf_counter()
     # generated on the GPU (csrc/fdx_synth.hip), then copied to host: the micro-batches arrive
     # from pinned host memory, as CDC batches would

@@ -516,18 +516,9 @@ struct PrepRow {
     int32_t r;
 };
 
-// A/B switches (compile time): where the feature table is stored (FDX_EMIT_POS: 0 = right after
-// the row's loads, 1 = behind the segment / ratio loads, 2 = after the rank row), by nontemporal
-// stores (FDX_EMIT_NT); the first row iteration peeled (FDX_ZFILL_PEEL)
-#ifndef FDX_EMIT_POS
-#define FDX_EMIT_POS 1
-#endif
-#ifndef FDX_ZFILL_PEEL
-#define FDX_ZFILL_PEEL 1
-#endif
-#ifndef FDX_EMIT_NT
-#define FDX_EMIT_NT 1
-#endif
+// The feature table is stored behind the row's segment / ratio loads (r04: right after the row's
+// loads or after the rank row measured slower), by nontemporal stores, and the row loop runs its
+// first iteration peeled.
 // EMIT: the featurized table besides the rank rows (fdx_forest_prepare_grouped_rows): 0 = none,
 // FDX_ROWS_INPUT_ORDER / FDX_ROWS_SLOT_ORDER = the fdx_feature_row record of each slot's row at its
 // input row / at its slot, stored as soon as the row's values are loaded (the record's registers
@@ -622,7 +613,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
     }
     int32_t r1 = row_of(i + stride), r2 = row_of(i + 2 * stride);  // slots one and two ahead
     int64_t q1 = rec_of(r1);
-    // one row per call; the loop below runs it with its first iteration peeled (FDX_ZFILL_PEEL), so
+    // one row per call; the loop below runs it with its first iteration peeled, so
     // that the loop header is reached only in the steady state: entered straight from the
     // prologue, whose last memory operations are the first row's loads, the header's merged wait
     // state forced s_waitcnt vmcnt(0) there -- every iteration then waited for the previous row's
@@ -657,12 +648,8 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
         q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
         v[0] = zval(cur.a, mean, scale, 0);
         bool nan = v[0] != v[0];
-        auto fst = [](auto *p, auto v) {  // feature-table store (FDX_EMIT_NT: nontemporal, the step never reads it)
-#if FDX_EMIT_NT
+        auto fst = [](auto *p, auto v) {  // feature-table store: nontemporal, the step never reads it
             __builtin_nontemporal_store(v, p);
-#else
-            *p = v;
-#endif
         };
         auto emit = [&]() {
             // the featurized row: a record at its input row (one random 80-byte write), or the
@@ -703,7 +690,6 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                 }
             }
         };
-        if constexpr (EMIT != 0 && FDX_EMIT_POS == 0) emit();
         uint16_t rq[W];
         bool rat_ok[W];
 #pragma unroll
@@ -746,7 +732,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                                                           (int64_t)max(cs[s] - 1, 0) * kW3Gap);
             // (stores issued behind the segment and ratio loads: waiting for those loads does
             // not wait for the stores -- vmcnt counts stores, in issue order)
-            if constexpr (EMIT != 0 && FDX_EMIT_POS == 1) emit();
+            if constexpr (EMIT != 0) emit();
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const float x = v[kW3Search[s]];
@@ -781,16 +767,83 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             dst[1] = live ? make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16)
                           : make_uint4(0, 0, 0, 0);
         }
-        if constexpr (EMIT != 0 && FDX_EMIT_POS == 2) emit();
         cur = nxt;
     };
-#if FDX_ZFILL_PEEL
-    if (i - lane < n) {
+    if (i - lane < n) {  // (the first iteration peeled)
         row_iter();
         i += stride;
     }
-#endif
     for (; i - lane < n; i += stride) row_iter();
+}
+
+
+// The featurized table alone (W = 3), for scoring rows that k_zfill_grouped_w3 does not build
+// (the wide layout, or a forest whose searched features outgrow the S-trees' LDS budget: the
+// rank rows then come from k_zfill_grouped).  Same columns, same arithmetic as k_zfill_grouped_w3's
+// emit: slot order writes every slot i < round_up(n, 64) (padding slots: row -1, zeros), input
+// order one fdx_feature_row at each live slot's row.
+template <int EMIT, bool COMPACT>
+__global__ void __launch_bounds__(256) k_feature_rows(
+    const int64_t *__restrict__ cts, const int32_t *__restrict__ cnb, const double *__restrict__ cval,
+    const int32_t *__restrict__ cust_perm, const int32_t *__restrict__ term_inv, const int64_t *__restrict__ term_rec,
+    int64_t n, int32_t flags_mode, int32_t val_is_sum, char *__restrict__ feat, int64_t fcap) {
+    constexpr int W = 3;
+    const int64_t end = EMIT == FDX_ROWS_SLOT_ORDER ? (n + 63) / 64 * 64 : n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = i < n ? (cust_perm ? cust_perm[i] : (int32_t)i) : -1;
+        const bool live = r >= 0;
+        if (EMIT == FDX_ROWS_INPUT_ORDER && !(live && (uint64_t)r < (uint64_t)fcap)) continue;
+        uint32_t c[W] = {0u, 0u, 0u}, tn[W] = {0u, 0u, 0u}, fl = 0u;
+        double avg[W] = {0.0, 0.0, 0.0}, rk[W] = {0.0, 0.0, 0.0};
+        if (live) {
+            bool we, ni;
+            day_flags(cts[i], flags_mode, we, ni);
+            fl = (uint32_t)we | (uint32_t)ni << 8;
+            const int64_t q = term_inv ? (int64_t)term_inv[r] : (int64_t)r;
+            int64_t tw[3];
+            if constexpr (COMPACT) {
+                compact_load(term_rec, q, tw);
+            } else {
+#pragma unroll
+                for (int w = 0; w < W; ++w) tw[w] = term_rec[q * W + w];
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const int32_t cw = cnb[(int64_t)w * n + i];
+                const double cv = cval[(int64_t)w * n + i];
+                c[w] = (uint32_t)cw;
+                avg[w] = (val_is_sum & 1) ? cv / (double)cw : cv;
+                tn[w] = (uint32_t)term_nb(tw[w]);
+                rk[w] = term_risk(tw[w]);
+            }
+        }
+        if constexpr (EMIT == FDX_ROWS_SLOT_ORDER) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(w, fcap))[i] = c[w];
+                reinterpret_cast<uint32_t *>(feat + FDX_FEATURE_COL(3 + w, fcap))[i] = tn[w];
+                reinterpret_cast<double *>(feat + FDX_FEATURE_COL(6 + w, fcap))[i] = avg[w];
+                reinterpret_cast<double *>(feat + FDX_FEATURE_COL(9 + w, fcap))[i] = rk[w];
+            }
+            reinterpret_cast<int32_t *>(feat + FDX_FEATURE_COL(12, fcap))[i] = live ? r : -1;
+            reinterpret_cast<uint16_t *>(feat + FDX_FEATURE_COL(13, fcap))[i] = (uint16_t)fl;
+        } else {
+            fdx_feature_row *o = reinterpret_cast<fdx_feature_row *>(feat) + r;
+            fdx_feature_row v;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                v.cust_nb[w] = (int32_t)c[w];
+                v.term_nb[w] = (int32_t)tn[w];
+                v.cust_avg[w] = avg[w];
+                v.term_risk[w] = rk[w];
+            }
+            v.weekend = (uint8_t)(fl & 1u);
+            v.night = (uint8_t)(fl >> 8);
+            v.pad[0] = v.pad[1] = 0;
+            v.row = r;
+            *o = v;
+        }
+    }
 }
 
 }  // namespace
@@ -1014,9 +1067,25 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
         FDX_LAUNCHED("k_zfill_grouped_w3");
         return FDX_OK;
     }
-    FDX_REQUIRE(!rows_out_d, "feature rows: n_windows = 3, compact terminal records and the rank layout only");
+    // (the wide layout, or a forest whose searched features outgrow the S-trees' LDS budget)
+    FDX_REQUIRE(!rows_out_d || n_windows == 3, "the featurized table has 3 windows (n_windows = %d)", n_windows);
     FDX_PREP(k_zfill_grouped, dim3(grid), st, cust_ts_d, cust_amount_d, cust_nb_d, cust_avg_d, cust_perm_d,
              term_inv_d, term_rec_d, n, n_windows, flags_mode, cust_val_is_sum, F->mean_d, F->scale_d, (void *)z, flag);
     FDX_LAUNCHED("k_zfill_grouped");
+    if (rows_out_d) {
+        char *feat = reinterpret_cast<char *>(rows_out_d);
+        const int32_t vs = cust_val_is_sum & 1;
+#define FDX_ROWS_K(E, C)                                                                                          \
+    hipLaunchKernelGGL((k_feature_rows<E, C>), dim3(stream_grid(n, 256)), dim3(256), 0, st, cust_ts_d, cust_nb_d,  \
+                       cust_avg_d, cust_perm_d, term_inv_d, term_rec_d, n, flags_mode, vs, feat, out_cap)
+        const bool compact = (cust_val_is_sum & 4) != 0;
+        if (rows_order == FDX_ROWS_SLOT_ORDER) {
+            if (compact) FDX_ROWS_K(FDX_ROWS_SLOT_ORDER, true); else FDX_ROWS_K(FDX_ROWS_SLOT_ORDER, false);
+        } else {
+            if (compact) FDX_ROWS_K(FDX_ROWS_INPUT_ORDER, true); else FDX_ROWS_K(FDX_ROWS_INPUT_ORDER, false);
+        }
+#undef FDX_ROWS_K
+        FDX_LAUNCHED("k_feature_rows");
+    }
     return FDX_OK;
 }

@@ -71,10 +71,7 @@ __device__ __forceinline__ void walk_step(const uint64_t *s_nodes, const char *g
 // wave-uniform exit test between blocks (all chains of the wave at leaves).  In-distribution
 // rows of the bench forest end at ~5 nodes (depth 20), far-out rows run all 20 steps; testing
 // every kExitEvery steps keeps the test's cost small in the second case.
-#ifndef FDX_EXIT_EVERY
-#define FDX_EXIT_EVERY 4
-#endif
-constexpr int kExitEvery = FDX_EXIT_EVERY;
+constexpr int kExitEvery = 4;
 template <bool NAN_AWARE, bool LDS, int XSTRIDE, int K>
 __device__ __forceinline__ void walk_group(const uint64_t *s_nodes, const char *gbase, const float *const (&xcol)[K],
                                            uint32_t (&p)[K], uint64_t (&nd)[K], int depth) {
@@ -279,6 +276,27 @@ __device__ __forceinline__ void rank_walk(const char *lds, const uint32_t (&lane
 // return in order): fewer issue slots per step.
 // `pre` steps run before the first exit test (the caller's estimate of the steps the wave will
 // need: extra steps at leaves are fixed points); returns the steps run (wave-uniform).
+// PIPE = 102 (chains in interleaved pairs; u32 planes, the default variant):
+// the group's VALU of a phase issued round-robin over its chains (sub, sub, and, and, med3,
+// med3, ...), so that no instruction waits on the one issued right before it, then the group's
+// reads; one asm block per group and phase.
+// The step of two chains (u32 planes): d = x - nd, st = med3(d, 1, nd & 0xFFF), pa += 4 st.
+__device__ __forceinline__ void il_node2(uint32_t &p0, uint32_t &p1, uint32_t x0, uint32_t x1, uint32_t n0, uint32_t n1) {
+    uint32_t d0, d1, o0, o1;
+    asm("v_sub_u32 %[d0], %[x0], %[n0]\n\tv_sub_u32 %[d1], %[x1], %[n1]\n\t"
+        "v_and_b32 %[o0], 0xfff, %[n0]\n\tv_and_b32 %[o1], 0xfff, %[n1]\n\t"
+        "v_med3_i32 %[d0], %[d0], 1, %[o0]\n\tv_med3_i32 %[d1], %[d1], 1, %[o1]\n\t"
+        "v_lshl_add_u32 %[p0], %[d0], 2, %[p0]\n\tv_lshl_add_u32 %[p1], %[d1], 2, %[p1]"
+        : [p0] "+v"(p0), [p1] "+v"(p1), [d0] "=&v"(d0), [d1] "=&v"(d1), [o0] "=&v"(o0), [o1] "=&v"(o1)
+        : [x0] "v"(x0), [x1] "v"(x1), [n0] "v"(n0), [n1] "v"(n1));
+}
+__device__ __forceinline__ void il_node1(uint32_t &p0, uint32_t x0, uint32_t n0) {
+    uint32_t d0, o0;
+    asm("v_sub_u32 %[d0], %[x0], %[n0]\n\tv_and_b32 %[o0], 0xfff, %[n0]\n\t"
+        "v_med3_i32 %[d0], %[d0], 1, %[o0]\n\tv_lshl_add_u32 %[p0], %[d0], 2, %[p0]"
+        : [p0] "+v"(p0), [d0] "=&v"(d0), [o0] "=&v"(o0) : [x0] "v"(x0), [n0] "v"(n0));
+}
+
 template <int P16, int K, int PW>
 __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                               uint32_t (&nd)[K], int depth, int pre = 0) {
@@ -288,6 +306,30 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
     auto step = [&]() {
+        if constexpr (PW >= 100) {
+            static_assert(PW == 102 && P16 == 0, "interleaved pairs: u32 planes");
+#pragma unroll
+            for (int g = 0; g < K; g += 2) {
+                if (g + 1 < K) {
+                    il_node2(pa[g], pa[g + 1], x[g], x[g + 1], nd[g], nd[g + 1]);
+                    nd[g + 1] = lds32(lds, pa[g + 1]);
+                    nd[g] = lds32(lds, pa[g]);
+                } else {
+                    il_node1(pa[g], x[g], nd[g]);
+                    nd[g] = lds32(lds, pa[g]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int g = 0; g < K; g += 2) {
+                const uint32_t a0 = (nd[g] & kSlotMask<P16>) | lane_base[g];
+                const uint32_t a1 = g + 1 < K ? (nd[g + 1] & kSlotMask<P16>) | lane_base[g + 1] : 0u;
+                x[g] = rank_x<P16>(lds, a0);
+                if (g + 1 < K) x[g + 1] = rank_x<P16>(lds, a1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return;
+        }
 #pragma unroll
         for (int g = 0; g < K; g += PW) {
 #pragma unroll
@@ -443,24 +485,13 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
-// A/B switch (compile time): the u32 row planes written by ds_write_addtid_b32 (1) or ds_write_b32 (0)
-#ifndef FDX_STAGE_ADDTID
-#define FDX_STAGE_ADDTID 1
-#endif
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // The 15 u32 plane words of row slot r * BLOCK + tid (rank << 16, NaN 0xFFFFFFFF).  With
 // ds_write_addtid_b32 (address = M0 + offset + 4 * lane; no address VGPR) a store moves 4 B per
 // lane in 2 LDS cycles, half of ds_write_b32's 4: the planes are re-staged for every 1,024-row
 // tile, 15 stores per lane against ~220 walk reads.  The kernel's code uses M0 nowhere else.
 template <int BLOCK>
-__device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uint32_t (&w)[8]) {
-    uint32_t x[15];
-#pragma unroll
-    for (int f = 0; f < 15; ++f) {
-        const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-        x[f] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
-    }
-#if FDX_STAGE_ADDTID
+__device__ __forceinline__ void stage_words(uint32_t *s_x, int r, const uint32_t (&x)[15]) {
     static_assert(14 * kRankPlaneRows * 4 < 65536, "plane offsets fit the 16-bit instruction offset");
     const uint32_t b = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(lds_u32 *)(s_x + r * BLOCK + (threadIdx.x & ~63u)));
@@ -489,10 +520,23 @@ __device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uin
           "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14])
         : "memory", "m0");
 #pragma clang diagnostic pop
-#else
+}
+// nan: the batch has NaN features (rank 0xFFFF -> 0xFFFFFFFF, the NaN-aware walk's marker: three
+// VALU per feature); without NaNs one VALU per feature (a shift or a mask of the rank pair)
+template <int BLOCK>
+__device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uint32_t (&w)[8], bool nan) {
+    uint32_t x[15];
+    if (nan) {
 #pragma unroll
-    for (int f = 0; f < 15; ++f) s_x[f * kRankPlaneRows + r * BLOCK + threadIdx.x] = x[f];
-#endif
+        for (int f = 0; f < 15; ++f) {
+            const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
+            x[f] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
+        }
+    } else {
+#pragma unroll
+        for (int f = 0; f < 15; ++f) x[f] = (f & 1) ? w[f >> 1] & 0xFFFF0000u : w[f >> 1] << 16;
+    }
+    stage_words<BLOCK>(s_x, r, x);
 }
 
 template <int BLOCK, int R, int G, int P16, int PIPE>
@@ -520,7 +564,8 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     }
     static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
     static_assert(BLOCK % 64 == 0, "whole waves (the u16 plane swizzle)");
-    constexpr int K = R * G;
+    constexpr int K = R * G;  // chains per lane of one walk group
+    (void)K;
     constexpr int kRowsPerBlock = BLOCK * R;
     constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
     __shared__ __align__(16) uint32_t s_mem[kXW + kNodeWords];
@@ -544,7 +589,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     // groups -- and the 32 lanes of a group read 32 different banks whatever features they test
     // (natural order put rows 2i, 2i+1 in one group: a 2-way conflict whenever their features
     // differ).  u32 planes are conflict-free in natural order.
-    const int pslot = P16 ? ((tid & ~63) | ((tid & 31) << 1) | ((tid >> 5) & 1)) : tid;
+    const int pslot = (P16 == 2 || P16 == 3) ? ((tid & ~63) | ((tid & 31) << 1) | ((tid >> 5) & 1)) : tid;
     uint32_t lrow[R];
 #pragma unroll
     for (int r = 0; r < R; ++r)  // compact planes: the byte address of the dword holding the lane's u16
@@ -565,7 +610,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 q2[r] = src[2];
                 q3[r] = src[3];
             }
-            pacc[r] = (first || !okr) ? 0.0 : acc[rw];
+            pacc[r] = first ? 0.0 : acc[okr ? rw : r0];  // (unconditional load: see out_slots)
         }
     };
     if (base < r1) fetch(base);
@@ -595,14 +640,23 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
 #pragma unroll
         for (int g = 0; g < NT; ++g) {
             rp[g] = kNB + (uint32_t)(root[t0 + g] - node_base) * 4u;
-            rn[g] = lds32(lds, rp[g]);
+            rn[g] = __builtin_amdgcn_readfirstlane(lds32(lds, rp[g]));  // uniform: SGPRs
             dmax = max(dmax, depth[t0 + g]);
         }
-        auto out_slot = [&](int64_t rw) -> int32_t {  // loaded here, used one tile later
-            return rw < r1 ? (last && out_perm ? out_perm[rw] : (int32_t)rw) : -1;
-        };
+        // the tile's output slots, loaded with its rank rows and used one tile later.  The load is
+        // unconditional (index clamped into the batch; rows past r1 are never stored: okp), in a
+        // wave-uniform branch: a lane-conditional load merged into its destination at a join made
+        // the compiler wait there with vmcnt(0) -- for every load in flight, i.e. for the next
+        // tile's rank rows right after issuing them, once per tile (r04 ISA; ~100 us per launch)
+        const bool perm_out = last && out_perm;
+        auto out_slots = [&](int64_t b) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) dst_n[r] = out_slot(base + r * BLOCK + tid);
+            for (int r = 0; r < R; ++r) {
+                const int64_t rw = b + r * BLOCK + tid;
+                dst_n[r] = perm_out ? out_perm[rw < r1 ? rw : r1 - 1] : (int32_t)rw;
+            }
+        };
+        out_slots(base);
         auto fold = [&]() {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -622,10 +676,18 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 }
             }
         };
-        for (; base < r1; base += stride) {
-            int64_t row[R];
-            bool ok[R];
-            double a[R];
+        // Tile loop: the next tile's rank rows, running sums and output slots are loaded at the TOP
+        // of an iteration and staged at its END (after this tile's walk, fold and leaf-value
+        // loads), so no prefetched register is carried around the loop.  Carried prefetch
+        // registers were copied at the latch or the head, behind a vmcnt(0) that waited for every
+        // load in flight (the next tile's rows right after issuing them, or the leaf gather just
+        // issued), once per tile (r04 ISA: ~100 us per launch).  The wait before the staging
+        // leaves the leaf loads in flight (in-order vmcnt: they are younger).
+        int64_t row[R];
+        bool ok[R];
+        double a[R];
+        int32_t dst[R];
+        auto stage_tile = [&]() {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 row[r] = base + r * BLOCK + tid;
@@ -639,7 +701,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 } else {
                     const uint32_t w8[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
                     if constexpr (P16 == 0) {
-                        stage_planes_u32<BLOCK>(s_x, r, w8);
+                        stage_planes_u32<BLOCK>(s_x, r, w8, any_nan);
                     } else {
 #pragma unroll
                         for (int f = 0; f < 16; ++f)
@@ -647,15 +709,15 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                     }
                 }
                 a[r] = pacc[r];
+                dst[r] = dst_n[r];
             }
-            int32_t dst[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) dst[r] = dst_n[r];
-            if (base + stride < r1) {
-                fetch(base + stride);
-#pragma unroll
-                for (int r = 0; r < R; ++r) dst_n[r] = out_slot(base + stride + r * BLOCK + tid);
-            }
+        };
+        if (base < r1) stage_tile();  // (the first tile's rows were fetched before the node fill)
+        while (base < r1) {
+            // unconditional (fetch clamps rows past r1 to r0): a conditional load left its
+            // registers to be merged at a join, behind a vmcnt(0) right after the loads
+            fetch(base + stride);
+            out_slots(base + stride);
             uint32_t pt[R * NT];
             // the previous tile's step count, less one exit interval, runs without exit tests
             // (rows of the bench forest walk ~20 of 20 steps: 5 tests per tile otherwise); when
@@ -672,6 +734,9 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 dstp[r] = dst[r];
                 okp[r] = ok[r];
             }
+            base += stride;
+            if (base >= r1) break;
+            stage_tile();
         }
         fold();
     };
@@ -691,6 +756,9 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
 #undef FDX_ONE_GROUP
         return;
     }
+    // the generic tile loop (leaf ids, per-tree values, chunks of more trees than one group):
+    // two rows per lane walk groups of 3 trees (6 chains) to stay within the register budget
+    constexpr int GG = R == 2 ? 3 : G;
     for (; base < r1; base += stride) {
         int64_t row[R];
         bool ok[R];
@@ -708,7 +776,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             } else {
                 const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
                 if constexpr (P16 == 0) {
-                    stage_planes_u32<BLOCK>(s_x, r, w);
+                    stage_planes_u32<BLOCK>(s_x, r, w, any_nan);
                 } else {
 #pragma unroll
                     for (int f = 0; f < 16; ++f)
@@ -718,26 +786,26 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             a[r] = pacc[r];
         }
         if (base + stride < r1) fetch(base + stride);
-        double pv[K];
+        double pv[R * GG];
         bool pending = false;
         int t = t0;
-        for (; t + G <= t1; t += G) {
-            uint32_t pa[K];
-            rank_trees<R, G, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
-            if (pending) rank_accumulate<R, G>(a, pv);
-            rank_leaf_values<K>(pa, node_base, lval, pv, kNB);
-            if (tv) rank_tree_values<R, G>(pv, t, row, ok, tv, tv_n);
+        for (; t + GG <= t1; t += GG) {
+            uint32_t pa[R * GG];
+            rank_trees<R, GG, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pa);
+            if (pending) rank_accumulate<R, GG>(a, pv);
+            rank_leaf_values<R * GG>(pa, node_base, lval, pv, kNB);
+            if (tv) rank_tree_values<R, GG>(pv, t, row, ok, tv, tv_n);
             pending = true;
-            if (leaf_out) rank_leaf_ids<R, G>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees, kNB);
+            if (leaf_out) rank_leaf_ids<R, GG>(pa, node_base, t, row, ok, out_perm, leaf_out, orig, n_trees, kNB);
         }
         const int nt = t1 - t;
 #define FDX_RANK_TAIL(NT)                                                                                  \
-    if constexpr (G > NT) {                                                                                \
+    if constexpr (GG > NT) {                                                                                \
         if (nt == NT) {                                                                                    \
             uint32_t pt[R * NT];                                                                           \
             double vt[R * NT];                                                                             \
             rank_trees<R, NT, P16, PIPE>(lds, lrow, t, root, depth, node_base, any_nan, ml, pt);           \
-            if (pending) rank_accumulate<R, G>(a, pv);                                                     \
+            if (pending) rank_accumulate<R, GG>(a, pv);                                                     \
             pending = false;                                                                               \
             rank_leaf_values<R * NT>(pt, node_base, lval, vt, kNB);                                        \
             if (tv) rank_tree_values<R, NT>(vt, t, row, ok, tv, tv_n);                                     \
@@ -755,7 +823,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         FDX_RANK_TAIL(8)
         FDX_RANK_TAIL(9)
 #undef FDX_RANK_TAIL
-        if (pending) rank_accumulate<R, G>(a, pv);
+        if (pending) rank_accumulate<R, GG>(a, pv);
         if (tv) continue;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1213,7 +1281,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 2); break;
+                default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK
             FDX_LAUNCHED("k_forest_rank");

@@ -140,12 +140,16 @@ struct Variant {
 };
 constexpr Variant kVariants[] = {
     {512, 1, 4, 0, 0, 0},    // 0: wide layout
-    {1024, 1, 10, 1, 0, 2},  // 1: rank layout v1, 10 chains per lane (the default: r03 sweep, 7.63 vs
-                             //    8.43 ms for 6 chains at config 2; 12 chains spill, 11.7 ms)
+    {1024, 1, 10, 1, 0, 102},  // 1: rank layout v1, 10 chains per lane (the default: r03 sweep, 7.63 vs
+                               //    8.43 ms for 6 chains at config 2; 12 chains spill, 11.7 ms), each
+                               //    step's VALU interleaved over chain pairs (r05: 6.51 -> 6.43 ms)
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
 };
+// (Round 5 measured v1 over paired u16 planes, two rows per lane with 768 / 512 lanes (12 chains
+// per lane, 12 / 8 waves per CU): 7.90 / 8.74 ms against 6.66 -- the walk's throughput follows
+// the waves per CU, not the chains per lane -- and removed them.)
 // (Round 4 measured compact v2 with 8 / 10 chains as well -- 7.27 ms against 6.91 for variant 1,
 // the extra depth of its jump nodes, profiles/r04e_forest_launches.txt -- and removed them.)
 // (Round 3 also measured v1 with 6 / 8 / 9 chains, compact v2 with 10 chains and register

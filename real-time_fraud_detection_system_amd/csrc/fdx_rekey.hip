@@ -23,19 +23,6 @@ constexpr int kMaxBins = 512;
 constexpr int kBlock = 256;
 constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096 keys per tile
-// A/B switch (compile time): when the scatter loads its payload streams (0: each after the
-// previous phase's stores; 1: stream 0 behind the key re-order, stream q + 1 during stream q's;
-// 2: stream 0 with the keys)
-#ifndef FDX_RADIX_PREFETCH
-#define FDX_RADIX_PREFETCH 1
-#endif
-constexpr int kRadixPrefetch = FDX_RADIX_PREFETCH;
-// A/B switch (compile time): k_radix_hist's counts by LDS atomics (1; re-keys 0.585 / 0.553 -> 0.553 /
-// 0.534 ms, profiles/r03am_radix_hist_ab.txt) or ballot multisplit (0)
-#ifndef FDX_RADIX_HIST_ATOMIC
-#define FDX_RADIX_HIST_ATOMIC 1
-#endif
-constexpr bool kHistAtomic = FDX_RADIX_HIST_ATOMIC != 0;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // ---------------------------------------------------------------- device-wide scan
@@ -149,9 +136,9 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, K flip) {
 // Per-tile digit counts, in the scatter's blocked order (wave w counts the 1,024 consecutive
 // keys [w * 1024, (w + 1) * 1024) of the tile).  Each wave keeps its own LDS counters (one
 // block-shared atomicAdd per key spent ~70 % of its LDS cycles on same-address conflicts, r02
-// PMC); by default each key is one LDS atomic add on them (kHistAtomic), else only the lowest
-// lane of each group of equal digits (ballot multisplit) adds the group's size -- no two lanes
-// on one counter, but BITS ballots per key, which the counts alone do not need.
+// PMC); each key is one LDS atomic add on them (the ballot multisplit -- only the lowest lane
+// of each group of equal digits adds the group's size -- took BITS ballots per key, which the
+// counts alone do not need: re-keys 0.585 / 0.553 -> 0.553 / 0.534 ms, r03am_radix_hist_ab.txt).
 // bad != nullptr (first pass of fdx_rekey_payload_checked): also count the keys >= key_limit
 // (as unsigned: negative int32 ids count too) -- the id range check rides on this pass's reads.
 template <typename K, int BITS>
@@ -166,7 +153,6 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
     for (int d = tid; d < kWavesPerBlock * kBins; d += kBlock) (&s_h[0][0])[d] = 0;
     __syncthreads();
     const int64_t wbase = (int64_t)blockIdx.x * kTile + (int64_t)wv * kWaveSpan + lane;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t *h = s_h[wv];
     K key[kItems];
 #pragma unroll
@@ -174,28 +160,11 @@ __global__ void __launch_bounds__(kBlock) k_radix_hist(const K *__restrict__ key
         const int64_t i = wbase + (int64_t)r * kWave;
         key[r] = i < n ? keys[i] : (K)0;
     }
-    if constexpr (kHistAtomic) {
-        // counts only (no ranks): one LDS atomic add per key on the wave's own counters -- lanes
-        // of one digit in one instruction serialise on their address, which costs less than the
-        // BITS ballots per key of the multisplit
+    // counts only (no ranks): one LDS atomic add per key on the wave's own counters -- lanes of
+    // one digit in one instruction serialise on their address
 #pragma unroll
-        for (int r = 0; r < kItems; ++r)
-            if (wbase + (int64_t)r * kWave < n) atomicAdd(&h[digit_of<K, BITS>(key[r], shift, flip)], 1u);
-    } else {
-#pragma unroll
-        for (int r = 0; r < kItems; ++r) {
-            const bool valid = wbase + (int64_t)r * kWave < n;
-            const uint32_t d = digit_of<K, BITS>(key[r], shift, flip);
-            uint64_t peers = __ballot(valid);
-#pragma unroll
-            for (int b = 0; b < BITS; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const uint64_t bb = __ballot(bit);
-                peers &= bit ? bb : ~bb;
-            }
-            if (valid && (peers & lt_mask) == 0) h[d] += (uint32_t)__popcll(peers);
-        }
-    }
+    for (int r = 0; r < kItems; ++r)
+        if (wbase + (int64_t)r * kWave < n) atomicAdd(&h[digit_of<K, BITS>(key[r], shift, flip)], 1u);
     if (bad) {
         int nb = 0;
 #pragma unroll
@@ -311,16 +280,14 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     else
         load_items(std::false_type{});
     // payload registers: stream q's 16 values of this lane, coalesced in input order (clamped:
-    // no branch); with kRadixPrefetch the loads of stream 0 go out before the key phases and
-    // those of stream q + 1 while stream q is re-ordered, instead of each after the previous
-    // phase's stores
+    // no branch); the loads of stream 0 go out behind the key re-order and those of stream q + 1
+    // while stream q is re-ordered (r03: each after the previous phase's stores, or stream 0 with
+    // the keys -- 170 VGPRs -- measured slower)
     uint64_t pv[PW > 0 ? kItems : 1];
     auto load_pay = [&](const uint64_t *pin) {
 #pragma unroll
         for (int r = 0; r < kItems; ++r) pv[r] = pin[min(wbase + (int64_t)r * kWave, n - 1)];
     };
-    if constexpr (PW > 0)
-        if (kRadixPrefetch == 2) load_pay(p0_in);
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const int64_t i = wbase + (int64_t)r * kWave;
@@ -388,8 +355,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
             s_val[p] = val[r];
         }
     }
-    if constexpr (PW > 0)
-        if (kRadixPrefetch == 1) load_pay(p0_in);
+    if constexpr (PW > 0) load_pay(p0_in);
     __syncthreads();
     const int64_t tcnt = std::min<int64_t>(kTile, n - base);
     int32_t dsts[kItems];  // destination of tile position tid + j * kBlock
@@ -409,12 +375,11 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
 #pragma unroll
         for (int q = 0; q < PW; ++q) {
             uint64_t *pout = q == 0 ? p0_out : p1_out;
-            if (kRadixPrefetch == 0) load_pay(q == 0 ? p0_in : p1_in);
             __syncthreads();  // the previous contents of the LDS slots are consumed
 #pragma unroll
             for (int r = 0; r < kItems; ++r)
                 if (wbase + (int64_t)r * kWave < n) s_pay[pos[r]] = pv[r];
-            if (kRadixPrefetch != 0 && q + 1 < PW) load_pay(p1_in);
+            if (q + 1 < PW) load_pay(p1_in);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kItems; ++j) {

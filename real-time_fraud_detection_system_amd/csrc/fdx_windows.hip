@@ -554,19 +554,11 @@ __global__ void __launch_bounds__(256) k_interleave(
 constexpr int kChunk = 16;   // rows per cooperative load; divides every ring size below
 // walk length classes: groups whose longest segment has >= kWalkSplitRows rows use the 256-row
 // ring on the fork stream (fdx_customer_windows_walk)
-#ifndef FDX_WALK_SPLIT  // walk launch shape: compile-time A/B only (tools/build_ab.sh, tools/walk_ab.py)
-#define FDX_WALK_SPLIT 480
-#endif
-#ifndef FDX_WALK_LP  // waves per group, long class
-#define FDX_WALK_LP 2
-#endif
-#ifndef FDX_WALK_SP  // waves per group, short class
-#define FDX_WALK_SP 1
-#endif
-#ifndef FDX_WALK_SINGLE  // one launch (256-row ring, FDX_WALK_LP waves per group) for every group
-#define FDX_WALK_SINGLE 0
-#endif
-constexpr int kWalkSplitRows = FDX_WALK_SPLIT;
+// (r03 walk shapes: 3 waves per long group 0.94 ms, both classes split 1.08-1.11, one launch for
+// every group 0.80, against 0.78 for this one: profiles/r03i_walk_shapes.jsonl, r03j_*)
+constexpr int kWalkSplitRows = 480;
+constexpr int kWalkLongWaves = 2;   // waves per group, long class (11 + 10 customers)
+constexpr int kWalkShortWaves = 1;  // waves per group, short class
 
 // kRing rows per segment stay in LDS.  Launched once per ring size over length classes of
 // groups (a block outside [lg_min, lg_max) exits at once): long segments belong to busy
@@ -1088,11 +1080,6 @@ constexpr int kTermLdsRows = 1024;  // rows of one segment staged per wave (12 K
 // stage (3 KB per wave instead of 12: about twice the resident waves for this latency-bound
 // kernel), the longer ones in a second launch with the full stage (see terminal_launch).
 constexpr int kTermShortRows = 256;
-// A/B switch (compile time): the W = 3 short pass with all searches interleaved
-#ifndef FDX_TERM_SHORT_NW
-#define FDX_TERM_SHORT_NW 1
-#endif
-constexpr bool kTermShortNW = FDX_TERM_SHORT_NW != 0;
 
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
@@ -1121,11 +1108,6 @@ __device__ __forceinline__ void term_store(int32_t *nb_out, double *risk_out, in
 // staged in LDS; a long segment does not use the LDS stage, so its run list takes the stage's
 // timestamp words instead (kMaxRunsLong entries).
 constexpr int kMaxRuns = 64;
-// A/B switch (compile time): W = 3 count records stored as two wide stores
-#ifndef FDX_REC_PAIR
-#define FDX_REC_PAIR 1
-#endif
-constexpr bool kRecPair = FDX_REC_PAIR != 0;
 
 // One row's window counts out: the compact W = 3 record (+ the full record in the overflow
 // area), the 24-byte record as two stores (8 + 16 or 16 + 8 bytes by its 16-byte alignment:
@@ -1147,7 +1129,7 @@ __device__ __forceinline__ void term_emit(int32_t *nb_out, double *risk_out, int
             hi = 0;
         }
         *reinterpret_cast<longlong2 *>(rec_out + 2 * row) = make_longlong2(lo, hi);
-    } else if (rec_out && n_win == 3 && kRecPair && ((uintptr_t)rec_out & 15) == 0) {
+    } else if (rec_out && n_win == 3 && ((uintptr_t)rec_out & 15) == 0) {
         int64_t *dst = rec_out + row * 3;
         const int64_t w0 = term_word(cn[0], cf[0]), w1 = term_word(cn[1], cf[1]), w2 = term_word(cn[2], cf[2]);
         if ((row & 1) == 0) {
@@ -1662,7 +1644,7 @@ static void terminal_launch(bool runs, const int64_t *gts, const uint8_t *gfr, c
         FDX_TERM_LAUNCH(true, kTermShortRows, 0, kTermShortRows);
         FDX_TERM_LAUNCH(true, kTermLdsRows, lo, inf);
     } else {
-        if (n_windows == 3 && kTermShortNW)
+        if (n_windows == 3)  // every search of a segment interleaved
             hipLaunchKernelGGL(k_terminal_short<3>, dim3(grid), dim3(kTermBlock), 0, st, gts, gfr, rows, seg_off,
                                n_seg, n, delay_ns, wa, n_windows, nb_d, risk_d, rec_d, compact_n);
         else
@@ -2056,22 +2038,16 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
                            STREAM, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, \
                            starts_d, LO, HI);                                                                  \
     FDX_LAUNCHED("k_customer_walk")
-#if FDX_WALK_SINGLE
-    (void)split;
-    FDX_WALK((21 + FDX_WALK_LP - 1) / FDX_WALK_LP, 256, FDX_WALK_LP, st, 0, INT32_MAX);
-    return FDX_OK;
-#else
     ForkStream *f;
     int rc = fork_stream(&f);
     if (rc) return rc;
     FDX_HIP(hipEventRecord(f->fork, st));
     FDX_HIP(hipStreamWaitEvent(f->side, f->fork, 0));
-    FDX_WALK((21 + FDX_WALK_LP - 1) / FDX_WALK_LP, 256, FDX_WALK_LP, f->side, split, INT32_MAX);
-    FDX_WALK((21 + FDX_WALK_SP - 1) / FDX_WALK_SP, 128, FDX_WALK_SP, st, 0, split);
+    FDX_WALK((21 + kWalkLongWaves - 1) / kWalkLongWaves, 256, kWalkLongWaves, f->side, split, INT32_MAX);
+    FDX_WALK((21 + kWalkShortWaves - 1) / kWalkShortWaves, 128, kWalkShortWaves, st, 0, split);
     FDX_HIP(hipEventRecord(f->join, f->side));
     FDX_HIP(hipStreamWaitEvent(st, f->join, 0));
     return FDX_OK;
-#endif
 #undef FDX_WALK
 }
 

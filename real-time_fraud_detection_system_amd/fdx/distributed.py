@@ -30,6 +30,7 @@ import torch.distributed as dist
 
 from . import _lib, ops
 from ._lib import check
+from .pipeline import check_rows_out
 
 
 class GpuKernels:
@@ -93,6 +94,14 @@ P2P_CHUNK_BYTES = 256 << 20
 _SHARD_SIDE_PRIORITY = -1
 
 
+def all_to_all_split_pairs(out, inp, group=None):
+    """The split-size exchange (one [world, 2] int64 tensor each way): RCCL all_to_all_single.
+    Module-level, like alltoallv, so that a test can route both through host memory (gloo on
+    one GPU, tests/test_gpu_sharded_world2.py)."""
+    dist.all_to_all_single(out, inp, group=group)
+    return out
+
+
 def alltoallv(out, inp, out_splits, in_splits, group=None):
     """all_to_all_single(out, inp, out_splits, in_splits) over rows of 2-D tensors: this
     rank's own block is a device copy, every other peer's block goes as point-to-point
@@ -132,7 +141,7 @@ def exchange_begin(K, term, world, group=None):
     # the pairs, taken on the host once they are read (exchange_finish) -- no device arithmetic
     send_pairs = send_seg.unfold(0, 2, 1).contiguous()    # [world, 2] int64 (a copy)
     recv_pairs = torch.empty_like(send_pairs)
-    dist.all_to_all_single(recv_pairs, send_pairs, group=group)
+    all_to_all_split_pairs(recv_pairs, send_pairs, group)
     return send_perm, send_pairs, recv_pairs
 
 
@@ -271,6 +280,7 @@ class ShardedPipeline:
         mk = mark or (lambda _name, _st: None)
         p = self.pipe
         W = len(p.windows_days)
+        check_rows_out(rows_out, ts)
         base, n_local = self._range(n_customers_local)
         # The terminal exchange (RCCL all-to-all there and back + the owner-side windows)
         # runs on a side stream, overlapped with the customer half on the main stream; the
@@ -311,6 +321,7 @@ class ShardedPipeline:
         mk("customer_layout", main)
         rc.check()
         p._slots_hint = lay.its.numel()
+        p.last_slots = lay.n_slots  # (the FeatureTable's slots, as FraudPipeline.run_fused)
         if scan:
             inb, isum = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days, lay=lay)
         elif walk:

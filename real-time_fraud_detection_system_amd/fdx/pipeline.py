@@ -151,9 +151,7 @@ class FraudPipeline:
         W = len(self.windows_days)
         mk = mark or (lambda _name, _st: None)
         caller = stream or torch.cuda.current_stream()
-        if rows_out is not None and (rows_out.buf.device != ts_ns.device or
-                                     (isinstance(rows_out, ops.FeatureRecords) and rows_out.cap < ts_ns.numel())):
-            raise ValueError("rows_out must be an ops.FeatureRecords(n) / ops.FeatureTable on the inputs' device")
+        check_rows_out(rows_out, ts_ns)
         if ts_ns.numel() == 0:  # an empty table: nothing to score
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
@@ -170,80 +168,85 @@ class FraudPipeline:
             for t in (ts_ns, customer, terminal, amount, fraud, proba) + ((ws,) if ws is not None else ()) + \
                 ((rows_out.buf,) if rows_out is not None else ()):
                 t.record_stream(main)
-        with torch.cuda.stream(main):
-            mk("start", main)
-            side.wait_stream(main)
-            # customer half first (the critical path): the re-key carries ts and amount into
-            # grouped order
-            scan = self.avg_mode == "scan"
-            walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
-            # the id range checks ride on the re-keys' first histogram pass (bad counts), read once
-            # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
-            bad = torch.empty(2, dtype=torch.int32, device=ts_ns.device) if validate else None
-            cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
-                                                       bad=bad[0:1] if validate else None)
-            mk("rekey_customer", main)
-            # the walk's layout plan goes right behind the re-key; its slot count is read only
-            # after the terminal half is enqueued (no host wait between the two)
-            pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
-            if validate:  # (its pinned copy behind the plan, not in front of it: up to 38 us)
-                rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
-            # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
-            # perm); the records come out in input row order, read by the row assembly through irow.
-            # Allocated under the side stream's context, so that the caching allocator hands
-            # these buffers to nothing on the main stream while the side stream still uses them.
-            compact = self.compact_records and W == 3
-            with torch.cuda.stream(side):
-                mk("start", side)
-                tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side,
-                                                         bad=bad[1:2] if validate else None)
-                if validate:
-                    rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
-                mk("rekey_terminal", side)
-                if compact:
-                    trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                        windows_days=self.windows_days, stream=side)
+        # an error raised after work was enqueued (a layout refused, an undersized feature table,
+        # ids out of range) still joins the streams back to the caller's before it propagates
+        try:
+            with torch.cuda.stream(main):
+                mk("start", main)
+                side.wait_stream(main)
+                # customer half first (the critical path): the re-key carries ts and amount into
+                # grouped order
+                scan = self.avg_mode == "scan"
+                walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
+                # the id range checks ride on the re-keys' first histogram pass (bad counts), read once
+                # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
+                bad = torch.empty(2, dtype=torch.int32, device=ts_ns.device) if validate else None
+                cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
+                                                           bad=bad[0:1] if validate else None)
+                mk("rekey_customer", main)
+                # the walk's layout plan goes right behind the re-key; its slot count is read only
+                # after the terminal half is enqueued (no host wait between the two)
+                pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
+                if validate:  # (its pinned copy behind the plan, not in front of it: up to 38 us)
+                    rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
+                # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
+                # perm); the records come out in input row order, read by the row assembly through irow.
+                # Allocated under the side stream's context, so that the caching allocator hands
+                # these buffers to nothing on the main stream while the side stream still uses them.
+                compact = self.compact_records and W == 3
+                with torch.cuda.stream(side):
+                    mk("start", side)
+                    tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side,
+                                                             bad=bad[1:2] if validate else None)
+                    if validate:
+                        rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
+                    mk("rekey_terminal", side)
+                    if compact:
+                        trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                            windows_days=self.windows_days, stream=side)
+                    else:
+                        trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
+                                                            windows_days=self.windows_days, stream=side)
+                    mk("terminal_windows", side)
+                for t in (ts_ns, customer, terminal, fraud) + ((bad,) if validate else ()):
+                    t.record_stream(side)  # inputs in use on the side stream
+                try:
+                    if pending is not None:
+                        lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
+                    else:
+                        lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
+                                                  self.windows_days if walk else None, grouped=True)
+                except _lib.FdxError:
+                    if validate:  # ids outside the range are the likelier cause: report them
+                        for c in rc:
+                            c.check()
+                    raise
+                mk("customer_layout", main)
+                self._slots_hint = lay.its.numel()
+                self.last_slots = lay.n_slots
+                if scan:  # the windows straight from the grouped rows into the layout's slots
+                    inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
+                elif walk:
+                    inb, isum = ops.customer_windows_walk(lay, cseg, main)
                 else:
-                    trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                        windows_days=self.windows_days, stream=side)
-                mk("terminal_windows", side)
-            for t in (ts_ns, customer, terminal, fraud) + ((bad,) if validate else ()):
-                t.record_stream(side)  # inputs in use on the side stream
-            try:
-                if pending is not None:
-                    lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
-                else:
-                    lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
-                                              self.windows_days if walk else None, grouped=True)
-            except _lib.FdxError:
-                if validate:  # ids outside the range are the likelier cause: report them
+                    inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, main)
+                mk("customer_walk", main)
+                main.wait_stream(side)
+                trec.record_stream(main)
+                ws = self._forest_ws(lay.n_slots, ws, amount.device)
+                ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
+                                           ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact,
+                                           rows_out=rows_out)
+                mk("assemble_rows", main)
+                ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
+                mk("forest_traverse", main)
+                if validate:  # read once everything is enqueued (the counts ran in the re-keys)
                     for c in rc:
                         c.check()
-                raise
-            mk("customer_layout", main)
-            self._slots_hint = lay.its.numel()
-            self.last_slots = lay.n_slots
-            if scan:  # the windows straight from the grouped rows into the layout's slots
-                inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
-            elif walk:
-                inb, isum = ops.customer_windows_walk(lay, cseg, main)
-            else:
-                inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, main)
-            mk("customer_walk", main)
-            main.wait_stream(side)
-            trec.record_stream(main)
-            ws = self._forest_ws(lay.n_slots, ws, amount.device)
-            ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                       ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact,
-                                       rows_out=rows_out)
-            mk("assemble_rows", main)
-            ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
-            mk("forest_traverse", main)
-            if validate:  # read once everything is enqueued (the counts ran in the re-keys)
-                for c in rc:
-                    c.check()
-        if main is not caller:
-            caller.wait_stream(main)
+        finally:
+            if main is not caller:
+                main.wait_stream(side)
+                caller.wait_stream(main)
         return proba
 
     def _forest_ws(self, n_rows, ws, device):
@@ -253,6 +256,20 @@ class FraudPipeline:
         if self._ws is None or self._ws.numel() < need:
             self._ws = ops.workspace(need, device)
         return self._ws
+
+
+def check_rows_out(rows_out, ts_ns: torch.Tensor) -> None:
+    """rows_out of run_fused / ShardedPipeline.run, checked before anything is enqueued: an
+    ops.FeatureRecords of >= n records or an ops.FeatureTable of >= n slots (the layout's slot
+    count is >= n; its exact value is checked by the assembly), on the inputs' device."""
+    if rows_out is None:
+        return
+    if not isinstance(rows_out, (ops.FeatureRecords, ops.FeatureTable)):
+        raise TypeError("rows_out must be an ops.FeatureRecords or an ops.FeatureTable")
+    if rows_out.buf.device != ts_ns.device:
+        raise ValueError("rows_out must be on the inputs' device")
+    if rows_out.cap < ts_ns.numel():
+        raise ValueError(f"rows_out holds {rows_out.cap} rows / slots < n = {ts_ns.numel()}")
 
 
 def _to_caller_order(f: Features, tperm: torch.Tensor, stream) -> Features:

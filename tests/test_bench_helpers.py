@@ -92,10 +92,14 @@ def test_stage_table_medians_and_rejects_inflated_isolated_times():
 
 
 def test_bench_stream_splits_configs4_state_over_ranks():
-    """bench_stream.py --gpus N: the 1M / 2M-key state of configs[4] split over the ranks."""
-    import re
+    """bench_stream.py --gpus N: the 1M / 2M-key state of configs[4] split over the ranks --
+    contiguous customer ranges covering every id once, every rank with all terminal ids."""
+    import bench_stream
 
-    src = open(os.path.join(ROOT, "bench_stream.py")).read()
-    assert re.search(r'"--customers", type=int, default=1_000_000', src)
-    assert re.search(r'"--terminals", type=int, default=2_000_000', src)
-    assert "n_c = args.customers // world" in src and "configs[4]" in src
+    a = bench_stream.parse([])
+    assert (a.customers, a.terminals, a.batch) == (1_000_000, 2_000_000, 65536)
+    for world in (1, 2, 4, 8):
+        shards = [bench_stream.rank_shard(a, world, r) for r in range(world)]
+        covered = np.concatenate([np.arange(base, base + n_c) for n_c, base, _ in shards])
+        np.testing.assert_array_equal(covered, np.arange(1_000_000))
+        assert all(t == 2_000_000 for _, _, t in shards)

@@ -161,3 +161,77 @@ def test_config1_featurized_table_rows(dev, config1, order):
     small = ops.FeatureTable(64, dev) if order == "slot" else ops.FeatureRecords(n - 1, dev)
     with pytest.raises(ValueError):
         pipe.run_fused(*args, p_rows, rows_out=small)
+
+
+def _many_threshold_forest():
+    """14 complete depth-11 trees whose 28,658 internal nodes all test TX_AMOUNT at distinct
+    thresholds: more than the 26,240 thresholds per searched feature whose S-tree fits
+    k_zfill_grouped_w3's LDS budget, within rank layout v1's 32,766."""
+    rng = np.random.default_rng(5)
+    L, R, F, TH, ML, V, off = [], [], [], [], [], [], [0]
+    thr = rng.permutation(np.unique(np.round(rng.uniform(-1.2, 3.0, 60_000), 6)))[: 14 * 2047]
+    k = 0
+    for _ in range(14):
+        left, right, feat, th, ml, val = [], [], [], [], [], []
+
+        def build(d):
+            nonlocal k
+            i = len(left)
+            left.append(-1); right.append(-1); feat.append(-2); th.append(-2.0); ml.append(0)
+            val.append(float(rng.integers(0, 1000)) / 999.0)
+            if d < 11:
+                feat[i] = 0
+                th[i] = float(thr[k])
+                k += 1
+                left[i] = build(d + 1)
+                right[i] = build(d + 1)
+            return i
+
+        build(0)
+        L += left; R += right; F += feat; TH += th; ML += ml; V += val
+        off.append(off[-1] + len(left))
+    arrays = dict(left=np.array(L, np.int64), right=np.array(R, np.int64), feature=np.array(F, np.int64),
+                  threshold=np.array(TH), missing_left=np.array(ML, np.uint8), value1=np.array(V),
+                  node_offsets=np.array(off, np.int64))
+    return arrays
+
+
+@pytest.mark.parametrize("order", ["input", "slot"])
+def test_featurized_table_without_search_trees(dev, config1, order):
+    """the featurized table must not depend on the scoring rows' LDS budget.  A forest
+    whose searched feature has too many thresholds for k_zfill_grouped_w3's S-trees is scored
+    through the general assembly (k_zfill_grouped) and its table written by k_feature_rows:
+    every feature of every row equal to the C oracle, scores equal to the float64 path's."""
+    from table_check import assert_same_features, table_as_X
+
+    g, d, Xo = config1
+    _, mean, scale = _load("rf100_d20")
+    arrays = _many_threshold_forest()
+    forest = ops.Forest(arrays, 15, mean, scale)
+    import ctypes
+
+    from fdx import _lib
+    lay, ns = ctypes.c_int32(), ctypes.c_int32()
+    _lib.load().fdx_forest_layout(forest._h, ctypes.byref(lay), ctypes.byref(ns))
+    assert lay.value == 1  # rank layout v1 (ranks fit), S-trees refused by their LDS budget
+    pipe = FraudPipeline(forest=forest)
+    n = len(d["ts"])
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 5_000, 10_000)
+    rows = ops.FeatureTable(n * 11 // 10, dev) if order == "slot" else ops.FeatureRecords(n, dev)
+    rows.buf.fill_(0xAB)
+    p = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, p, rows_out=rows)
+    _, p64 = pipe.run(*args)
+    np.testing.assert_array_equal(p.cpu().numpy(), p64.cpu().numpy())
+    if order == "slot":
+        Xt = table_as_X(rows, pipe.last_slots, d["amount"])
+    else:
+        col = {k: v.cpu().numpy() for k, v in rows.columns().items()}
+        np.testing.assert_array_equal(col["row"], np.arange(n, dtype=np.int32))
+        Xt = np.zeros((n, 15))
+        Xt[:, 0] = d["amount"]
+        Xt[:, 1], Xt[:, 2] = col["weekend"], col["night"]
+        for w in range(3):
+            Xt[:, 3 + 2 * w], Xt[:, 4 + 2 * w] = col["cust_nb"][w], col["cust_avg"][w]
+            Xt[:, 9 + 2 * w], Xt[:, 10 + 2 * w] = col["term_nb"][w], col["term_risk"][w]
+    assert_same_features(Xt, Xo, f"table ({order} order) without S-trees vs oracle")

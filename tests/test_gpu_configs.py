@@ -20,6 +20,7 @@ import torch
 import oracle
 from fdx import _lib, ops, synth
 from fdx.pipeline import FraudPipeline
+from table_check import assert_same_features, table_as_X
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -69,12 +70,19 @@ def test_config2_full_size_fused_path_every_row(dev):
     pipe = FraudPipeline(forest=forest)
     proba = torch.empty(n, dtype=torch.float64, device=dev)
     ws = ops.workspace(forest.workspace_size(n * 11 // 10), dev)
-    pipe.run_fused(*args, 50_000, 100_000, proba, ws)
+    rows = ops.FeatureTable(n * 11 // 10, dev)  # the bench step's own featurized table
+    rows.buf.fill_(0xAB)
+    pipe.run_fused(*args, 50_000, 100_000, proba, ws, rows_out=rows)
     fused = proba.cpu().numpy()
+    m_slots = pipe.last_slots
     feats = pipe.featurize(*args, 50_000, 100_000)
     p64 = pipe.score(feats.X).cpu().numpy()
     np.testing.assert_array_equal(fused, p64)
     X = feats.X.cpu().numpy()
+    # every feature of every row of the fused path's table (interleave + walk + assembly) equals
+    # the float64 path's X, itself checked against the oracle on sampled segments below
+    assert_same_features(table_as_X(rows, m_slots, d["amount"]), X, "config 2 fused table")
+    del rows
     np.testing.assert_array_equal(X[:, 0], d["amount"])
     rows = _check_sampled_segments(d, X)
     assert rows > 10_000

@@ -10,6 +10,7 @@ import torch
 import oracle
 from fdx import ops
 from fdx.pipeline import FraudPipeline
+from table_check import assert_same_features, table_as_X
 
 pytestmark = pytest.mark.gpu
 NS = 1_000_000_000
@@ -48,10 +49,18 @@ def _run_all(dev, golden, d, n_c, n_t):
     assert X.shape == (n, 15)
     p_ref = pipe.score(feats.X).cpu().numpy()
     p = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
-    pipe.run_fused(*args, n_c, n_t, p, ops.workspace(forest.workspace_size(max(n, 1) * 2 + 4096), dev))
+    # the fused path (interleave + walk + assembly: the kernels the bench times) writes its own
+    # featurized table; every feature of every row must equal the oracle's, not only the proba
+    rows = ops.FeatureTable(max(n, 1) * 21 + 4096, dev)  # (a lone long customer pads its group of 21)
+    rows.buf.fill_(0xAB)
+    pipe.run_fused(*args, n_c, n_t, p, ops.workspace(forest.workspace_size(max(n, 1) * 2 + 4096), dev),
+                   rows_out=rows)
     np.testing.assert_array_equal(p.cpu().numpy(), p_ref)
     if n:
         np.testing.assert_array_equal(p_ref, oracle.forest_predict(X, arrays, z["mean"], z["scale"]))
+        Xt = table_as_X(rows, pipe.last_slots, d["amount"])
+        _check(d, Xt, n_c, n_t)
+        assert_same_features(Xt, X, "fused table vs featurize")
     Xs = FraudPipeline(forest=forest, avg_mode="scan").featurize(*args, n_c, n_t).X.cpu().numpy()
     np.testing.assert_array_equal(Xs[:, [0, 1, 2, 3, 5, 7, 9, 10, 11, 12, 13, 14]],
                                   X[:, [0, 1, 2, 3, 5, 7, 9, 10, 11, 12, 13, 14]])
@@ -86,6 +95,33 @@ def test_one_customer_one_terminal_long_segments(dev, golden):
          "amount": np.round(rng.uniform(1, 300, n), 2), "fraud": (rng.random(n) < 0.03).astype(np.uint8)}
     X = _run_all(dev, golden, d, 1, 1)
     _check(d, X, 1, 1)
+
+
+def test_walk_rings_overflow_at_chunk_boundaries(dev, golden):
+    """Customers whose 30-day windows hold more rows than the customer walk's LDS rings (128
+    rows in the short class, 256 in the long class, which takes groups whose longest customer
+    has >= 480 rows): lengths on both sides of 16-row chunk, ring and class boundaries, dense in
+    time so that every window is full, beside a crowd of short customers; then the fused path's
+    own featurized table row by row against the oracle (a ring overwrite that moves
+    no leaf must still fail a test)."""
+    rng = np.random.default_rng(21)
+    lens = [15, 16, 17, 127, 128, 129, 255, 256, 257, 300, 479, 480, 481, 700, 1500]
+    cust, ts = [], []
+    for c, m in enumerate(lens):  # m rows within 20 days: all inside the 30-day window
+        cust.append(np.full(m, c))
+        ts.append(rng.integers(40 * 86400, 60 * 86400, m))
+    n_small = 3000
+    cust.append(len(lens) + rng.integers(0, 400, n_small))
+    ts.append(rng.integers(0, 90 * 86400, n_small))
+    cust, ts = np.concatenate(cust), np.concatenate(ts)
+    o = np.argsort(ts, kind="stable")
+    n = len(o)
+    d = {"ts": (ts[o] * NS).astype(np.int64), "customer": cust[o].astype(np.int32),
+         "terminal": rng.integers(0, 50, n).astype(np.int32), "amount": np.round(rng.uniform(1, 300, n), 2),
+         "fraud": (rng.random(n) < 0.05).astype(np.uint8)}
+    d["ts"][500:530] = d["ts"][500]  # ties inside the busy windows
+    X = _run_all(dev, golden, d, len(lens) + 400, 50)
+    _check(d, X, len(lens) + 400, 50)
 
 
 def test_all_rows_same_timestamp(dev, golden):

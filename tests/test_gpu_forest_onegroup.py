@@ -19,7 +19,7 @@ from forest_gen import random_forest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = [1, 2, 3, 4]  # v1 (10 chains per lane), v2 (6), compact v2 (6), v2 (10)
+VARIANTS = [1, 2, 3, 4]  # v1 (10 chains per lane, interleaved pairs), v2 (6), compact v2 (6), v2 (10)
 
 
 def T(a, dt, dev):

@@ -1,8 +1,7 @@
 """A/B probe for the customer layout fill (k_interleave<true, true>): config-2 rows (50k
 customers, 183 days) -> payload re-key -> one-launch plan, then
 fdx_customer_layout_fill_starts_grouped timed alone (--reps); prints the time and a digest of
-the slots (its / iamt / irow) and the window starts so that builds of libfdx.so with different
-fill shapes (tools/build_ab.sh, tools/with_lib.py) can be compared bit for bit.
+the slots (its / iamt / irow) and the window starts so that two builds of libfdx.so (tools/with_lib.py) can be compared bit for bit.
 """
 import argparse
 import json

@@ -1,7 +1,7 @@
 """A/B probe for the customer-window walk: config-2 rows (50k customers, 183 days) -> payload
 re-key -> interleaved layout with window starts -> fdx_customer_windows_walk, timed alone
-(--reps); prints the time and a bit-level digest of the NB / SUM planes so that builds of
-libfdx.so with different walk shapes (tools/build_ab.sh, tools/with_lib.py) can be compared.
+(--reps); prints the time and a bit-level digest of the NB / SUM planes so that two builds of
+libfdx.so (tools/with_lib.py) can be compared.
 """
 import argparse
 import json
