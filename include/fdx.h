@@ -547,6 +547,21 @@ int fdx_segment_latest(const int64_t *ts_d, const int32_t *perm_d, const int64_t
                        int32_t *out_row_d, void *stream);
 int fdx_segment_first_in_range(const int64_t *ts_d, const int32_t *perm_d, const int64_t *seg_off_d,
                                int64_t n_seg, int64_t t_lo, int64_t t_hi, int32_t *out_row_d, void *stream);
+/* The same two snapshots straight from the featurized table the scoring path writes
+ * (fdx_forest_prepare_grouped_rows, FDX_ROWS_SLOT_ORDER: row_d = its FDX_FEATURE_COL(12) column,
+ * slot -> input row, -1 = padding), input rows in time order; ts_d / key_d by input row:
+ *   FDX_SELECT_LATEST:         out_slot_d[k] = the slot of the first input row holding key k's
+ *                              maximum ts (groupby(key).TX_DATETIME.idxmax(), :2914-2918)
+ *   FDX_SELECT_FIRST_IN_RANGE: out_slot_d[k] = the slot of key k's first input row with
+ *                              t_lo <= ts < t_hi (:3606-3635)
+ * -1 for a key without such a row; the feature columns of the chosen rows are read at those
+ * slots.  Workspace: fdx_table_select_workspace_size(n_keys). */
+#define FDX_SELECT_LATEST 0
+#define FDX_SELECT_FIRST_IN_RANGE 1
+size_t fdx_table_select_workspace_size(int64_t n_keys);
+int fdx_table_select(const int32_t *row_d, int64_t n_slots, const int64_t *ts_d, const int32_t *key_d,
+                     int64_t n_keys, int32_t mode, int64_t t_lo, int64_t t_hi, int32_t *out_slot_d, void *workspace_d,
+                     size_t workspace_bytes, void *stream);
 /* f-2 Debezium CDC records of a micro-batch (pyspark/scripts/kafka_s3_sink_transactions.py):
  *   fdx_cdc_decode: tx_amount bytes (record i = bytes_d[offsets_d[i] .. offsets_d[i+1]),
  *     big-endian two's complement, 1..8 bytes; :64-71) -> unscaled_d (int64 cents) and

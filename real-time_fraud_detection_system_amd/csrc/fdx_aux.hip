@@ -279,6 +279,54 @@ __global__ void __launch_bounds__(256) k_cpk_day_topk(const unsigned long long *
     }
 }
 
+// f-1 from the featurized table itself (FeatureTable, slot order: slot s holds input row row[s],
+// -1 for padding), without a grouping of the input: per key, atomics over the slots.
+//   LATEST: the max ts of the key (pass 1), then the smallest input row holding it (pass 2) --
+//           input rows are in time order (frame order), so this is groupby(key).idxmax()
+//   FIRST_IN_RANGE: the smallest input row with t_lo <= ts < t_hi (drop_duplicates keep='first')
+// best[k] = (row << 32) | slot, so the minimum carries the chosen row's slot.
+__global__ void __launch_bounds__(256) k_tsel_init(int64_t *__restrict__ best_ts, uint64_t *__restrict__ best,
+                                                   int64_t n_keys) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += (int64_t)gridDim.x * blockDim.x) {
+        best_ts[k] = INT64_MIN;
+        best[k] = UINT64_MAX;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tsel_max(const int32_t *__restrict__ row, int64_t n_slots,
+                                                  const int64_t *__restrict__ ts, const int32_t *__restrict__ key,
+                                                  int64_t n_keys, int64_t *__restrict__ best_ts) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = row[s];
+        if (r < 0) continue;
+        const int32_t k = key[r];
+        if ((uint32_t)k < (uint64_t)n_keys) atomicMax(reinterpret_cast<long long *>(best_ts + k), (long long)ts[r]);
+    }
+}
+
+template <bool LATEST>
+__global__ void __launch_bounds__(256) k_tsel_min(const int32_t *__restrict__ row, int64_t n_slots,
+                                                  const int64_t *__restrict__ ts, const int32_t *__restrict__ key,
+                                                  int64_t n_keys, int64_t t_lo, int64_t t_hi,
+                                                  const int64_t *__restrict__ best_ts, uint64_t *__restrict__ best) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = row[s];
+        if (r < 0) continue;
+        const int32_t k = key[r];
+        if ((uint32_t)k >= (uint64_t)n_keys) continue;
+        const int64_t t = ts[r];
+        if (LATEST ? t == best_ts[k] : (t >= t_lo && t < t_hi))
+            atomicMin(reinterpret_cast<unsigned long long *>(best + k),
+                      (unsigned long long)(((uint64_t)(uint32_t)r << 32) | (uint64_t)(uint32_t)s));
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tsel_out(const uint64_t *__restrict__ best, int64_t n_keys,
+                                                  int32_t *__restrict__ out_slot) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += (int64_t)gridDim.x * blockDim.x)
+        out_slot[k] = best[k] == UINT64_MAX ? -1 : (int32_t)(uint32_t)(best[k] & 0xFFFFFFFFu);
+}
+
 }  // namespace
 }  // namespace fdx
 
@@ -486,5 +534,44 @@ extern "C" int fdx_cdc_compact(const uint8_t *keep_d, int64_t n, const int64_t *
                        terminal_d, ts_ns_d, amount_d, fraud_d, customer_out_d, terminal_out_d, ts_out_d, amount_out_d,
                        fraud_out_d, row_out_d, count_d);
     FDX_LAUNCHED("k_cdc_compact");
+    return FDX_OK;
+}
+
+extern "C" size_t fdx_table_select_workspace_size(int64_t n_keys) {
+    return (size_t)(n_keys > 0 ? n_keys : 0) * 16 + 256;
+}
+
+extern "C" int fdx_table_select(const int32_t *row_d, int64_t n_slots, const int64_t *ts_d, const int32_t *key_d,
+                                int64_t n_keys, int32_t mode, int64_t t_lo, int64_t t_hi, int32_t *out_slot_d,
+                                void *ws, size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(n_slots >= 0 && n_keys >= 0 && n_keys <= INT32_MAX, "bad size");
+    FDX_REQUIRE(mode == FDX_SELECT_LATEST || mode == FDX_SELECT_FIRST_IN_RANGE, "mode must be FDX_SELECT_*");
+    if (n_keys == 0) return FDX_OK;
+    FDX_REQUIRE(out_slot_d && (n_slots == 0 || (row_d && ts_d && key_d)), "null pointer");
+    FDX_REQUIRE(n_slots <= INT32_MAX, "more than 2^31 slots");
+    if (!ws || ws_bytes < fdx_table_select_workspace_size(n_keys)) {
+        set_error("table select workspace too small: %zu < %zu", ws_bytes, fdx_table_select_workspace_size(n_keys));
+        return FDX_E_WORKSPACE;
+    }
+    int64_t *best_ts = reinterpret_cast<int64_t *>(ws);
+    uint64_t *best = reinterpret_cast<uint64_t *>(best_ts + n_keys);
+    hipStream_t st = as_stream(stream);
+    const unsigned gk = stream_grid(n_keys, 256), gs = stream_grid(std::max<int64_t>(n_slots, 1), 256);
+    hipLaunchKernelGGL(k_tsel_init, dim3(gk), dim3(256), 0, st, best_ts, best, n_keys);
+    FDX_LAUNCHED("k_tsel_init");
+    if (n_slots > 0) {
+        if (mode == FDX_SELECT_LATEST) {
+            hipLaunchKernelGGL(k_tsel_max, dim3(gs), dim3(256), 0, st, row_d, n_slots, ts_d, key_d, n_keys, best_ts);
+            FDX_LAUNCHED("k_tsel_max");
+            hipLaunchKernelGGL(k_tsel_min<true>, dim3(gs), dim3(256), 0, st, row_d, n_slots, ts_d, key_d, n_keys, t_lo,
+                               t_hi, best_ts, best);
+        } else {
+            hipLaunchKernelGGL(k_tsel_min<false>, dim3(gs), dim3(256), 0, st, row_d, n_slots, ts_d, key_d, n_keys, t_lo,
+                               t_hi, best_ts, best);
+        }
+        FDX_LAUNCHED("k_tsel_min");
+    }
+    hipLaunchKernelGGL(k_tsel_out, dim3(gk), dim3(256), 0, st, best, n_keys, out_slot_d);
+    FDX_LAUNCHED("k_tsel_out");
     return FDX_OK;
 }

@@ -19,6 +19,7 @@ FDX_FLAGS_SPARK = 1
 FDX_ROWS_INPUT_ORDER = 1  # fdx_forest_prepare_grouped_rows: the featurized table by input row
 FDX_ROWS_SLOT_ORDER = 2   # ... by scoring slot (coalesced; each record carries its row)
 FDX_KEY_MOD, FDX_KEY_DIV, FDX_KEY_SUB = 0, 1, 2
+FDX_SELECT_LATEST, FDX_SELECT_FIRST_IN_RANGE = 0, 1  # fdx_table_select
 MAX_WINDOWS = 8
 MAX_FEATURES = 32
 
@@ -79,6 +80,8 @@ SIGNATURES = {
                                                                 P]),
     "fdx_segment_latest": (ctypes.c_int, [P, P, P, c_i64, P, P]),
     "fdx_segment_first_in_range": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i64, P, P]),
+    "fdx_table_select_workspace_size": (c_sz, [c_i64]),
+    "fdx_table_select": (ctypes.c_int, [P, c_i64, P, P, c_i64, c_i32, c_i64, c_i64, P, P, c_sz, P]),
     "fdx_cdc_decode": (ctypes.c_int, [P, P, P, c_i64, P, P, P, P, P]),
     "fdx_dedup_latest_workspace_size": (c_sz, [c_i64]),
     "fdx_dedup_latest": (ctypes.c_int, [P, P, c_i64, P, P, P, c_sz, P]),

@@ -1,6 +1,8 @@
 """the batch -> streaming hand-off either side of the hot path.
 
-f-1 feature snapshots (the tables the Spark scoring job LEFT JOINs, fraud_detection.py:118-122):
+f-1 feature snapshots (the tables the Spark scoring job LEFT JOINs, fraud_detection.py:118-122),
+  from a frame (below) or straight from the featurized table the scoring step writes
+  (latest_terminal_features_from_table, customer_features_on_from_table: fdx_table_select):
   latest_terminal_features(df)     feature_transformation.ipynb:2914-2918
       df.loc[df.groupby('TERMINAL_ID').TX_DATETIME.idxmax()].filter(regex='TERMINAL_ID|TERMINAL_ID_RISK')
   customer_features_on(df, date)   :3461, :3606-3635, :4182
@@ -88,6 +90,70 @@ def dedup_latest(key: torch.Tensor, kafka_ts: torch.Tensor, bad: torch.Tensor | 
     if own and n and int(bad.item()):
         raise _lib.FdxUnsupported("tx_id -1 is reserved (the dedup table's empty key)")
     return keep
+
+
+def table_select(rows, n_slots: int, ts_ns: torch.Tensor, key: torch.Tensor, n_keys: int, mode: int,
+                 t_lo: int = 0, t_hi: int = 0, stream=None) -> torch.Tensor:
+    """Per key: the slot of the featurized table (ops.FeatureTable, slot order) holding the row
+    fdx_table_select picks (FDX_SELECT_LATEST / FDX_SELECT_FIRST_IN_RANGE), -1 if none.
+    ts_ns / key: by input row (time order)."""
+    if not isinstance(rows, ops.FeatureTable):
+        raise TypeError("table_select reads an ops.FeatureTable (slot order)")
+    ops._dev(ts_ns, torch.int64, "ts_ns"); ops._dev(key, torch.int32, "key")
+    out = torch.empty(max(int(n_keys), 0), dtype=torch.int32, device=ts_ns.device)
+    L = _lib.load()
+    ws = ops.workspace(L.fdx_table_select_workspace_size(int(n_keys)), ts_ns.device)
+    row = rows.columns(n_slots)["row"]
+    check(L.fdx_table_select(ops._ptr(row), int(n_slots), ops._ptr(ts_ns), ops._ptr(key), int(n_keys), int(mode),
+                             int(t_lo), int(t_hi), ops._ptr(out), ops._ptr(ws), ws.numel(), ops._s(stream)),
+          "fdx_table_select")
+    return out
+
+
+def _windows_label(w):
+    return f"{w}DAY_WINDOW"
+
+
+def latest_terminal_features_from_table(rows, n_slots: int, ts_ns: torch.Tensor, terminal: torch.Tensor,
+                                        n_terminals: int, windows_days=(1, 7, 30)) -> pd.DataFrame:
+    """feature_transformation.ipynb:2914-2918 on the table the scoring step wrote:
+    df.loc[df.groupby('TERMINAL_ID').TX_DATETIME.idxmax()].filter(regex='TERMINAL_ID|TERMINAL_ID_RISK')
+    -- index = the chosen input rows, rows in terminal order, the reference table's column
+    order and dtypes (counts as float64, as pandas' rolling count)."""
+    slots = table_select(rows, n_slots, ts_ns, terminal, n_terminals, _lib.FDX_SELECT_LATEST)
+    keep = slots >= 0
+    s = slots[keep].long()
+    col = rows.columns(n_slots)
+    r = col["row"][s].long()
+    out = {"TERMINAL_ID": terminal[r].cpu().numpy()}
+    nb, rk = col["term_nb"][:, s].cpu().numpy(), col["term_risk"][:, s].cpu().numpy()
+    for j, w in enumerate(windows_days):
+        out[f"TERMINAL_ID_NB_TX_{_windows_label(w)}"] = nb[j].astype(np.float64)
+        out[f"TERMINAL_ID_RISK_{_windows_label(w)}"] = rk[j]
+    return pd.DataFrame(out, index=pd.Index(r.cpu().numpy()))
+
+
+def customer_features_on_from_table(rows, n_slots: int, ts_ns: torch.Tensor, customer: torch.Tensor,
+                                    n_customers: int, date: datetime.date, windows_days=(1, 7, 30)) -> pd.DataFrame:
+    """feature_transformation.ipynb:3606-3635 on the table the scoring step wrote: each
+    customer's first transaction of `date` with its lower-cased customer columns and dt = date,
+    rows in frame (input) order, index = those input rows."""
+    lo = int(np.datetime64(date, "ns").astype(np.int64))
+    slots = table_select(rows, n_slots, ts_ns, customer, n_customers, _lib.FDX_SELECT_FIRST_IN_RANGE, lo,
+                         lo + NS_PER_DAY)
+    s = slots[slots >= 0].long()
+    col = rows.columns(n_slots)
+    r = col["row"][s].long()
+    o = torch.argsort(r)  # drop_duplicates keeps frame order
+    s, r = s[o], r[o]
+    out = {"customer_id": customer[r].cpu().numpy()}
+    nb, av = col["cust_nb"][:, s].cpu().numpy(), col["cust_avg"][:, s].cpu().numpy()
+    for j, w in enumerate(windows_days):
+        out[f"customer_id_nb_tx_{_windows_label(w).lower()}"] = nb[j].astype(np.float64)
+        out[f"customer_id_avg_amount_{_windows_label(w).lower()}"] = av[j]
+    f = pd.DataFrame(out, index=pd.Index(r.cpu().numpy()))
+    f["dt"] = date
+    return f
 
 
 # ------------------------------------------------------------------------------ pandas layer
