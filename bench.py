@@ -42,11 +42,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # row's feature rank), each 2 LDS-array cycles per wave64 instruction (MI355X_MICROARCH.md
 # §LDS table, ds_read_b32); one LDS-array cycle per clock per CU, 256 CUs at 2.4 GHz
 LDS_PEAK_STEPS = 256 * 2.4e9 / 4 * 64
-# ... and the MEASURED ceiling of that access pattern: random-address ds_read_b32 from a 64 KiB
-# LDS table, 1,024-thread block per CU, 32 independent reads in flight per lane, no
-# dependency: 1.561e11 wave-reads/s chip-wide (tools/lds_probe.hip, profiles/r02_lds_probe.txt;
-# conflict-free reads reach 2.9e11) -> node steps/s at 2 reads per step
-LDS_RANDOM_STEPS = 1.561e11 * 64 / 2
+# (round 4 also printed a "measured random-read ceiling" from tools/lds_probe.hip's wall-clock rate
+# of bank-conflicted reads; it is dropped: the walk's own counters -- the LDS array's busy share
+# and the waves' s_waitcnt share, from profiles/pmc_kernels.json -- say how close it runs)
 
 # SURVEY.md §8(d) algorithmic bytes per transaction (compact logical I/O, read once + write once)
 ALG = {"K2": 30, "K1-cust": 58, "K1-term": 49, "K3": 90, "end-to-end": 107}
@@ -98,6 +96,17 @@ def walk_steps_per_row(arrays):
                 d[rt[i]] = d[i] + 1
         total += int(d.max())
     return total
+
+
+def pmc_counters(name_part):
+    """The committed SQ counters of the first kernel whose name contains name_part, per
+    dispatch (profiles/pmc_kernels.json), or {}."""
+    p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        d = json.load(f)
+    return next((v for k, v in d["kernels"].items() if name_part in k), {})
 
 
 def pmc_table():
@@ -526,7 +535,8 @@ def main():
         "dtype": "f64",
         "setup_s": {"generate_on_gpu": round(t_gen, 2)},
         "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234+rank), "
-                "resident in HBM",
+                "resident in HBM" + ("; each rank draws its customers' rows from its own seed, so the configs[3] "
+                                     "union differs per N (its distributions do not)" if world > 1 else ""),
         "config": {"workload": (f"configs[1]: {n_cl} customers / {n_terms // world} terminals / {wl['days']} days "
                                 f"per GPU" if wl["name"] == "configs1" else
                                 f"configs[3]: {wl['n_customers_total']} customers / {n_terms} terminals / "
@@ -551,12 +561,22 @@ def main():
     out["roofline_lds"] = {"kernel": "k_forest_rank", "bound": "lds", "unit": "node steps/s",
                            "achieved": float(f"{ach_steps:.4g}"), "peak": float(f"{LDS_PEAK_STEPS:.4g}"),
                            "frac": round(ach_steps / LDS_PEAK_STEPS, 4), "node_steps_per_row_max": steps_max,
-                           "note": "2 ds_read per step at 2 LDS cycles each; steps = sum of tree depths (upper "
-                                   "bound: wave-wide early exit), so frac is an upper bound",
-                           "measured_random_read_peak": float(f"{LDS_RANDOM_STEPS:.4g}"),
-                           "frac_of_measured_random_read_peak": round(ach_steps / LDS_RANDOM_STEPS, 4),
-                           "measured_peak_source": "tools/lds_probe.hip (profiles/r02_lds_probe.txt): random "
-                                                   "ds_read_b32, 32 independent reads in flight per lane"}
+                           "note": "peak = the LDS array's conflict-free rate: 2 ds_read_b32 per step at 2 LDS "
+                                   "cycles each (MI355X_MICROARCH.md §LDS); steps = sum of tree depths (upper "
+                                   "bound: wave-wide early exit), so frac is an upper bound"}
+    sq = pmc_counters("k_forest_rank")
+    if sq.get("SQ_LDS_IDX_ACTIVE") and sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_WAVE_CYCLES"):
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles: per-CU cycles = it / 8; SQ_LDS_IDX_ACTIVE
+        # sums every CU's LDS-array cycles; the SQ_WAIT / WAVE counters share one unit
+        cu_cycles = sq["GRBM_GUI_ACTIVE"] / 8
+        out["roofline_lds"]["pmc"] = {
+            "lds_array_busy_share": round(sq["SQ_LDS_IDX_ACTIVE"] / 256 / cu_cycles, 3),
+            "lds_bank_conflict_share": round(sq.get("SQ_LDS_BANK_CONFLICT", 0) / sq["SQ_LDS_IDX_ACTIVE"], 3),
+            "wave_waitcnt_share": round(sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"], 3),
+            "wave_issue_stall_share": round(sq.get("SQ_WAIT_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"], 3),
+            "valu_busy_share": round(sq.get("SQ_INSTS_VALU", 0) / 1024 * 2 / cu_cycles, 3),
+            "source": "profiles/pmc_kernels.json (per dispatch; VALU at 2 cycles per wave64 instruction "
+                      "on SIMD-32, 1,024 SIMDs)"}
     if marks_all:
         ms_of = lambda steps: {name: [mk[name][0].elapsed_time(mk[name][1]) for mk in steps]  # noqa: E731
                                for name in steps[0] if not name.startswith("_")}
@@ -600,8 +620,10 @@ def main():
                           "end_to_end": {"alg_bytes_per_tx": e2e_b, "achieved_GBs": round(e2e, 1),
                                          "time": "ms_per_step", "features_emitted": args.emit_features,
                                          "bytes": f"raw columns in {E2E_IN} + proba out {E2E_PROBA}"
-                                                  + (f" + feature columns out {E2E_FEATURES} (by "
-                                                     f"{args.emit_features}, with the row index)" if emit
+                                                  + (f" + feature columns out {E2E_FEATURES} (the 14 "
+                                                     f"columns in §8(d)'s compact logical form; the table as "
+                                                     f"written by {args.emit_features} adds the row index and "
+                                                     f"padding: 78 B per slot / 80 B per record)" if emit
                                                      else " (featurized table not written: --emit-features none)")
                                                   + f"; SURVEY.md §8(d)'s fused ideal is {ALG['end-to-end']}",
                                          "frac": round(e2e / HBM_PEAK_GBS, 4)},

@@ -235,3 +235,46 @@ def test_featurized_table_without_search_trees(dev, config1, order):
             Xt[:, 3 + 2 * w], Xt[:, 4 + 2 * w] = col["cust_nb"][w], col["cust_avg"][w]
             Xt[:, 9 + 2 * w], Xt[:, 10 + 2 * w] = col["term_nb"][w], col["term_risk"][w]
     assert_same_features(Xt, Xo, f"table ({order} order) without S-trees vs oracle")
+
+
+def test_serving_snapshots_from_the_step_table(dev, config1):
+    """the featurized table the scoring step writes has a consumer.  The serving
+    snapshots built straight from run_fused's FeatureTable (fdx_table_select) equal the
+    reference's pandas expressions on the featurized frame (the oracle's features, the
+    notebook's column order, time order):
+      latest per terminal  feature_transformation.ipynb:2914-2918
+      customers of a date  :3606-3635 (lower-case, filter, date rows, dt, drop_duplicates)"""
+    import datetime
+
+    from fdx import serving
+
+    g, d, Xo = config1
+    arrays, mean, scale = _load("rf100_d20")
+    pipe = FraudPipeline(forest=ops.Forest(arrays, 15, mean, scale))
+    n = len(d["ts"])
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 5_000, 10_000)
+    rows = ops.FeatureTable(n * 11 // 10, dev)
+    p = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, p, rows_out=rows)
+    m = pipe.last_slots
+    # the reference's featurized frame (time order, the notebook's columns)
+    df = pd.DataFrame({"TRANSACTION_ID": np.arange(n), "TX_DATETIME": d["ts"].astype("datetime64[ns]"),
+                       "CUSTOMER_ID": d["customer"], "TERMINAL_ID": d["terminal"], "TX_AMOUNT": d["amount"],
+                       "TX_FRAUD": d["fraud"]})
+    for j, c in enumerate(FEATS[1:], start=1):
+        df[c] = Xo[:, j]
+    df["TX_DURING_WEEKEND"] = df["TX_DURING_WEEKEND"].astype(np.int64)
+    df["TX_DURING_NIGHT"] = df["TX_DURING_NIGHT"].astype(np.int64)
+    want = df.loc[df.groupby("TERMINAL_ID").TX_DATETIME.idxmax()].filter(regex="TERMINAL_ID|TERMINAL_ID_RISK")
+    got = serving.latest_terminal_features_from_table(rows, m, g["ts"], g["terminal"], 10_000)
+    pd.testing.assert_frame_equal(got, want, check_dtype=False, check_exact=True, check_index_type=False)
+    for day in (datetime.date(2024, 6, 2), datetime.date(2024, 8, 15), datetime.date(2024, 11, 29)):
+        low = df.copy()
+        low.columns = map(str.lower, low.columns)
+        low = low.filter(regex="customer_id|tx_datetime")
+        low = low[low.tx_datetime.dt.date == day].copy()
+        low["dt"] = day
+        want_c = low.drop(columns=["tx_datetime"]).drop_duplicates(subset=["customer_id"])
+        got_c = serving.customer_features_on_from_table(rows, m, g["ts"], g["customer"], 5_000, day)
+        assert len(got_c) > 100, day
+        pd.testing.assert_frame_equal(got_c, want_c, check_dtype=False, check_exact=True, check_index_type=False)
