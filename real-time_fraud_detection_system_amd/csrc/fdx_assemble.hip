@@ -120,14 +120,6 @@ __device__ __forceinline__ void rank_fixed(const float (&v)[16], const int (&fs)
     }
 }
 
-// ranks of the features in `need` by a full lower_bound over U_f in global memory (the rare
-// fallback of k_zfill_grouped_w3: values outside its integer / ratio rank tables)
-__device__ __forceinline__ void rank_row_global(const float (&v)[16], const RankTab &rt, uint32_t (&out)[16],
-                                             uint32_t need) {
-#pragma unroll
-    for (int f = 0; f < 16; ++f)
-        if ((need >> f) & 1u) out[f] = rank_of(v[f], rt.u + rt.off[f], rt.cnt[f]);
-}
 
 // every thread of the block: stage the sample table into LDS (prepare kernels, RANK mode)
 __device__ __forceinline__ void stage_samples(float *s_smp, const RankTab &rt) {
@@ -506,6 +498,13 @@ __global__ void __launch_bounds__(256) k_zfill_grouped(
 // arithmetic, same fallbacks).
 constexpr int kW3Block = 1024;
 
+// [a < x] as the sign bit of a - x: the S-tree / segment keys are finite or +inf and never -0.0
+// (build_search_trees and the segment table store +0.0 for -0.0: the same comparisons), f32
+// denormals are kept (a - x == 0 only for a == x), and a NaN x is routed by the caller (rank
+// 0xFFFF) -- so this is exactly the IEEE compare, without a v_cmp -> v_cndmask pair per key
+// (each pair took an s_nop for the VCC hazard: 8 per S-tree level, r05 ISA)
+__device__ __forceinline__ uint32_t lt_bit(float a, float x) { return __float_as_uint(a - x) >> 31; }
+
 struct PrepRow {
     int64_t t;
     double a;
@@ -560,6 +559,18 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
     static_assert(sizeof(fdx_feature_row) == 80, "5 x 16-byte stores per feature record");
     __shared__ __align__(16) float s_t[kW3TreeFloats];  // the S-trees (RankTab::etab)
     __shared__ uint16_t s_itab[16 * kIntTab];
+    // the scaler in LDS (identity where absent: x - 0.0 and x / 1.0 are exact): as kernel-argument
+    // scalars its 30 doubles stayed live in SGPRs across the row loop, which spilled 129 SGPRs
+    // into VGPR lanes (a v_readlane per use in the loop; r05 ISA)
+    __shared__ double s_ms[32];
+    __shared__ int32_t s_oc[32];  // rt.off / rt.cnt of the 16 slots: the rare full-search fallback
+    if (threadIdx.x < 16) {
+        s_ms[threadIdx.x] = mean && (int)threadIdx.x < nf ? mean[threadIdx.x] : 0.0;
+        s_ms[16 + threadIdx.x] = scale && (int)threadIdx.x < nf ? scale[threadIdx.x] : 1.0;
+        s_oc[threadIdx.x] = rt.off[threadIdx.x];
+        s_oc[16 + threadIdx.x] = rt.cnt[threadIdx.x];
+    }
+    auto zs = [&](double x, int f) -> float { return (float)((x - s_ms[f]) / s_ms[16 + f]); };
     for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
     for (int e = threadIdx.x; e < rt.n_etab / 4; e += blockDim.x)
         reinterpret_cast<float4 *>(s_t)[e] = reinterpret_cast<const float4 *>(rt.etab)[e];
@@ -640,13 +651,13 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             if (c >= 0 && c < kIntTab) {
                 q[f] = s_itab[f * kIntTab + c];
             } else {
-                v[f] = zval((double)c, mean, scale, f);
+                v[f] = zs((double)c, f);
                 need |= 1u << f;
             }
         };
         q[1] = s_itab[1 * kIntTab + (we ? 1 : 0)];
         q[2] = s_itab[2 * kIntTab + (ni ? 1 : 0)];
-        v[0] = zval(cur.a, mean, scale, 0);
+        v[0] = zs(cur.a, 0);
         bool nan = v[0] != v[0];
         auto fst = [](auto *p, auto v) {  // feature-table store: nontemporal, the step never reads it
             __builtin_nontemporal_store(v, p);
@@ -696,7 +707,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
         for (int w = 0; w < W; ++w) {
             const int32_t c = cur.c[w];
             count(3 + 2 * w, c);
-            v[4 + 2 * w] = zval((val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w], mean, scale, 4 + 2 * w);
+            v[4 + 2 * w] = zs((val_is_sum & 1) ? cur.cv[w] / (double)c : cur.cv[w], 4 + 2 * w);
             nan |= v[4 + 2 * w] != v[4 + 2 * w];
             const int64_t tw = cur.tw[w];
             const int32_t tnb = term_nb(tw), tfr = (int32_t)((uint64_t)tw >> 32);
@@ -716,8 +727,8 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
                     const float4 *nd = reinterpret_cast<const float4 *>(s_t) + 2 * (rt.eoff[s] + ek[s]);
                     const float4 a = nd[0], b = nd[1];
                     const float x = v[kW3Search[s]];
-                    const int32_t c = (int32_t)(a.x < x) + (int32_t)(a.y < x) + (int32_t)(a.z < x) + (int32_t)(a.w < x) +
-                                      (int32_t)(b.x < x) + (int32_t)(b.y < x) + (int32_t)(b.z < x) + (int32_t)(b.w < x);
+                    const int32_t c = (int32_t)(lt_bit(a.x, x) + lt_bit(a.y, x) + lt_bit(a.z, x) + lt_bit(a.w, x) +
+                                                lt_bit(b.x, x) + lt_bit(b.y, x) + lt_bit(b.z, x) + lt_bit(b.w, x));
                     cs[s] = cs[s] * 9 + c;
                     ek[s] = ek[s] * 9 + 1 + c;
                 }
@@ -736,7 +747,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const float x = v[kW3Search[s]];
-                kc[s] = (uint32_t)(sg[s].x < x) + (uint32_t)(sg[s].y < x) + (uint32_t)(sg[s].z < x) + (uint32_t)(sg[s].w < x);
+                kc[s] = lt_bit(sg[s].x, x) + lt_bit(sg[s].y, x) + lt_bit(sg[s].z, x) + lt_bit(sg[s].w, x);
             }
         }
 #pragma unroll
@@ -751,14 +762,18 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             if (rat_ok[w]) {
                 q[fr_] = rq[w];
             } else {
-                v[fr_] = zval(term_risk(cur.tw[w]), mean, scale, fr_);
+                v[fr_] = zs(term_risk(cur.tw[w]), fr_);
                 need |= 1u << fr_;
                 nan |= v[fr_] != v[fr_];
             }
         }
         if (live && nan) *nan_flag = 1;
         need &= (1u << nf) - 1u;
-        if (live && need) rank_row_global(v, rt, q, need);  // table overflows (rare): full lower_bound in HBM
+        if (live && need) {  // table overflows (rare): a full lower_bound over U_f in HBM
+#pragma unroll
+            for (int f = 0; f < 16; ++f)
+                if ((need >> f) & 1u) q[f] = rank_of(v[f], rt.u + s_oc[f], s_oc[16 + f]);
+        }
         q[15] = 0u;
         if (i < n) {  // padding slot of the interleaved layout: the zero row
             uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + i * 16);

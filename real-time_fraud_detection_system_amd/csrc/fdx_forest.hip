@@ -1011,7 +1011,8 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
         F->ruoff[f] = (int32_t)useg.size();
         F->rsoff[f] = (int32_t)smp.size();
         F->rscnt[f] = ns;
-        for (int32_t j = 0; j < ns * seg; ++j) useg.push_back(j < c ? RL.thr[(size_t)(RL.thr_off[f] + j)] : INFINITY);
+        for (int32_t j = 0; j < ns * seg; ++j)  // (+ 0.0f: -0.0 as +0.0, see lt_bit in fdx_assemble.hip)
+            useg.push_back(j < c ? RL.thr[(size_t)(RL.thr_off[f] + j)] + 0.0f : INFINITY);
         for (int32_t j = 0; j < ns; ++j) smp.push_back(RL.thr[(size_t)(RL.thr_off[f] + j * seg)]);
     }
     F->rnsmp = (int32_t)smp.size();

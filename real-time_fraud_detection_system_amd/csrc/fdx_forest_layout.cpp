@@ -310,7 +310,8 @@ void fdx::build_search_trees(const RankLayout &L, std::vector<float> &trees, int
             if (k >= nn) return;
             for (int j = 0; j < 8; ++j) {
                 fill(9 * k + 1 + j);
-                t[(size_t)(8 * k + j)] = i < ns ? thr[(size_t)i * kW3Gap] : INFINITY;
+                // (-0.0 stored as +0.0: the same comparisons, and the kernel's sign-bit compare needs it)
+                t[(size_t)(8 * k + j)] = i < ns ? thr[(size_t)i * kW3Gap] + 0.0f : INFINITY;
                 ++i;
             }
             fill(9 * k + 9);
