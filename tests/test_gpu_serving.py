@@ -101,3 +101,54 @@ def test_cdc_decode_and_dedup_random_batch(dev):
     np.testing.assert_array_equal(out.tx_amount_cents.values, cents[idx])
     secs = np.array([int(us[i] / 1_000_000) for i in idx], np.int64)   # from_unixtime(us / 1e6)
     np.testing.assert_array_equal(out.tx_datetime.values.astype(np.int64), secs * 1_000_000_000)
+
+
+@pytest.mark.parametrize("n_slots_extra", [0, 700])
+def test_table_select_edges(dev, n_slots_extra):
+    """fdx_table_select on a hand-made slot table against numpy: tied timestamps (the first
+    input row of the tied maxima, as idxmax), keys without rows (-1), padding slots (row -1),
+    rows whose key is out of range (ignored), a time range that holds no row, and an empty
+    table."""
+    import torch
+
+    from fdx import _lib, ops
+
+    rng = np.random.default_rng(11)
+    n, n_keys = 5000, 300
+    ts = np.sort(rng.integers(0, 40, n)) * 3_600_000_000_000  # hour-floored: many ties
+    key = rng.integers(0, n_keys - 10, n).astype(np.int32)   # keys 290..299 never occur
+    key[rng.choice(n, 25, replace=False)] = -1                 # out of range: ignored
+    key[rng.choice(n, 25, replace=False)] = n_keys + 7
+    rows = np.concatenate([rng.permutation(n), -np.ones(n_slots_extra, np.int64)])
+    rows = rows[rng.permutation(len(rows))].astype(np.int32)
+    m = len(rows)
+    tab = ops.FeatureTable(m, dev)
+    tab.columns(m)["row"].copy_(torch.from_numpy(rows))
+    ts_d = torch.from_numpy(ts).to(dev)
+    key_d = torch.from_numpy(key).to(dev)
+    slot_of_row = np.empty(n, np.int64)
+    live = rows >= 0
+    slot_of_row[rows[live]] = np.nonzero(live)[0]
+
+    def want(pick):
+        out = -np.ones(n_keys, np.int32)
+        for k in range(n_keys):
+            r = pick(np.nonzero(key == k)[0])
+            if r is not None:
+                out[k] = slot_of_row[r]
+        return out
+
+    def latest(rs):
+        return None if len(rs) == 0 else rs[np.argmax(ts[rs])]  # first of the tied maxima
+
+    got = serving.table_select(tab, m, ts_d, key_d, n_keys, _lib.FDX_SELECT_LATEST).cpu().numpy()
+    np.testing.assert_array_equal(got, want(latest))
+    for lo, hi in ((5 * 3_600_000_000_000, 9 * 3_600_000_000_000), (10**18, 10**18 + 5), (0, 1)):
+        def first(rs, lo=lo, hi=hi):
+            rs = rs[(ts[rs] >= lo) & (ts[rs] < hi)]
+            return None if len(rs) == 0 else rs.min()
+
+        got = serving.table_select(tab, m, ts_d, key_d, n_keys, _lib.FDX_SELECT_FIRST_IN_RANGE, lo, hi).cpu().numpy()
+        np.testing.assert_array_equal(got, want(first), err_msg=f"[{lo}, {hi})")
+    empty = serving.table_select(tab, 0, ts_d, key_d, n_keys, _lib.FDX_SELECT_LATEST).cpu().numpy()
+    np.testing.assert_array_equal(empty, -np.ones(n_keys, np.int32))
