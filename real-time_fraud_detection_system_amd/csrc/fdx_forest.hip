@@ -355,12 +355,37 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
             __builtin_amdgcn_sched_barrier(0);
         }
     };
+    // The walk's last possible step (d = depth - 1) moves every chain to its leaf and reads
+    // nothing: the node and rank reads a step issues serve the NEXT step, and after the last one
+    // only the leaf ADDRESS is used (leaf values / ids are indexed by it).  The bench rows walk
+    // ~19.8 of 20 steps per tree, so this drops 2 of ~40 LDS reads per tree.
+    auto last_step = [&]() {
+        if constexpr (PW >= 100) {
+#pragma unroll
+            for (int g = 0; g < K; g += 2) {
+                if (g + 1 < K)
+                    il_node2(pa[g], pa[g + 1], x[g], x[g + 1], nd[g], nd[g + 1]);
+                else
+                    il_node1(pa[g], x[g], nd[g]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t d = P16 ? (int32_t)((x[k] << (P16 == 3 ? sh : 16u)) + nd[k]) : (int32_t)(x[k] - nd[k]);
+                uint32_t st, pn;
+                asm("v_med3_i32 %1, %2, 1, %3\n\tv_lshl_add_u32 %0, %1, 2, %4"
+                    : "=v"(pn), "=&v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>), "v"(pa[k]));
+                pa[k] = pn;
+            }
+        }
+    };
     int d = 0;
-    for (; d + kExitEvery <= pre; d += kExitEvery) {  // whole unrolled intervals, no test
+    // whole unrolled intervals, no test (pre <= depth - kExitEvery: never the last step)
+    for (; d + kExitEvery <= pre; d += kExitEvery) {
 #pragma unroll
         for (int e = 0; e < kExitEvery; ++e) step();
     }
-    for (; d + kExitEvery <= depth; d += kExitEvery) {
+    for (; d + kExitEvery < depth; d += kExitEvery) {
 #pragma unroll
         for (int e = 0; e < kExitEvery; ++e) step();
         uint32_t moving = 0;
@@ -368,8 +393,16 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
         for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
         if (!__any(moving != 0)) return d + kExitEvery;
     }
-    for (; d < depth; ++d) step();
-    return d;
+    if (d < depth) {  // 1 .. kExitEvery steps left, the last without reads
+        if (d + kExitEvery == depth) {
+#pragma unroll
+            for (int e = 0; e < kExitEvery - 1; ++e) step();
+        } else {
+            for (; d < depth - 1; ++d) step();
+        }
+        last_step();
+    }
+    return depth;
 }
 
 template <int R, int GG, int P16, int PIPE>
