@@ -392,13 +392,8 @@ int fdx_forest_pack_rank(const fdx_forest_desc *desc, uint32_t *nodes_out, int32
  * reference's deployed RandomForestClassifier(random_state=0), model_training.ipynb:2212): 32
  * u16 threshold-rank SLOTS, feature f spanning ceil(|U_f| / 32767) consecutive slots; slot s
  * holds min(max(r_f - slot_base[s], 0), 32767).  Node (4 B): [30:16] k' | [15:11] slot |
- * [10:0] right offset; leaf 0x7FFF0000; jump 0xFFFF0000 | offset.  version = 1, 2 or 3 (1 = the
- * fdx_forest_pack_rank layout; thr_off_out then has 17 meaningful entries of 33, slot tables 0;
- * 3 = the v1 node words in two-level packets of 4 words -- P | L | R | X, one packet per internal
- * node at an even depth, leaves implicit: the leaf reached from packet p by P's decision a and
- * its child's decision b (0 = left) has index 4p + 2a + b in orig_out / leaf_value_out;
- * missing_left_out of P / L / R at 4p + 0 / 1 / 2; depth_out = two-level steps; the word
- * format is described at build_rank_layout, csrc/fdx_forest_layout.cpp).
+ * [10:0] right offset; leaf 0x7FFF0000; jump 0xFFFF0000 | offset.  version = 1 or 2 (1 = the
+ * fdx_forest_pack_rank layout; thr_off_out then has 17 meaningful entries of 33, slot tables 0).
  * fdx_forest_create picks v1 when the forest fits it, else v2 when <= 16 features need <= 32
  * slots, else the wide 8-byte layout.  v2 forests score through fdx_forest_predict /
  * prepare + traverse (the fused scoring-pipeline prepares need v1). */

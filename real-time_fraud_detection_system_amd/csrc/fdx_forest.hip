@@ -307,7 +307,7 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
     auto step = [&]() {
         if constexpr (PW >= 100) {
-            static_assert(PW == 102 && P16 == 0, "interleaved pairs: u32 planes");
+            static_assert((PW == 102 || PW == 103) && P16 == 0, "interleaved pairs: u32 planes");
 #pragma unroll
             for (int g = 0; g < K; g += 2) {
                 if (g + 1 < K) {
@@ -322,8 +322,10 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
             }
 #pragma unroll
             for (int g = 0; g < K; g += 2) {
-                const uint32_t a0 = (nd[g] & kSlotMask<P16>) | lane_base[g];
-                const uint32_t a1 = g + 1 < K ? (nd[g + 1] & kSlotMask<P16>) | lane_base[g + 1] : 0u;
+                // PW 103 (STUDY, wrong results): the rank address from the node's ADDRESS, so the
+                // rank read does not wait for the node read -- one LDS round trip per step
+                const uint32_t a0 = ((PW == 103 ? pa[g] << 10 : nd[g]) & kSlotMask<P16>) | lane_base[g];
+                const uint32_t a1 = g + 1 < K ? ((PW == 103 ? pa[g + 1] << 10 : nd[g + 1]) & kSlotMask<P16>) | lane_base[g + 1] : 0u;
                 x[g] = rank_x<P16>(lds, a0);
                 if (g + 1 < K) x[g + 1] = rank_x<P16>(lds, a1);
                 __builtin_amdgcn_sched_barrier(0);
@@ -403,144 +405,6 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
     return depth;
 }
 
-// ---- rank layout v1 in two-level packets (variant 5; layout: build_rank_layout fmt 3 in
-// fdx_forest_layout.cpp).  A step decides two levels from one 16-byte packet P | L | R | X:
-//   a = x_P - P < 0 (left)            c = a ? L : R          LG = a ? P : X
-//   b = x_c - c < 0 (left)            offset = (b ? LG : c) & 0x7FF packets (0: at the leaf)
-// 3 LDS reads (ds_read_b128 packet, P's rank, c's rank) and 11 VALU per two levels, against
-// 4 reads and 10 VALU for two v1 steps; leaves are not stored, so the words per tree drop too.
-// After the last step the chain's "address" is the leaf slot 4p + 2a + b (byte address of
-// packet p + 8a + 4b), which rank_leaf_values / rank_leaf_ids index like a v1 leaf.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 lds128(const char *lds, uint32_t byte_addr) {
-    return *reinterpret_cast<const u32x4 *>(lds + byte_addr);  // 16-byte aligned: ds_read_b128
-}
-// P's decision and the choice of c / LG, then c's rank address (5 VALU; the sign of x_P - P as
-// a mask: bfi selects without a lane mask):  d = x_P - P, m = d >> 31, c = bfi(m, L, R),
-// lg = bfi(m, P, X), addr = (c & 0xF000) | lane_base
-__device__ __forceinline__ void pk_decide_a(uint32_t &c, uint32_t &lg, uint32_t &addr, uint32_t &m, uint32_t P,
-                                            uint32_t Lw, uint32_t Rw, uint32_t X, uint32_t xP, uint32_t lb) {
-    asm("v_sub_u32 %[m], %[xP], %[P]\n\t"
-        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
-        "v_bfi_b32 %[c], %[m], %[L], %[R]\n\t"
-        "v_bfi_b32 %[lg], %[m], %[P], %[X]\n\t"
-        "v_and_or_b32 %[a], %[c], %[fm], %[lb]"
-        : [c] "=&v"(c), [lg] "=&v"(lg), [a] "=&v"(addr), [m] "=&v"(m)
-        : [P] "v"(P), [L] "v"(Lw), [R] "v"(Rw), [X] "v"(X), [xP] "v"(xP), [lb] "v"(lb), [fm] "s"(0xF000u));
-}
-// c's decision and the move (5 VALU): m = (x_c - c) >> 31, off = bfi(m, lg, c) & 0x7FF, pa += 16 off
-__device__ __forceinline__ void pk_decide_b(uint32_t &pa, uint32_t &off, uint32_t &m, uint32_t c, uint32_t lg,
-                                            uint32_t xc) {
-    asm("v_sub_u32 %[m], %[xc], %[c]\n\t"
-        "v_ashrrev_i32 %[m], 31, %[m]\n\t"
-        "v_bfi_b32 %[o], %[m], %[lg], %[c]\n\t"
-        "v_and_b32 %[o], 0x7ff, %[o]\n\t"
-        "v_lshl_add_u32 %[pa], %[o], 4, %[pa]"
-        : [pa] "+v"(pa), [o] "=&v"(off), [m] "=&v"(m)
-        : [c] "v"(c), [lg] "v"(lg), [xc] "v"(xc));
-}
-template <int K>
-__device__ __forceinline__ int rank_walk_packets(const char *lds, const uint32_t (&lb)[K], uint32_t (&pa)[K],
-                                                 int depth, int pre) {
-    u32x4 pk[K];
-    uint32_t xP[K], c[K], lg[K], xc[K], off[K], mA[K], mB[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) pk[k] = lds128(lds, pa[k]);
-#pragma unroll
-    for (int k = 0; k < K; ++k) xP[k] = lds32(lds, (pk[k].x & 0xF000u) | lb[k]);
-    // three phases per step, each one chain after another with its LDS read issued right away,
-    // so every read has the other chains' work of two phases to arrive
-    auto phase_a = [&]() {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            uint32_t addr;
-            pk_decide_a(c[k], lg[k], addr, mA[k], pk[k].x, pk[k].y, pk[k].z, pk[k].w, xP[k], lb[k]);
-            xc[k] = lds32(lds, addr);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    auto phase_b = [&](bool fetch) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            uint32_t p = pa[k];
-            pk_decide_b(p, off[k], mB[k], c[k], lg[k], xc[k]);
-            if (fetch) {
-                pa[k] = p;
-                pk[k] = lds128(lds, p);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    auto phase_c = [&]() {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            xP[k] = lds32(lds, (pk[k].x & 0xF000u) | lb[k]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    auto step = [&]() {
-        phase_a();
-        phase_b(true);
-        phase_c();
-    };
-    // the last step reads no next packet: the chain is at its leaf, which the two decisions name
-    // (masks -1 = left): slot 2a + b, i.e. pa += 12 + 8 mA + 4 mB
-    auto finish = [&]() {
-        phase_a();
-        phase_b(false);
-#pragma unroll
-        for (int k = 0; k < K; ++k) pa[k] += 12u + (mA[k] << 3) + (mB[k] << 2);
-    };
-    int d = 0;
-    for (; d + kExitEvery <= pre; d += kExitEvery) {  // (pre <= depth - kExitEvery)
-#pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) step();
-    }
-    for (; d + kExitEvery < depth; d += kExitEvery) {
-#pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) step();
-        uint32_t moving = 0;  // offset 0 = every chain stayed: all at leaves (the step re-read the same packet)
-#pragma unroll
-        for (int k = 0; k < K; ++k) moving |= off[k];
-        if (!__any(moving != 0)) {
-            finish();
-            return d + kExitEvery;
-        }
-    }
-    if (d < depth) {  // (depth >= 1: the layout gives a single-leaf tree one step)
-        if (d + kExitEvery == depth) {
-#pragma unroll
-            for (int e = 0; e < kExitEvery - 1; ++e) step();
-        } else {
-            for (; d < depth - 1; ++d) step();
-        }
-        finish();
-    }
-    return depth;
-}
-// NaN-aware form (a batch with NaN features; ranks of NaN are 0xFFFFFFFF): a NaN decides by
-// missing_go_to_left of P / L / R, kept at 4p + 0 / 1 / 2 of ml (the chunk's slice)
-template <int K>
-__device__ __forceinline__ void rank_walk_packets_nan(const char *lds, const uint32_t (&lb)[K], uint32_t (&pa)[K],
-                                                      int depth, const uint8_t *__restrict__ ml) {
-    for (int d = 0; d < depth; ++d) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const u32x4 q = lds128(lds, pa[k]);
-            const uint32_t x = lds32(lds, (q.x & 0xF000u) | lb[k]);
-            const uint32_t i = (pa[k] - kRankNodeB) >> 2;
-            const bool a = x == 0xFFFFFFFFu ? ml[i] != 0 : (int32_t)(x - q.x) < 0;
-            const uint32_t c = a ? q.y : q.z, lg = a ? q.x : q.w;
-            const uint32_t y = lds32(lds, (c & 0xF000u) | lb[k]);
-            const bool b = y == 0xFFFFFFFFu ? ml[i + (a ? 1 : 2)] != 0 : (int32_t)(y - c) < 0;
-            if (d + 1 < depth)
-                pa[k] += ((b ? lg : c) & 0x7FFu) << 4;
-            else
-                pa[k] += (a ? 0u : 8u) + (b ? 0u : 4u);
-        }
-    }
-}
-
 template <int R, int GG, int P16, int PIPE>
 __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lrow)[R], int t,
                                            const int32_t *__restrict__ root, const int32_t *__restrict__ depth,
@@ -552,7 +416,7 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
 #pragma unroll
     for (int g = 0; g < GG; ++g) {
         const uint32_t p0 = kNodeB<P16> + (uint32_t)(root[t + g] - node_base) * 4u;
-        const uint32_t n0 = PIPE == 202 ? 0u : lds32(lds, p0);
+        const uint32_t n0 = lds32(lds, p0);
         dmax = max(dmax, depth[t + g]);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -561,16 +425,10 @@ __device__ __forceinline__ void rank_trees(const char *lds, const uint32_t (&lro
             lane_base[r * GG + g] = lrow[r];
         }
     }
-    if constexpr (PIPE == 202) {
-        if (any_nan)
-            rank_walk_packets_nan<K>(lds, lane_base, pa, dmax, ml);
-        else
-            rank_walk_packets<K>(lds, lane_base, pa, dmax, 0);
-    } else if (any_nan) {
+    if (any_nan)
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
-    } else {
+    else
         rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax);
-    }
 }
 
 // rank_trees with the roots read once per launch (rp = root byte addresses, rn = root nodes,
@@ -589,19 +447,11 @@ __device__ __forceinline__ int rank_trees_from(const char *lds, const uint32_t (
             nd[r * GG + g] = rn[g];
             lane_base[r * GG + g] = lrow[r];
         }
-    if constexpr (PIPE == 202) {
-        if (any_nan) {
-            rank_walk_packets_nan<K>(lds, lane_base, pa, dmax, ml);
-            return 0;
-        }
-        return rank_walk_packets<K>(lds, lane_base, pa, dmax, pre);
-    } else {
-        if (any_nan) {
-            rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
-            return 0;
-        }
-        return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, pre);
+    if (any_nan) {
+        rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
+        return 0;
     }
+    return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, pre);
 }
 
 template <int K>
@@ -943,9 +793,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     }
     // the generic tile loop (leaf ids, per-tree values, chunks of more trees than one group):
     // two rows per lane walk groups of 3 trees (6 chains) to stay within the register budget
-    // (packets: the group pipeline holds a group's leaf values while the next group walks, and a
-    // packet chain keeps ~6 VGPRs against v1's 3: groups of 4 keep it within 128 VGPRs)
-    constexpr int GG = R == 2 ? 3 : (PIPE == 202 && G > 4 ? 4 : G);
+    constexpr int GG = R == 2 ? 3 : G;
     for (; base < r1; base += stride) {
         int64_t row[R];
         bool ok[R];
@@ -1035,10 +883,10 @@ using namespace fdx;
 
 namespace fdx {
 namespace {
-int install_rank_layout(fdx_forest_s *F, int fmt, hipStream_t st);
-// node format a variant runs on: 1 = rank layout v1, 2 = v2, 3 = v1 words in two-level packets
-int variant_format(const Variant &v) { return v.pipe == 202 ? 3 : (v.p16 == 2 || v.p16 == 3 ? 2 : 1); }
-int forest_format(const fdx_forest_s *F) { return F->rank_pk ? 3 : (F->rank_v2 ? 2 : 1); }
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
+// node format a variant runs on: 1 = rank layout v1, 2 = v2
+int variant_format(const Variant &v) { return v.p16 == 2 || v.p16 == 3 ? 2 : 1; }
+int forest_format(const fdx_forest_s *F) { return F->rank_v2 ? 2 : 1; }
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
 
@@ -1102,7 +950,7 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
     // every failure below leaves the forest exactly as it was: the previous node format (the
     // rank layout is rebuilt in it when it was switched), the previous variant and its chunks
     auto refuse = [&](const char *why, int a) {
-        if (forest_format(F) != had) install_rank_layout(F, had, nullptr);
+        if (forest_format(F) != had) install_rank_layout(F, had == 2, nullptr);
         F->variant = prev;
         build_chunks(F);
         upload_chunks(F);
@@ -1110,8 +958,8 @@ extern "C" int fdx_forest_set_variant(fdx_forest F, int32_t variant) {
         return FDX_E_UNSUPPORTED;
     };
     if (v.rank && variant_format(v) != had) {  // the variant runs on the other node format
-        if (install_rank_layout(F, variant_format(v), nullptr))
-            return refuse("variant %d needs rank layout format %d, which this forest does not fit", variant_format(v));
+        if (install_rank_layout(F, variant_format(v) == 2, nullptr))
+            return refuse("variant %d needs rank layout v%d, which this forest does not fit", variant_format(v));
     }
     if (v.rank && v.p16 == 3 && !F->rank_identity)
         return refuse("variant %d needs one threshold slot per feature (<= %d slots)", 16);
@@ -1150,25 +998,22 @@ void free_rank_buffers(fdx_forest_s *F) {
     }
 }
 
-// Build the rank layout (fmt: 1 = v1, 2 = v2, 3 = v1 words in two-level packets) from the host
-// copy of the packed forest and upload it with its search tables; synchronous (creation /
-// set_variant, off the hot path).  On FDX_E_UNSUPPORTED the forest has no rank layout (rank_ok =
-// false).
-int install_rank_layout(fdx_forest_s *F, int fmt, hipStream_t st) {
-    const bool v2 = fmt == 2;
+// Build the rank layout (v2 nodes when `v2`, else v1) from the host copy of the packed forest
+// and upload it with its search tables; synchronous (creation / set_variant, off the hot path).
+// On FDX_E_UNSUPPORTED the forest has no rank layout (rank_ok = false).
+int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
     free_rank_buffers(F);
-    F->rank_ok = F->rank_v2 = F->rank_identity = F->rank_pk = false;
+    F->rank_ok = F->rank_v2 = F->rank_identity = false;
     fdx_forest_desc d{};
     d.n_trees = F->n_trees;
     d.n_features = F->n_features;
     d.node_offsets = F->node_offsets.data();
     RankLayout RL;
     if (v2 && F->zstride != 16) return FDX_E_UNSUPPORTED;
-    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, fmt);
+    int rc = build_rank_layout(&d, F->h_packed, F->h_orig, F->h_depth, kRankNodeCap, RL, v2);
     if (rc) return rc;
     F->rank_ok = true;
     F->rank_v2 = v2;
-    F->rank_pk = fmt == 3;
     if (v2) {
         bool ident = RL.n_slots <= 16 && RL.n_slots == F->n_features;
         for (int j = 0; j < RL.n_slots && ident; ++j) ident = RL.slot_feat[j] == j && RL.slot_base[j] == 0;
@@ -1312,8 +1157,8 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     // than 4,096 nodes under one threshold rank or ranks past 12 bits -- the deployed model);
     // else the wide 8-byte layout.  (fdx_forest_set_variant switches an existing forest to the
     // other rank format.)
-    rc = install_rank_layout(F, 1, st);
-    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, 2, st);
+    rc = install_rank_layout(F, false, st);
+    if (rc == FDX_E_UNSUPPORTED) rc = install_rank_layout(F, true, st);
     if (rc == FDX_E_UNSUPPORTED) rc = FDX_OK;  // the wide layout serves it
     if (rc) {
         fdx_forest_destroy(F);
@@ -1472,7 +1317,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 6, 0, 202); break;
+                case 5: FDX_LAUNCH_RANK(1024, 1, 10, 0, 103); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -53,8 +53,6 @@ struct fdx_forest_s {
     // rank layout v2 (32 threshold-rank slots, see build_rank_layout)
     bool rank_v2 = false;
     bool rank_identity = false;  // v2 with slot s = feature s (<= 16 slots): v1 rank rows, compact planes
-    // rank layout v1 in two-level PACKETS (v1 node words, 16-byte packets: see build_rank_layout)
-    bool rank_pk = false;
     // host copies of the packed forest and scaler (set_variant rebuilds the rank layout in the
     // other node format when a variant needs it)
     std::vector<uint64_t> h_packed;
@@ -148,8 +146,7 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
-    {1024, 1, 6, 1, 0, 202},   // 5: rank layout v1 in two-level packets (the parent and both children
-                               //    in one ds_read_b128; 3 LDS reads per two levels instead of 4)
+    {1024, 1, 10, 1, 0, 103},  // 5: STUDY: rank reads independent of node reads (wrong results)
 };
 // (Round 5 measured v1 over paired u16 planes, two rows per lane with 768 / 512 lanes (12 chains
 // per lane, 12 / 8 waves per CU): 7.90 / 8.74 ms against 6.66 -- the walk's throughput follows
@@ -193,8 +190,6 @@ struct RankLayout {
     int32_t thr_off[33] = {};
     // v2: threshold-rank slots (a feature with more than kSlotSpan thresholds spans several)
     bool v2 = false;
-    // v1 node words in two-level packets (nodes: 4 dwords per packet; lval / orig / ml by dword)
-    bool pk = false;
     int32_t n_slots = 0, slot_feat[32] = {}, slot_base[32] = {};
 };
 constexpr int64_t kSlotSpan = 32767;  // thresholds per rank-layout-v2 slot (build_rank_layout)
@@ -202,9 +197,8 @@ constexpr int64_t kSlotSpan = 32767;  // thresholds per rank-layout-v2 slot (bui
 // kW3Search features: trees (floats, 8 per node), eoff (node offset) and elev (levels) per
 // searched feature.  Empty when they exceed kW3TreeFloats.
 void build_search_trees(const RankLayout &L, std::vector<float> &trees, int32_t eoff[4], int32_t elev[4]);
-// fmt: 1 = v1, 2 = v2, 3 = v1 node words in two-level packets
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
-                      RankLayout &L, int fmt = 1);
+                      RankLayout &L, bool v2 = false);
 
 }  // namespace fdx

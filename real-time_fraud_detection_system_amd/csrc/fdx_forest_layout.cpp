@@ -110,127 +110,6 @@ int pack_forest(const fdx_forest_desc *d, std::vector<uint64_t> &packed, std::ve
 
 
 
-// Two-level packets over the v1 node words (fmt 3 of build_rank_layout, described there).
-static int build_packets(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
-                         const std::vector<int32_t> &worig, int64_t max_tree_nodes,
-                         const std::vector<std::vector<float>> &U, RankLayout &L) {
-    constexpr uint32_t kMarker = 0x0000F000u;  // leaf child: feature 15 (the sentinel plane), k 0, offset 0
-    constexpr uint32_t kBias = 0x800u;         // bit 11 of every internal word (see build_rank_layout)
-    bool ok = true;
-    auto internal = [&](int64_t w) { return (packed[(size_t)w] >> 63) != 0; };
-    auto right_of = [&](int64_t w) { return w + (int64_t)(((uint32_t)(packed[(size_t)w] >> 32) & 0xFFFFFFu) >> 3); };
-    auto leaf_value = [&](int64_t w) {
-        double v;
-        const uint64_t nd = packed[(size_t)w];
-        memcpy(&v, &nd, 8);
-        return v;
-    };
-    auto word = [&](int64_t w) {  // v1 node word of internal node w, offset field 0
-        const uint64_t nd = packed[(size_t)w];
-        const uint32_t hi = (uint32_t)(nd >> 32), lo = (uint32_t)nd;
-        const int f = (int)((hi >> 24) & 63);
-        float t;
-        memcpy(&t, &lo, 4);
-        const int64_t k = std::lower_bound(U[f].begin(), U[f].end(), t) - U[f].begin();
-        return ((uint32_t)k << 16) | ((uint32_t)f << 12) | kBias;
-    };
-    auto feat = [&](int64_t w) { return internal(w) ? (uint32_t)((packed[(size_t)w] >> 56) & 63) : 15u; };
-    auto mleft = [&](int64_t w) { return (uint8_t)(internal(w) ? (packed[(size_t)w] >> 62) & 1 : 0); };
-    int64_t base = 0;  // first packet of the tree being emitted (dword index / 4)
-    // emits the packet of node w (internal, or the root of a single-leaf tree); returns its index
-    std::function<int64_t(int64_t)> emit = [&](int64_t w) -> int64_t {
-        const int64_t p = (int64_t)L.nodes.size() / 4;
-        for (int j = 0; j < 4; ++j) {
-            L.nodes.push_back(0); L.orig.push_back(-1); L.lval.push_back(0.0); L.ml.push_back(0);
-        }
-        auto leaf_at = [&](int j, int64_t leaf) {
-            L.lval[(size_t)(4 * p + j)] = leaf_value(leaf);
-            L.orig[(size_t)(4 * p + j)] = worig[(size_t)leaf];
-        };
-        auto rel = [&](int64_t q) -> uint32_t {
-            if (q - p < 1 || q - p > 2047) ok = false;
-            return (uint32_t)(q - p) & 0x7FFu;
-        };
-        if (!internal(w)) {  // a single-leaf tree
-            L.nodes[(size_t)(4 * p)] = L.nodes[(size_t)(4 * p + 1)] = L.nodes[(size_t)(4 * p + 2)] = kMarker;
-            L.nodes[(size_t)(4 * p + 3)] = 0xFFFF0000u;
-            leaf_at(3, w);
-            return p;
-        }
-        const int64_t l = w + 1, r = right_of(w);
-        uint32_t P = word(w), Lw = kMarker, Rw = kMarker;
-        uint32_t X = 0;
-        const int64_t g[4] = {internal(l) ? l + 1 : -1, internal(l) ? right_of(l) : -1, internal(r) ? r + 1 : -1,
-                              internal(r) ? right_of(r) : -1};
-        for (int j = 0; j < 4; ++j) X |= (g[j] >= 0 ? feat(g[j]) : 15u) << (16 + 4 * j);
-        L.ml[(size_t)(4 * p)] = mleft(w);
-        L.ml[(size_t)(4 * p + 1)] = mleft(l);
-        L.ml[(size_t)(4 * p + 2)] = mleft(r);
-        if (internal(l)) {
-            Lw = word(l);
-            if (internal(g[0])) {
-                if (emit(g[0]) != p + 1) ok = false;  // LL follows its grandparent
-                P |= 1u;
-            } else {
-                leaf_at(0, g[0]);
-            }
-            if (internal(g[1])) Lw |= rel(emit(g[1])); else leaf_at(1, g[1]);
-        } else {
-            leaf_at(1, l);
-        }
-        if (internal(r)) {
-            Rw = word(r);
-            if (internal(g[2])) X |= rel(emit(g[2])); else leaf_at(2, g[2]);
-            if (internal(g[3])) Rw |= rel(emit(g[3])); else leaf_at(3, g[3]);
-        } else {
-            leaf_at(3, r);
-        }
-        L.nodes[(size_t)(4 * p)] = P;
-        L.nodes[(size_t)(4 * p + 1)] = Lw;
-        L.nodes[(size_t)(4 * p + 2)] = Rw;
-        L.nodes[(size_t)(4 * p + 3)] = X;
-        return p;
-    };
-    for (int32_t tr = 0; tr < d->n_trees; ++tr) {
-        const int64_t tb = (int64_t)L.nodes.size();
-        base = tb / 4;
-        const int64_t r0 = d->node_offsets[tr];
-        emit(r0);
-        if (!ok) {
-            set_error("packet layout: tree %d: an offset exceeds 2047 packets", tr);
-            return FDX_E_UNSUPPORTED;
-        }
-        const int64_t te = (int64_t)L.nodes.size();
-        if (te - tb > max_tree_nodes) {
-            set_error("packet layout: tree %d has %lld words > LDS budget %lld", tr, (long long)(te - tb),
-                      (long long)max_tree_nodes);
-            return FDX_E_UNSUPPORTED;
-        }
-        // steps: a leaf at depth D is reached by step ceil(D / 2); a single leaf takes one step
-        int32_t dm = 0;
-        std::vector<std::pair<int64_t, int32_t>> stk{{r0, 0}};
-        while (!stk.empty()) {
-            auto [w, dep] = stk.back();
-            stk.pop_back();
-            if (internal(w)) {
-                stk.push_back({w + 1, dep + 1});
-                stk.push_back({right_of(w), dep + 1});
-            } else {
-                dm = std::max(dm, dep);
-            }
-        }
-        L.root.push_back((int32_t)tb);
-        L.depth.push_back(std::max<int32_t>(1, (dm + 1) / 2));
-        L.offsets.push_back(te);
-    }
-    (void)base;
-    if (L.nodes.size() >= (size_t(1) << 31)) {
-        set_error("packet layout: too many nodes");
-        return FDX_E_UNSUPPORTED;
-    }
-    return FDX_OK;
-}
-
 // Returns FDX_OK, or FDX_E_UNSUPPORTED (with the reason in fdx_last_error) when the forest
 // does not fit the layout (> 15 features, > 32767 distinct thresholds of one feature, a
 // tree larger than the LDS node budget).  `max_tree_nodes` = LDS node budget per chunk.
@@ -245,30 +124,9 @@ static int build_packets(const fdx_forest_desc *d, const std::vector<uint64_t> &
 // slot | [10:0] right offset; leaf 0x7FFF0000 (k' = 0x7FFF >= every r_j: a fixed point of
 // the u16-plane step); jump 0xFFFF0000 | offset (k' = -1 in the step's 16-bit arithmetic:
 // always right).  No sentinel slot.
-//
-// fmt 3 (v1 node words in two-level PACKETS; the walk: fdx_forest.hip rank_walk_packets): a
-// tree is a pre-order sequence of 16-byte packets, one per internal node P at an even depth:
-//   word 0  P  = [30:16] k | [15:12] feature | [11] 1 | [10:0] LLo
-//   word 1  L  = P's left child: [30:16] k | [15:12] feature | [11] 1 | [10:0] LRo -- or the leaf
-//                marker 0x0000F000
-//   word 2  R  = P's right child, [10:0] RRo -- or the marker
-//   word 3  X  = [31:16] the grandchildren's features (LL, LR, RL, RR; 15 = none) | [10:0] RLo
-// where xyo is the offset, in packets, from this packet to the packet of grandchild xy (LL's is
-// always the next packet: LLo = 1), or 0 when that grandchild is a leaf.  Bit 11 keeps the low
-// half of an internal word nonzero, so x - word < 0 <=> r <= k even for feature 0 with offset 0
-// (the v1 walk has that for free: a right offset is never 0).  A step of the walk
-// decides two levels: P's test picks c = L or R (and LG = LLo or RLo), c's test picks LG or c's
-// own offset; offset 0 = stay (the chain is at its leaf: every later step repeats the same two
-// decisions).  Leaves are not stored: the leaf reached from packet p by decisions a (P: 0 = left)
-// and b (c: 0 = left) has index 4p + 2a + b (a leaf child takes b = 1: the marker's sentinel test
-// goes right), and lval / orig are indexed by it; ml holds missing_go_to_left of P, L, R at
-// 4p + 0 / 1 / 2.  A tree that is a single leaf is one packet of markers (a = b = 1).  Steps
-// per tree = max(1, ceil(max leaf depth / 2)).  Offsets are < 2048 packets (no jump nodes; a
-// tree that needs a longer one stays in the v1 layout).
 int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &packed,
                       const std::vector<int32_t> &worig, const std::vector<int32_t> &wdepth, int64_t max_tree_nodes,
-                      RankLayout &L, int fmt) {
-    const bool v2 = fmt == 2;
+                      RankLayout &L, bool v2) {
     if (!v2 && d->n_features > 15) {
         set_error("rank layout: %d features > 15", d->n_features);
         return FDX_E_UNSUPPORTED;
@@ -278,7 +136,6 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
     const int64_t max_off = v2 ? 2047 : kRankMaxOffset;
     const uint32_t leaf_word = v2 ? 0x7FFF0000u : kRankLeaf, jump_word = v2 ? 0xFFFF0000u : kRankJump;
     L.v2 = v2;
-    L.pk = fmt == 3;
     // U_f: sorted unique float32 thresholds per feature
     std::vector<std::vector<float>> U(64);
     for (uint64_t nd : packed)
@@ -318,7 +175,6 @@ int build_rank_layout(const fdx_forest_desc *d, const std::vector<uint64_t> &pac
     L.thr_off[nfeat] = (int32_t)L.thr.size();
     L.nodes.clear(); L.orig.clear(); L.lval.clear(); L.ml.clear(); L.root.clear(); L.depth.clear();
     L.offsets.assign(1, 0);
-    if (L.pk) return build_packets(d, packed, worig, max_tree_nodes, U, L);
     struct Pend { int64_t owner; };
     std::vector<Pend> pend;
     int margin = 0;
@@ -471,13 +327,13 @@ static int rank_layout_host(const fdx_forest_desc *d, RankLayout &RL, int versio
     std::vector<int32_t> orig, root, depth;
     int rc = pack_forest(d, packed, orig, root, depth);
     if (rc) return rc;
-    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version);
+    return build_rank_layout(d, packed, orig, depth, kRankNodeCap, RL, version == 2);
 }
 
 extern "C" int fdx_forest_rank_layout_size2(const fdx_forest_desc *d, int32_t version, int64_t *n_nodes,
                                             int32_t *n_thresholds, int32_t *n_slots) {
     FDX_REQUIRE(n_nodes && n_thresholds && n_slots, "null output");
-    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3 (packets)");
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
     RankLayout RL;
     int rc = rank_layout_host(d, RL, version);
     if (rc) return rc;
@@ -491,7 +347,7 @@ extern "C" int fdx_forest_pack_rank2(const fdx_forest_desc *d, int32_t version, 
                                      int32_t *orig_out, double *leaf_value_out, uint8_t *missing_left_out,
                                      int32_t *root_out, int32_t *depth_out, float *thr_out, int32_t *thr_off_out,
                                      int32_t *slot_feat_out, int32_t *slot_base_out) {
-    FDX_REQUIRE(version >= 1 && version <= 3, "version must be 1, 2 or 3 (packets)");
+    FDX_REQUIRE(version == 1 || version == 2, "version must be 1 or 2");
     FDX_REQUIRE(nodes_out && orig_out && leaf_value_out && missing_left_out && root_out && depth_out && thr_off_out &&
                     slot_feat_out && slot_base_out,
                 "null output");

@@ -320,93 +320,3 @@ def test_search_trees_count_samples(which):
         seg = useg[(np.maximum(cs - 1, 0) * 4)[:, None] + np.arange(4)]
         rank = np.where(cs > 0, (cs - 1) * 4 + (seg < v[:, None]).sum(1), 0)
         np.testing.assert_array_equal(rank, np.searchsorted(thr, v, side="left"))
-
-
-def walk_packets(R, z32):
-    """numpy model of the packet walk (k_forest_rank, variant 5: rank_walk_packets): per step,
-    P's test (x_P - P < 0: left; NaN: missing_go_to_left) picks c = L or R and LG = P or X, c's
-    test picks LG or c, offset = that word & 0x7FF packets (0 = stay); after the last step the
-    leaf is 4p + 2a + b (a, b = 1 for right)."""
-    n = z32.shape[0]
-    xv = np.zeros((n, 16), np.int64)
-    nanm = np.zeros((n, 16), bool)
-    for f in range(min(z32.shape[1], 15)):
-        u = R["thr"][R["thr_off"][f]:R["thr_off"][f + 1]]
-        xv[:, f] = np.searchsorted(u, z32[:, f], side="left").astype(np.int64) << 16
-        nanm[:, f] = np.isnan(z32[:, f])
-    xv[:, 15] = 0x4000 << 16
-    nodes = R["nodes"].astype(np.int64)
-    acc = np.zeros(n)
-    nt = len(R["root"])
-    leaves = np.zeros((n, nt), np.int32)
-    rows = np.arange(n)
-    for t in range(nt):
-        p = np.full(n, R["root"][t], np.int64)
-        assert R["depth"][t] >= 1
-        for s in range(int(R["depth"][t])):
-            P, Lw, Rw, X = nodes[p], nodes[p + 1], nodes[p + 2], nodes[p + 3]
-            fP = (P >> 12) & 15
-            a_left = np.where(nanm[rows, fP], R["ml"][p] != 0, xv[rows, fP] - P < 0)
-            c = np.where(a_left, Lw, Rw)
-            lgo = np.where(a_left, P, X)
-            fc = (c >> 12) & 15
-            b_left = np.where(nanm[rows, fc], R["ml"][p + np.where(a_left, 1, 2)] != 0, xv[rows, fc] - c < 0)
-            st = np.where(b_left, lgo, c) & 0x7FF
-            if s + 1 < R["depth"][t]:
-                p = p + 4 * st
-        assert (st == 0).all(), "walk did not end on leaves within depth"
-        idx = p + 2 * (~a_left) + (~b_left)
-        acc = acc + R["lval"][idx]
-        leaves[:, t] = R["orig"][idx]
-    return acc / nt, leaves
-
-
-def test_packet_layout_reproduces_sklearn(golden):
-    """Two-level packets (version 3) give sklearn's leaves and proba on the golden forests
-    (incl. 20 % NaN features), with one packet per internal node at an even depth."""
-    for name in ("forest_dt2.npz", "forest_rf5d8.npz", "forest_rf3.npz"):
-        z = golden(name)
-        R = pack_rank2(z, version=3)
-        assert R is not None and len(R["nodes"]) % 4 == 0
-        proba, leaves = walk_packets(R, _z32(z["X"], z["mean"], z["scale"]))
-        np.testing.assert_array_equal(leaves, z["leaves"])
-        np.testing.assert_array_equal(proba, z["proba"])
-
-
-def test_packet_layout_random_forests_nan_and_single_leaf_trees():
-    """Random unbalanced forests (leaves at every depth, NaN rows routed by missing_go_to_left)
-    plus single-leaf trees and depth-1 stumps: leaves and proba equal the C oracle."""
-    rng = np.random.default_rng(23)
-    a = random_forest(rng, 6, 11, p_leaf=0.15)
-    # prepend a single-leaf tree and a stump
-    lone = dict(left=np.array([-1]), right=np.array([-1]), feature=np.array([-2]), threshold=np.array([-2.0]),
-                missing_left=np.array([0], np.uint8), value1=np.array([0.375]))
-    stump = dict(left=np.array([1, -1, -1]), right=np.array([2, -1, -1]), feature=np.array([3, -2, -2]),
-                 threshold=np.array([0.25, -2.0, -2.0]), missing_left=np.array([1, 0, 0], np.uint8),
-                 value1=np.array([0.0, 0.125, 0.875]))
-    parts = [lone, stump] + [{k: a[k][a["node_offsets"][t]:a["node_offsets"][t + 1]] for k in lone}
-                             for t in range(len(a["node_offsets"]) - 1)]
-    b = {k: np.concatenate([pt[k] for pt in parts]) for k in lone}
-    b["node_offsets"] = np.concatenate([[0], np.cumsum([len(pt["left"]) for pt in parts])]).astype(np.int64)
-    R = pack_rank2(b, version=3)
-    assert R is not None
-    X = rng.normal(size=(4000, 15))
-    X[rng.random(X.shape) < 0.05] = np.nan
-    op, ol = oracle.forest_predict(X, b, want_leaves=True)
-    proba, leaves = walk_packets(R, X.astype(np.float32))
-    np.testing.assert_array_equal(leaves, ol)
-    np.testing.assert_array_equal(proba, op)
-
-
-def test_packet_layout_bench_model():
-    """The config-3 model in packets: fewer LDS words than v1 (leaves are implicit), ten
-    two-level steps per depth-20 tree, sklearn's predict_proba bit for bit."""
-    from conftest import ROOT
-
-    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
-    R = pack_rank2(z, version=3)
-    assert R is not None
-    assert len(R["nodes"]) < len(pack_rank(z)["nodes"])
-    assert (R["depth"] == 10).all()
-    proba, _ = walk_packets(R, _z32(z["check_X"], z["mean"], z["scale"]))
-    np.testing.assert_array_equal(proba, z["check_proba"])
