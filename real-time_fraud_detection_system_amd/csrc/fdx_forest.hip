@@ -237,7 +237,7 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         uint32_t st;
-        if (NAN_AWARE && x[k] == (P16 ? 0xFFFFu : 0xFFFFFFFFu)) {
+        if (NAN_AWARE && x[k] == (P16 ? 0xFFFFu : 0xFFFF0000u)) {  // (u32 planes: stage_planes_u32)
             st = mleft[(pa[k] - kNodeB<P16>) >> 2] != 0 ? 1u : (nd[k] & kOffMask<P16>);
         } else {
             const int32_t d = P16 ? (int32_t)((x[k] << 16) + nd[k]) : (int32_t)(x[k] - nd[k]);
@@ -380,18 +380,19 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
         }
     };
     int d = 0;
-    // whole unrolled intervals, no test (pre <= depth - kExitEvery: never the last step)
-    for (; d + kExitEvery <= pre; d += kExitEvery) {
-#pragma unroll
-        for (int e = 0; e < kExitEvery; ++e) step();
-    }
+    // whole unrolled intervals; the exit test only past the first `pre` steps (pre <= depth -
+    // kExitEvery: never the last step).  One loop, not a test-free loop and a testing one: two
+    // loops over the same step got different registers, and the copies between them cost ~30
+    // v_mov per tile.
     for (; d + kExitEvery < depth; d += kExitEvery) {
 #pragma unroll
         for (int e = 0; e < kExitEvery; ++e) step();
-        uint32_t moving = 0;
+        if (d + kExitEvery > pre) {  // (uniform)
+            uint32_t moving = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
-        if (!__any(moving != 0)) return d + kExitEvery;
+            for (int k = 0; k < K; ++k) moving |= nd[k] & kOffMask<P16>;
+            if (!__any(moving != 0)) return d + kExitEvery;
+        }
     }
     if (d < depth) {  // 1 .. kExitEvery steps left, the last without reads
         if (d + kExitEvery == depth) {
@@ -451,15 +452,48 @@ __device__ __forceinline__ int rank_trees_from(const char *lds, const uint32_t (
         rank_walk<true, P16, K>(lds, lane_base, pa, nd, dmax, ml);
         return 0;
     }
-    return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, pre);
+    if constexpr (PIPE == 102) {
+        // the first step from the launch-uniform root words (SGPRs): d = x - root,
+        // med3(d, 1, root & 0xFFF) with the offset masked on the scalar unit, pa = root address +
+        // 4 step -- 3 VALU and no copy of the roots into VGPRs (4 VALU + 2 v_mov per chain)
+        if (dmax <= 0) return 0;
+        uint32_t x[K];
+#pragma unroll
+        for (int g = 0; g < GG; ++g)
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[r * GG + g] = lds32(lds, (rn[g] & 0xF000u) | lane_base[r * GG + g]);
+#pragma unroll
+        for (int g = 0; g < GG; ++g) {
+            const uint32_t off = __builtin_amdgcn_readfirstlane(rn[g] & 0xFFFu);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int k = r * GG + g;
+                uint32_t dd, st;
+                asm("v_sub_u32 %[d], %[x], %[n]\n\t"
+                    "v_med3_i32 %[s], %[d], 1, %[o]\n\t"
+                    "v_lshl_add_u32 %[p], %[s], 2, %[b]"
+                    : [p] "=v"(pa[k]), [d] "=&v"(dd), [s] "=&v"(st)
+                    : [x] "v"(x[k]), [n] "s"(rn[g]), [o] "s"(off), [b] "s"(rp[g]));
+            }
+        }
+        if (dmax == 1) return 1;  // (the walk's last step reads nothing)
+#pragma unroll
+        for (int k = 0; k < K; ++k) nd[k] = lds32(lds, pa[k]);
+        return 1 + rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax - 1, pre - 1);
+    } else {
+        return rank_walk_pipe<P16, K, PIPE>(lds, lane_base, pa, nd, dmax, pre);
+    }
 }
 
 template <int K>
 __device__ __forceinline__ void rank_leaf_values(const uint32_t (&pa)[K], int64_t node_base,
                                                  const double *__restrict__ lval, double (&v)[K],
                                                  uint32_t nodeb = kRankNodeB) {
+    // lval[node_base + (pa - nodeb) / 4] as a uniform 64-bit base + a 32-bit byte offset 2 * pa:
+    // one VALU per load (global_load saddr + voffset) instead of a 64-bit address per lane
+    const char *base = reinterpret_cast<const char *>(lval + node_base) - (size_t)(nodeb >> 2) * sizeof(double);
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = lval[node_base + ((pa[k] - nodeb) >> 2)];
+    for (int k = 0; k < K; ++k) v[k] = *reinterpret_cast<const double *>(base + (uint32_t)(pa[k] << 1));
 }
 
 // a[r] += v[r*GG + g] in tree order
@@ -521,7 +555,7 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-// The 15 u32 plane words of row slot r * BLOCK + tid (rank << 16, NaN 0xFFFFFFFF).  With
+// The 15 u32 plane words of row slot r * BLOCK + tid (rank << 16, NaN 0xFFFF0000).  With
 // ds_write_addtid_b32 (address = M0 + offset + 4 * lane; no address VGPR) a store moves 4 B per
 // lane in 2 LDS cycles, half of ds_write_b32's 4: the planes are re-staged for every 1,024-row
 // tile, 15 stores per lane against ~220 walk reads.  The kernel's code uses M0 nowhere else.
@@ -556,21 +590,15 @@ __device__ __forceinline__ void stage_words(uint32_t *s_x, int r, const uint32_t
         : "memory", "m0");
 #pragma clang diagnostic pop
 }
-// nan: the batch has NaN features (rank 0xFFFF -> 0xFFFFFFFF, the NaN-aware walk's marker: three
-// VALU per feature); without NaNs one VALU per feature (a shift or a mask of the rank pair)
+// One VALU per feature (a shift or a mask of the rank pair).  A NaN feature's rank 0xFFFF becomes
+// 0xFFFF0000, the NaN-aware walk's marker (ranks are <= 0x7FFF): no second form for NaN batches
+// (a form per batch kind left the compiler computing one and moving it into the other's
+// registers, 15 v_mov per tile).
 template <int BLOCK>
-__device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uint32_t (&w)[8], bool nan) {
+__device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uint32_t (&w)[8]) {
     uint32_t x[15];
-    if (nan) {
 #pragma unroll
-        for (int f = 0; f < 15; ++f) {
-            const uint32_t u = (w[f >> 1] >> ((f & 1) * 16)) & 0xFFFFu;
-            x[f] = u == 0xFFFFu ? 0xFFFFFFFFu : u << 16;
-        }
-    } else {
-#pragma unroll
-        for (int f = 0; f < 15; ++f) x[f] = (f & 1) ? w[f >> 1] & 0xFFFF0000u : w[f >> 1] << 16;
-    }
+    for (int f = 0; f < 15; ++f) x[f] = (f & 1) ? w[f >> 1] & 0xFFFF0000u : w[f >> 1] << 16;
     stage_words<BLOCK>(s_x, r, x);
 }
 
@@ -736,7 +764,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 } else {
                     const uint32_t w8[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
                     if constexpr (P16 == 0) {
-                        stage_planes_u32<BLOCK>(s_x, r, w8, any_nan);
+                        stage_planes_u32<BLOCK>(s_x, r, w8);
                     } else {
 #pragma unroll
                         for (int f = 0; f < 16; ++f)
@@ -811,7 +839,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             } else {
                 const uint32_t w[8] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w};
                 if constexpr (P16 == 0) {
-                    stage_planes_u32<BLOCK>(s_x, r, w, any_nan);
+                    stage_planes_u32<BLOCK>(s_x, r, w);
                 } else {
 #pragma unroll
                     for (int f = 0; f < 16; ++f)

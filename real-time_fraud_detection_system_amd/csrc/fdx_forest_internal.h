@@ -84,7 +84,7 @@ constexpr uint32_t kInternal = 0x80000000u;
 // d > 4095, so med3 = j: it forwards to p + j (the packer inserts jumps after leaves wherever
 // a right offset would exceed 4095).  No lane-mask instruction, so no VCC hazard stalls.
 // Leaf values (float64) and sklearn node ids live in global arrays indexed by rank-layout
-// position; NaN row values are 0xFFFF (u16) / 0xFFFFFFFF (LDS), resolved by
+// position; NaN row values are 0xFFFF (u16) / 0xFFFF0000 (LDS), resolved by
 // missing_go_to_left from a global byte array in the NaN-aware walk.  Ranks travel through
 // HBM as 16 x u16 = 32 B per row (half the float32 row).
 constexpr uint32_t kRankLeaf = 0x7FFFF000u;

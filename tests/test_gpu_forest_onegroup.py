@@ -121,3 +121,37 @@ def test_refused_variant_leaves_the_forest_intact(dev):
     f.set_variant(2)
     assert f.n_chunks == nc0
     np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+
+
+def _lone_and_stump():
+    lone = dict(left=np.array([-1]), right=np.array([-1]), feature=np.array([-2]), threshold=np.array([-2.0]),
+                missing_left=np.array([0], np.uint8), value1=np.array([0.375]))
+    stump = dict(left=np.array([1, -1, -1]), right=np.array([2, -1, -1]), feature=np.array([3, -2, -2]),
+                 threshold=np.array([0.25, -2.0, -2.0]), missing_left=np.array([1, 0, 0], np.uint8),
+                 value1=np.array([0.0, 0.125, 0.875]))
+    return lone, stump
+
+
+def _forest_of(parts):
+    b = {k: np.concatenate([pt[k] for pt in parts]) for k in parts[0]}
+    b["node_offsets"] = np.concatenate([[0], np.cumsum([len(pt["left"]) for pt in parts])]).astype(np.int64)
+    for k in ("left", "right", "feature"):
+        b[k] = b[k].astype(np.int64)
+    return b
+
+
+@pytest.mark.parametrize("kinds", ["lone", "stump", "lone+stump", "stump+lone+stump"])
+def test_one_group_degenerate_depths(dev, kinds):
+    """Chunks whose deepest tree has depth 0 (a single leaf) or 1 (a stump): the walk's first step
+    from the launch-uniform root words and its read-free last step coincide or vanish.  Every
+    row == the C oracle, NaN rows included (missing_go_to_left of the stump)."""
+    lone, stump = _lone_and_stump()
+    arr = _forest_of([{"lone": lone, "stump": stump}[k] for k in kinds.split("+")])
+    f = ops.Forest(arr, 15)
+    assert f.variant == 1
+    rng = np.random.default_rng(len(kinds))
+    X = rng.normal(size=(300_001, 15))
+    X[rng.random(X.shape) < 0.03] = np.nan
+    for Xi in (np.nan_to_num(X, nan=0.5), X):
+        p = f.predict(T(Xi, torch.float64, dev)).cpu().numpy()
+        np.testing.assert_array_equal(p, oracle.forest_predict(Xi, arr))
