@@ -152,6 +152,10 @@ def parse():
                          "transaction in SURVEY.md §8(d)'s compact form + the row index, as columns by scoring slot "
                          "(default, coalesced: ops.FeatureTable) or as 80-byte records by input row (one random "
                          "write per row: ops.FeatureRecords); none: scores only")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal of the N > 1 orchestration on a one-GPU box: every rank on cuda:0, a gloo "
+                         "process group, the exchange's two collectives staged through host memory (RCCL needs a "
+                         "GPU per rank); the line is marked \"rehearsal\" and its timing is not a measurement")
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (RCCL all-to-all) path even at 1 GPU (measures its overhead)")
     return ap.parse_args()
@@ -371,6 +375,33 @@ def cpu_baseline(data, arrays, mean, scale, check_X, check_proba, score_rows):
             "host": info}
 
 
+def rehearse_host_collectives():
+    """--rehearse-one-gpu: the exchange's two collectives (fdx.distributed.all_to_all_split_pairs
+    and alltoallv, module-level for this) copy their device buffers through host memory and run
+    the same gloo all-to-all / batched point-to-point there; everything else is the product path
+    (as tests/test_gpu_aa_sharded_world2.py does)."""
+    import torch
+    import torch.distributed as dist
+
+    from fdx import distributed as D
+
+    staged_v = D.alltoallv
+
+    def pairs_host(out, inp, group=None):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), group=group)
+        out.copy_(h)
+        return out
+
+    def alltoallv_host(out, inp, out_splits, in_splits, group=None):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        staged_v(h, inp.cpu(), out_splits, in_splits, group)
+        out.copy_(h)
+        return out
+
+    D.all_to_all_split_pairs, D.alltoallv = pairs_host, alltoallv_host
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -385,10 +416,15 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    cdev = torch.device("cpu") if args.rehearse_one_gpu else dev  # bench's own reductions
+    if world > 1 and args.rehearse_one_gpu:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, f"world {dist.get_world_size()} != --gpus {args.gpus}"
+        rehearse_host_collectives()
+    elif world > 1:
         dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus, f"world {dist.get_world_size()} != --gpus {args.gpus}"
     elif args.sharded:
@@ -483,7 +519,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt, float(n_local)], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, float(n_local)], dtype=torch.float64, device=cdev)
         dtm = t[:1].clone()
         dist.all_reduce(dtm, op=dist.ReduceOp.MAX)
         tot = t[1:].clone()
@@ -534,6 +570,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "setup_s": {"generate_on_gpu": round(t_gen, 2)},
+        **({"rehearsal": "--rehearse-one-gpu: every rank on one GPU, host-staged gloo collectives; not a "
+                         "measurement"} if args.rehearse_one_gpu else {}),
         "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234+rank), "
                 "resident in HBM" + ("; each rank draws its customers' rows from its own seed, so the configs[3] "
                                      "union differs per N (its distributions do not)" if world > 1 else ""),
@@ -647,7 +685,7 @@ def main():
             link_ms.append(span(mk, *mk["exchange_rows"]) + span(mk, *mk["exchange_back"]))
         mean = lambda v: sum(v) / len(v)  # noqa: E731
         loc = torch.tensor([float(n_local), float(shard_stats.get("bytes_to_peers", 0)), mean(ex_ms), mean(link_ms),
-                            mean(hidden_ms)], dtype=torch.float64, device=dev)
+                            mean(hidden_ms)], dtype=torch.float64, device=cdev)
         if world > 1:
             allr = [torch.empty_like(loc) for _ in range(world)]
             dist.all_gather(allr, loc)
