@@ -78,6 +78,8 @@ def _bit_length(c):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="as bench.py: every rank on cuda:0, gloo, host-staged exchange collectives (not a measurement)")
     ap.add_argument("--customers", type=int, default=1_000_000)
     ap.add_argument("--terminals", type=int, default=2_000_000)
     ap.add_argument("--history-days", type=int, default=38)
@@ -104,7 +106,7 @@ def rank_shard(args, world: int, rank: int):
 
 def main():
     args = parse()
-    from bench import load_model, spawn_ranks, stdout_to_stderr
+    from bench import load_model, rehearse_host_collectives, spawn_ranks, stdout_to_stderr
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))  # one process per GPU, before this one touches the GPU
@@ -118,12 +120,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    cdev = torch.device("cpu") if args.rehearse_one_gpu else dev  # this script's own collectives
+    if world > 1 and args.rehearse_one_gpu:
+        dist.init_process_group("gloo")
+        rehearse_host_collectives()
+    elif world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     n_c, base, _ = rank_shard(args, world, rank)
@@ -154,12 +160,12 @@ def main():
     if rank == 0:
         cuts = s_ts[::per_rank].astype(np.int64)
         cuts = np.r_[cuts, s_ts[-1] + 1] if len(s_ts) else np.array([split, split + 1])
-        hdr = torch.tensor([len(cuts)], dtype=torch.int64, device=dev)
+        hdr = torch.tensor([len(cuts)], dtype=torch.int64, device=cdev)
     else:
-        hdr = torch.zeros(1, dtype=torch.int64, device=dev)
+        hdr = torch.zeros(1, dtype=torch.int64, device=cdev)
     if world > 1:
         dist.broadcast(hdr, 0)
-    cut_t = torch.zeros(int(hdr.item()), dtype=torch.int64, device=dev)
+    cut_t = torch.zeros(int(hdr.item()), dtype=torch.int64, device=cdev)
     if rank == 0:
         cut_t.copy_(torch.from_numpy(cuts))
     if world > 1:
@@ -259,10 +265,10 @@ def main():
     lat, dev_ms = np.array(lat), np.array(dev_ms)
     total_rows = rows
     if world > 1:
-        t = torch.tensor(np.stack([lat, dev_ms]), dtype=torch.float64, device=dev)
+        t = torch.tensor(np.stack([lat, dev_ms]), dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         lat, dev_ms = t[0].cpu().numpy(), t[1].cpu().numpy()
-        r = torch.tensor([rows], dtype=torch.int64, device=dev)
+        r = torch.tensor([rows], dtype=torch.int64, device=cdev)
         dist.all_reduce(r)
         total_rows = int(r.item())
     out = {
@@ -281,6 +287,8 @@ def main():
         "warmup": int(n_warm),
         "mean_batch_tx": round(total_rows / max(n_timed, 1), 1),
         "dtype": "f64",
+        **({"rehearsal": "--rehearse-one-gpu: every rank on one GPU, host-staged gloo collectives; not a "
+                         "measurement"} if args.rehearse_one_gpu else {}),
         "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 4321+rank)",
         "config": {"workload": f"configs[4]: tail of configs[3] ({args.customers} customers / {args.terminals} "
                                f"terminals), {args.history_days} days of history in the state, then day "
