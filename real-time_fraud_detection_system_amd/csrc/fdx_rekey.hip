@@ -243,42 +243,44 @@ __global__ void __launch_bounds__(kBlock) k_radix_scatter(
     // bound tested per item, the flag byte's use right after its load made the compiler wait
     // for each item in turn (16 dependent HBM round trips per tile)
     const bool full = base + kTile <= n;  // uniform
-    auto load_items = [&](auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        if (vals_in) {
+    if (vals_in) {
+        if (full) {
 #pragma unroll
             for (int r = 0; r < kItems; ++r) {
                 const int64_t i = wbase + (int64_t)r * kWave;
-                key[r] = (FULL || i < n) ? keys_in[FULL ? i : min(i, n - 1)] : (K)0;
-                val[r] = (FULL || i < n) ? vals_in[FULL ? i : min(i, n - 1)] : 0u;
-            }
-        } else if (flag_in) {
-            uint32_t fl[kItems];
-#pragma unroll
-            for (int r = 0; r < kItems; ++r) {
-                const int64_t i = FULL ? wbase + (int64_t)r * kWave : min(wbase + (int64_t)r * kWave, n - 1);
                 key[r] = keys_in[i];
-                fl[r] = flag_in[i];
-            }
-#pragma unroll
-            for (int r = 0; r < kItems; ++r) {
-                const int64_t i = wbase + (int64_t)r * kWave;
-                val[r] = (uint32_t)i | (fl[r] ? 0x80000000u : 0u);
-                if (!FULL && i >= n) key[r] = (K)0;
+                val[r] = vals_in[i];
             }
         } else {
 #pragma unroll
             for (int r = 0; r < kItems; ++r) {
-                const int64_t i = wbase + (int64_t)r * kWave;
-                key[r] = FULL ? keys_in[i] : (i < n ? keys_in[min(i, n - 1)] : (K)0);
-                val[r] = (uint32_t)i;
+                const int64_t i = wbase + (int64_t)r * kWave, j = min(i, n - 1);
+                key[r] = i < n ? keys_in[j] : (K)0;
+                val[r] = i < n ? vals_in[j] : 0u;
             }
         }
-    };
-    if (full)
-        load_items(std::true_type{});
-    else
-        load_items(std::false_type{});
+    } else if (flag_in) {
+        uint32_t fl[kItems];
+#pragma unroll
+        for (int r = 0; r < kItems; ++r) {
+            const int64_t i = min(wbase + (int64_t)r * kWave, n - 1);  // (full tiles: never clamped)
+            key[r] = keys_in[i];
+            fl[r] = flag_in[i];
+        }
+#pragma unroll
+        for (int r = 0; r < kItems; ++r) {
+            const int64_t i = wbase + (int64_t)r * kWave;
+            val[r] = (uint32_t)i | (fl[r] ? 0x80000000u : 0u);
+            if (i >= n) key[r] = (K)0;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < kItems; ++r) {
+            const int64_t i = wbase + (int64_t)r * kWave;
+            key[r] = i < n ? keys_in[min(i, n - 1)] : (K)0;
+            val[r] = (uint32_t)i;
+        }
+    }
     // payload registers: stream q's 16 values of this lane, coalesced in input order (clamped:
     // no branch); the loads of stream 0 go out behind the key re-order and those of stream q + 1
     // while stream q is re-ordered (r03: each after the previous phase's stores, or stream 0 with
