@@ -307,7 +307,7 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
     auto step = [&]() {
         if constexpr (PW >= 100) {
-            static_assert((PW == 102 || PW == 103) && P16 == 0, "interleaved pairs: u32 planes");
+            static_assert(PW == 102 && P16 == 0, "interleaved pairs: u32 planes");
 #pragma unroll
             for (int g = 0; g < K; g += 2) {
                 if (g + 1 < K) {
@@ -322,10 +322,8 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
             }
 #pragma unroll
             for (int g = 0; g < K; g += 2) {
-                // PW 103 (STUDY, wrong results): the rank address from the node's ADDRESS, so the
-                // rank read does not wait for the node read -- one LDS round trip per step
-                const uint32_t a0 = ((PW == 103 ? pa[g] << 10 : nd[g]) & kSlotMask<P16>) | lane_base[g];
-                const uint32_t a1 = g + 1 < K ? ((PW == 103 ? pa[g + 1] << 10 : nd[g + 1]) & kSlotMask<P16>) | lane_base[g + 1] : 0u;
+                const uint32_t a0 = (nd[g] & kSlotMask<P16>) | lane_base[g];
+                const uint32_t a1 = g + 1 < K ? (nd[g + 1] & kSlotMask<P16>) | lane_base[g + 1] : 0u;
                 x[g] = rank_x<P16>(lds, a0);
                 if (g + 1 < K) x[g + 1] = rank_x<P16>(lds, a1);
                 __builtin_amdgcn_sched_barrier(0);
@@ -1345,7 +1343,6 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 10, 0, 103); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -146,8 +146,10 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
-    {1024, 1, 10, 1, 0, 103},  // 5: STUDY: rank reads independent of node reads (wrong results)
 };
+// (Round 5 also measured a one-round-trip study form (rank address from the node's address, wrong
+// results: 7.05 vs 6.70 ms) and two-level packets (commit 654bb3b: bit-exact, 12 % slower per
+// tree-step; profiles/r05uz_forest_walk_studies.txt) and removed them.)
 // (Round 5 measured v1 over paired u16 planes, two rows per lane with 768 / 512 lanes (12 chains
 // per lane, 12 / 8 waves per CU): 7.90 / 8.74 ms against 6.66 -- the walk's throughput follows
 // the waves per CU, not the chains per lane -- and removed them.)

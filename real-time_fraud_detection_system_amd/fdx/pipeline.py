@@ -48,6 +48,11 @@ class FraudPipeline:
     # terminal half's (measured, profiles/r03m* and r03w*)
     crit_priority = -1
     side_priority = 0
+    # run_fused: the terminal half starts once the customer re-key is done on the device, so the
+    # critical chain's re-key has the GPU to itself (started together, the two re-keys took 0.90 and
+    # 1.00 ms in step instead of 0.56 and 0.46 alone; the terminal half then overlaps the layout plan,
+    # the layout and the walk: front half + assembly 3.84 -> 3.74 ms, profiles/r05ak_stream_order_ab.txt)
+    terminal_after_customer_rekey = True
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
@@ -134,8 +139,9 @@ class FraudPipeline:
         input row order.
 
         Streams: the terminal half (re-key + windows) runs on a side stream, concurrently with
-        the customer half -- the customer walk is a latency-bound recurrence with one lane per
-        (customer, window) that leaves most SIMDs idle; the two meet at the row assembly.  The
+        the customer half's layout plan, layout and walk (it waits for the customer re-key:
+        terminal_after_customer_rekey) -- the customer walk is a latency-bound recurrence with one
+        lane per (customer, window) that leaves most SIMDs idle; the two meet at the row assembly.  The
         critical chain (customer half, assembly, forest) runs on a high-priority stream of the
         pipeline's own, ordered after the caller's stream on entry and before it on return.
         mark(stage, stream) is called after each stage is enqueued on its stream (bench.py
@@ -184,6 +190,8 @@ class FraudPipeline:
                 cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
                                                            bad=bad[0:1] if validate else None)
                 mk("rekey_customer", main)
+                if self.terminal_after_customer_rekey:
+                    side.wait_stream(main)
                 # the walk's layout plan goes right behind the re-key; its slot count is read only
                 # after the terminal half is enqueued (no host wait between the two)
                 pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
