@@ -44,14 +44,16 @@ class FraudPipeline:
     sums, fully parallel, within ~1e-13 relative of pandas (the counts
     and every other feature stay exact)."""
 
-    # run_fused's stream priorities (lower = higher priority): the critical chain's and the
-    # terminal half's (measured, profiles/r03m* and r03w*)
-    crit_priority = -1
-    side_priority = 0
-    # run_fused: the terminal half starts once the customer re-key is done on the device, so the
-    # critical chain's re-key has the GPU to itself (started together, the two re-keys took 0.90 and
-    # 1.00 ms in step instead of 0.56 and 0.46 alone; the terminal half then overlaps the layout plan,
-    # the layout and the walk: front half + assembly 3.84 -> 3.74 ms, profiles/r05ak_stream_order_ab.txt)
+    # run_fused: the terminal half starts once the customer re-key is done on the device, so that
+    # re-key has the GPU to itself (started together, the two re-keys took 0.90 and 1.00 ms in step
+    # instead of 0.56 and 0.46 alone), and then runs at the HIGHER stream priority (lower number):
+    # the customer walk's one-wave blocks take 22 KB of LDS each, 7 per CU fill a CU's LDS, and
+    # dispatched first they left the terminal scatter (37-42 KB blocks) no CU until the walk's
+    # queue drained (1.2 ms for a 0.2 ms pass, profiles/r05am trace).  Front half + assembly:
+    # 3.84 (both at the start, customer high) -> 3.74 (terminal after the customer re-key) ->
+    # 3.58-3.60 ms (and at high priority); profiles/r05ak_stream_order_ab.txt, r05an_priority_ab.txt.
+    crit_priority = 0
+    side_priority = -1
     terminal_after_customer_rekey = True
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
@@ -142,8 +144,9 @@ class FraudPipeline:
         the customer half's layout plan, layout and walk (it waits for the customer re-key:
         terminal_after_customer_rekey) -- the customer walk is a latency-bound recurrence with one
         lane per (customer, window) that leaves most SIMDs idle; the two meet at the row assembly.  The
-        critical chain (customer half, assembly, forest) runs on a high-priority stream of the
-        pipeline's own, ordered after the caller's stream on entry and before it on return.
+        customer half, assembly and forest run on a stream of the pipeline's own, the terminal half
+        on a higher-priority one (crit_priority / side_priority), ordered after the caller's stream
+        on entry and before it on return.
         mark(stage, stream) is called after each stage is enqueued on its stream (bench.py
         records a HIP event there).  validate: the customer / terminal ids must lie in
         [0, n_customers) / [0, n_terminals) (counted on the device, read once everything is
@@ -162,10 +165,7 @@ class FraudPipeline:
             return proba
         if getattr(self, "_side", None) is None or self._side.device != ts_ns.device:
             self._side = torch.cuda.Stream(device=ts_ns.device, priority=self.side_priority)
-            # the customer half -> assembly -> forest chain is the critical path: it runs on a
-            # high-priority stream of the pipeline's own, the terminal half on a default one,
-            # so that the dispatcher serves the critical kernels first when both have work
-            # (measured: 12.35-12.40 -> 12.19-12.22 ms/step at config 2, profiles/r03m*)
+            # two streams of the pipeline's own; their priorities: crit_priority / side_priority
             self._crit = torch.cuda.Stream(device=ts_ns.device, priority=self.crit_priority)
         main = self._crit if overlap else caller
         side = self._side if overlap else caller
