@@ -559,6 +559,12 @@ constexpr int kChunk = 16;   // rows per cooperative load; divides every ring si
 constexpr int kWalkSplitRows = 480;
 constexpr int kWalkLongWaves = 2;   // waves per group, long class (11 + 10 customers)
 constexpr int kWalkShortWaves = 1;  // waves per group, short class
+// rows per chunk of k_customer_walk: 8, not kChunk = 16 -- the per-chunk register arrays (outputs
+// double-buffered over two chunks, window starts) take 116-124 VGPRs instead of 184-200, so a walk
+// wave leaves room for other kernels' waves on its SIMD (the terminal re-key runs beside the walk):
+// step minus forest 3.59-3.60 -> 3.56-3.57 ms on one box, the walk alone 0.72 -> 0.73 ms
+// (profiles/r05aq_walk_chunk_ab.txt)
+constexpr int kWalkChunk = 8;
 
 // kRing rows per segment stay in LDS.  Launched once per ring size over length classes of
 // groups (a block outside [lg_min, lg_max) exits at once): long segments belong to busy
@@ -724,7 +730,7 @@ __global__ void __launch_bounds__(64) k_customer_ring(
 // the next chunk's wait for its prefetched amounts had to assume the stores were skipped and
 // waited for them too (vmcnt counts stores).  Needs the outputs within 2^31 bytes (the host picks).
 typedef unsigned int fdx_u32x2 __attribute__((ext_vector_type(2)));
-template <int S_MAX, int kRing, int P, bool BUF>
+template <int S_MAX, int kRing, int P, bool BUF, int kChunk = fdx::kChunk>
 __global__ void __launch_bounds__(64) k_customer_walk(
     const double *__restrict__ iamt, const int64_t *__restrict__ seg_off, const int32_t *__restrict__ sorder,
     const uint32_t *__restrict__ goff, int64_t n_seg, int32_t S, int64_t n_slots, int32_t n_win,
@@ -2030,11 +2036,11 @@ extern "C" int fdx_customer_windows_walk(const double *iamt_d, const int64_t *se
     const bool buf = (int64_t)n_windows * n_slots * 8 < (int64_t)INT32_MAX / 8 * 8;
 #define FDX_WALK(SM, RING, P, STREAM, LO, HI)                                                                 \
     if (buf)                                                                                                  \
-        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, true>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
+        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, true, kWalkChunk>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
                            STREAM, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, \
                            starts_d, LO, HI);                                                                  \
     else                                                                                                      \
-        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, false>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
+        hipLaunchKernelGGL((k_customer_walk<SM, RING, P, false, kWalkChunk>), dim3((unsigned)(n_groups * (P))), dim3(64), 0, \
                            STREAM, iamt_d, seg_off_d, sorder_d, goff_d, n_seg, S, n_slots, n_windows, nb_d, sum_d, \
                            starts_d, LO, HI);                                                                  \
     FDX_LAUNCHED("k_customer_walk")
