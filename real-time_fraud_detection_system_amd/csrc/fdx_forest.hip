@@ -926,6 +926,25 @@ void build_chunks(fdx_forest_s *F) {
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
     F->chunks.clear();
+    if (v.rank) {
+        // rank layouts (every tree fits the budget): packed greedily from the LAST tree, so the
+        // partial chunk is the first launch and the last launch -- the one that scatters proba to
+        // the scoring slots' input rows, one random 8-byte store per row -- walks a full chunk
+        // beside those stores (same contiguous tree ranges in tree order, same float64 sums)
+        for (int32_t u = F->n_trees; u > 0;) {
+            int32_t t = u - 1;
+            while (t > 0 && off[u] - off[t - 1] <= cap_nodes) --t;
+            fdx_forest_s::Chunk c;
+            c.t0 = t;
+            c.t1 = u;
+            c.node_base = off[t];
+            c.nodes = off[u] - off[t];
+            c.in_lds = c.nodes <= cap_nodes;
+            F->chunks.insert(F->chunks.begin(), c);
+            u = t;
+        }
+        return;
+    }
     for (int32_t t = 0; t < F->n_trees;) {
         fdx_forest_s::Chunk c;
         c.t0 = t;
