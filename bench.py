@@ -540,7 +540,7 @@ def main():
             step(True, overlap=False, into=iso_all)
         torch.cuda.synchronize()
     trav_ms = sum(a.elapsed_time(b) for a, b in trav) / max(len(trav), 1)
-    launches = forest.n_chunks
+    launches = forest.traverse_launches(n_local)
     fvar = forest.variant
     # §8(d): K3 = 90 B per transaction (15 features in, proba out), over the traversal time
     achieved = ALG["K3"] * n_local / (trav_ms * 1e-3) / 1e9

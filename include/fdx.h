@@ -440,6 +440,11 @@ int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t 
                        int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
                         void *workspace_d, size_t workspace_bytes, void *stream);
+/* *launches = the tree-walk kernel launches fdx_forest_traverse makes for n rows (with a full
+ * fdx_forest_workspace_size workspace): 1 when every LDS chunk is one walk group and no leaf ids
+ * are asked for (one launch walks the chunks in turn), or for small batches (all chunks at
+ * once); else one per chunk (n_chunks of fdx_forest_info). */
+int fdx_forest_traverse_launches(fdx_forest forest, int64_t n, int32_t with_leaves, int32_t *launches);
 /* Traversal kernel shape (one default per layout):
  *   0 = wide layout (8-byte nodes, float32 rows; any forest, the only one for > 15 features),
  *   1 = rank layout v1, 1,024 threads x 10 trees per lane (the default when the forest fits v1),

@@ -552,6 +552,9 @@ __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv,
 // only ever read by that thread, so no barrier is needed to refill them), and the leaf
 // values of a walk group are loaded while the next group walks (accumulation stays in tree
 // order).  The float64 running sum crosses launches through acc, as in k_forest_chunk.
+// persist > 0 (every chunk one walk group): ONE launch walks chunks 0 .. persist-1 in turn, each
+// block refilling its LDS nodes between chunks; the running sum crosses chunks through acc,
+// written and read back by the same lane (a block owns the same tiles in every chunk).
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // The 15 u32 plane words of row slot r * BLOCK + tid (rank << 16, NaN 0xFFFF0000).  With
 // ds_write_addtid_b32 (address = M0 + offset + 4 * lane; no address VGPR) a store moves 4 B per
@@ -608,7 +611,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const uint8_t *__restrict__ mleft, double *__restrict__ acc, double *__restrict__ proba,
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
     int32_t n_trees, int first, int last, const int32_t *__restrict__ chunk_t,
-    const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n) {
+    const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n, int32_t persist) {
     // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots
     constexpr int kPlaneRows = kRankPlaneRows;
     constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
@@ -633,10 +636,22 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
     const int tid = threadIdx.x;
-    {
+    // persist > 0: this one launch walks chunks [0, persist) in turn (see the chunk loop below)
+    auto chunk_params = [&](int c) {
+        t0 = chunk_t[c];
+        t1 = chunk_t[c + 1];
+        node_base = chunk_base[c];
+        chunk_nodes = (int32_t)(chunk_base[c + 1] - node_base);
+        first = c == 0;
+        last = c + 1 == persist;
+    };
+    if (persist > 0) chunk_params(0);
+    auto fill_nodes = [&]() {
         const uint32_t *nb = nodes + node_base;
+#pragma unroll 1
         for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
-    }
+    };
+    fill_nodes();
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
 #pragma unroll
     for (int r = 0; r < R; ++r) {  // slot 15: the leaf / jump sentinel (v2 needs none)
@@ -674,7 +689,30 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             pacc[r] = first ? 0.0 : acc[okr ? rw : r0];  // (unconditional load: see out_slots)
         }
     };
-    if (base < r1) fetch(base);
+    // fetch with 32-bit byte offsets from the uniform bases (global_load saddr + voffset: no 64-bit
+    // address per lane and array); the one-group loop runs only when every offset fits (r1 * 32 B)
+    auto fetch32 = [&](int64_t b) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t rw = b + r * BLOCK + tid;
+            const uint32_t ro = (uint32_t)(rw < r1 ? rw : r0);
+            const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(zr) + ro * (kRowU16 * 2u));
+            q0[r] = src[0];
+            q1[r] = src[1];
+            if (P16 == 2) {
+                q2[r] = src[2];
+                q3[r] = src[3];
+            }
+            pacc[r] = first ? 0.0 : *reinterpret_cast<const double *>(reinterpret_cast<const char *>(acc) + ro * 8u);
+        }
+    };
+    const bool small = !tv && !leaf_out && r1 * (kRowU16 * 2) <= UINT32_MAX;  // (uniform)
+    if (base < r1) {
+        if (small)
+            fetch32(base);
+        else
+            fetch(base);
+    }
     // A chunk of at most G trees (every chunk of the bench forest: 5-6 trees of ~3.9k nodes per
     // 94 KiB) is ONE walk group per tile, so the group pipeline below never runs and each tile
     // waited for its leaf-value loads (and, last chunk, its output slots) right after its walk.
@@ -684,7 +722,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     auto one_group = [&](auto ntag) {
         constexpr int NT = decltype(ntag)::value;
         double pv[R * NT], ap[R];
-        int64_t rowp[R];
+        uint32_t rowp[R];
         int32_t dstp[R], dst_n[R];
         bool okp[R];
 #pragma unroll
@@ -714,7 +752,9 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int64_t rw = b + r * BLOCK + tid;
-                dst_n[r] = perm_out ? out_perm[rw < r1 ? rw : r1 - 1] : (int32_t)rw;
+                const uint32_t rc = (uint32_t)(rw < r1 ? rw : r1 - 1);  // (32-bit offsets: see fetch32)
+                dst_n[r] = perm_out ? *reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(out_perm) + rc * 4u)
+                                    : (int32_t)rw;
             }
         };
         out_slots(base);
@@ -733,7 +773,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
                 if (last) {
                     if (dstp[r] >= 0) proba[dstp[r]] = ap[r] / (double)n_trees;  // < 0: padding slot
                 } else {
-                    acc[rowp[r]] = ap[r];
+                    *reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + rowp[r] * 8u) = ap[r];
                 }
             }
         };
@@ -744,15 +784,15 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         // load in flight (the next tile's rows right after issuing them, or the leaf gather just
         // issued), once per tile (r04 ISA: ~100 us per launch).  The wait before the staging
         // leaves the leaf loads in flight (in-order vmcnt: they are younger).
-        int64_t row[R];
+        uint32_t row[R];
         bool ok[R];
         double a[R];
         int32_t dst[R];
         auto stage_tile = [&]() {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                row[r] = base + r * BLOCK + tid;
-                ok[r] = row[r] < r1;
+                row[r] = (uint32_t)(base + r * BLOCK + tid);
+                ok[r] = row[r] < (uint32_t)r1;
                 if constexpr (P16 == 2) {
                     const uint32_t w16[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                               q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
@@ -777,7 +817,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         while (base < r1) {
             // unconditional (fetch clamps rows past r1 to r0): a conditional load left its
             // registers to be merged at a join, behind a vmcnt(0) right after the loads
-            fetch(base + stride);
+            fetch32(base + stride);
             out_slots(base + stride);
             uint32_t pt[R * NT];
             // the previous tile's step count, less one exit interval, runs without exit tests
@@ -802,20 +842,33 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         fold();
     };
     // (9+ trees: register spills)
-    if (!tv && !leaf_out && t1 - t0 <= (G < 8 ? G : 8) && r1 <= INT32_MAX) {
+    if (small && (persist > 0 || t1 - t0 <= (G < 8 ? G : 8))) {
+        // Chunk loop (persist > 0; the host checks that every chunk is one group): a block walks
+        // the same tiles (blockIdx.x + k * gridDim.x) in every chunk, so a row's running sum is
+        // only ever handed between chunks by the lane that holds it -- no grid-wide sync between
+        // chunks, only the block's own barrier around the node refill.
+        for (int c = 0;;) {
 #define FDX_ONE_GROUP(NT) \
     if constexpr (G >= NT) \
         if (t1 - t0 == NT) one_group(std::integral_constant<int, NT>{});
-        FDX_ONE_GROUP(1)
-        FDX_ONE_GROUP(2)
-        FDX_ONE_GROUP(3)
-        FDX_ONE_GROUP(4)
-        FDX_ONE_GROUP(5)
-        FDX_ONE_GROUP(6)
-        FDX_ONE_GROUP(7)
-        FDX_ONE_GROUP(8)
+            FDX_ONE_GROUP(1)
+            FDX_ONE_GROUP(2)
+            FDX_ONE_GROUP(3)
+            FDX_ONE_GROUP(4)
+            FDX_ONE_GROUP(5)
+            FDX_ONE_GROUP(6)
+            FDX_ONE_GROUP(7)
+            FDX_ONE_GROUP(8)
 #undef FDX_ONE_GROUP
-        return;
+            if (++c >= persist) return;
+            chunk_params(c);
+            ml = mleft + node_base;
+            base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
+            if (base < r1) fetch32(base);  // (this lane stored these rows' running sums itself)
+            __syncthreads();  // every wave is done with the previous chunk's nodes
+            fill_nodes();
+            __syncthreads();
+        }
     }
     // the generic tile loop (leaf ids, per-tree values, chunks of more trees than one group):
     // two rows per lane walk groups of 3 trees (6 chains) to stay within the register budget
@@ -1327,6 +1380,29 @@ int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, dou
 
 }  // namespace fdx
 
+// One k_forest_rank launch for every chunk (its chunk loop) when each chunk is one walk group:
+// 10.16 vs 10.28 ms/step at configs[1], the 18 launches' drain and ramp gone
+// (profiles/r05ba_one_launch_ab.txt)
+static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
+    const int64_t row_bytes = kVariants[F->variant].p16 == 2 ? 64 : 32;  // (the kernel's 32-bit offsets)
+    bool ok = rank_mode(F) && !leaves && F->chunks.size() > 1 && n * row_bytes <= (int64_t)UINT32_MAX;
+    for (const auto &ch : F->chunks) ok = ok && ch.t1 - ch.t0 <= std::min(8, kVariants[F->variant].group);
+    return ok;
+}
+
+extern "C" int fdx_forest_traverse_launches(fdx_forest F, int64_t n, int32_t with_leaves, int32_t *launches) {
+    FDX_REQUIRE(F && launches, "null pointer");
+    FDX_REQUIRE(n >= 0, "n < 0");
+    const int64_t nc = (int64_t)F->chunks.size();
+    if (n == 0)
+        *launches = 0;
+    else if (rank_mode(F) && nc > 1 && n <= concurrent_rows(F))
+        *launches = 1;  // all chunks at once (grid.y = chunk), + k_tree_sum
+    else
+        *launches = one_launch_ok(F, n, with_leaves != 0) ? 1 : (int32_t)nc;
+    return FDX_OK;
+}
+
 static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32_t *out_perm_d,
                            int32_t *leaf_d, void *ws, size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
@@ -1346,7 +1422,9 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         double *tv = nullptr;
         if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n))
             tv = reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + align_up(sizeof(double) * (size_t)n) + 256);
-        for (size_t c = 0; c < (tv ? 1 : nc); ++c) {
+        const bool one_launch = !tv && one_launch_ok(F, n, leaf_d != nullptr);
+        const int32_t persist = one_launch ? (int32_t)nc : 0;
+        for (size_t c = 0; c < (tv || one_launch ? 1 : nc); ++c) {
             const auto &ch = F->chunks[c];
             const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_RANK(B, R, G, P, PIPE)                                                                      \
@@ -1356,7 +1434,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,    \
                            (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, (int64_t)0, n,       \
                            F->rlval_d, F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first,  \
-                           last, F->chunk_t_d, F->chunk_base_d, tv, n);                                           \
+                           last, F->chunk_t_d, F->chunk_base_d, tv, n, persist);                                  \
     } while (0)
             switch (F->variant) {
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;

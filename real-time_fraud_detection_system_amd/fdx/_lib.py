@@ -141,6 +141,7 @@ SIGNATURES = {
     "fdx_synth_plan": (ctypes.c_int, [ctypes.POINTER(SynthDesc), P, c_sz, P, P]),
     "fdx_synth_fill": (ctypes.c_int, [ctypes.POINTER(SynthDesc), c_i64, P, c_sz, P, P, P, P, P, P, P, P]),
     "fdx_forest_info": (ctypes.c_int, [P, P, P, P, P]),
+    "fdx_forest_traverse_launches": (ctypes.c_int, [P, ctypes.c_int64, ctypes.c_int32, P]),
     "fdx_forest_workspace_size": (c_sz, [P, c_i64]),
     "fdx_forest_workspace_size_max": (ctypes.c_size_t, [P, c_i64]),
     "fdx_forest_predict": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, P, P, c_sz, P]),

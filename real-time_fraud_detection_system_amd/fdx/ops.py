@@ -626,6 +626,13 @@ class Forest:
         self.n_chunks = nc.value
         self.variant = int(variant)
 
+    def traverse_launches(self, n: int, want_leaves: bool = False) -> int:
+        """tree-walk kernel launches of one traversal of n rows (fdx_forest_traverse_launches)"""
+        k = ctypes.c_int32()
+        check(_lib.load().fdx_forest_traverse_launches(self._h, int(n), int(bool(want_leaves)), ctypes.byref(k)),
+              "fdx_forest_traverse_launches")
+        return k.value
+
     def workspace_size(self, n: int) -> int:
         return int(_lib.load().fdx_forest_workspace_size(self._h, int(n)))
 

@@ -99,6 +99,35 @@ def test_one_group_bench_model(dev):
     np.testing.assert_array_equal(pc, np.concatenate([z["check_proba"]] * 64))
 
 
+def test_one_launch_chunk_loop(dev):
+    """Every chunk of the bench forest is one walk group, so a large batch walks all 18 chunks in
+    ONE k_forest_rank launch (the kernel's chunk loop, running sums handed between chunks by the
+    lane that owns the row); with leaf ids it is one launch per chunk, and a small batch runs every
+    chunk at once.  All three give the same probabilities, bit for bit, and the leaf ids are the
+    oracle's."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arr = _arrays(z)
+    f = ops.Forest(arr, 15, z["mean"], z["scale"])
+    n = 300_017  # > 256 CUs x 1,024 rows: past the all-chunks-at-once size
+    assert f.n_chunks == 18
+    assert f.traverse_launches(n) == 1
+    assert f.traverse_launches(n, want_leaves=True) == f.n_chunks
+    assert f.traverse_launches(1000) == 1 and f.traverse_launches(0) == 0
+    rng = np.random.default_rng(11)
+    X = np.vstack([z["check_X"]] * (n // len(z["check_X"]) + 1))[:n]
+    X = X * (1 + rng.normal(scale=0.05, size=X.shape) * (rng.random(X.shape) < 0.5))
+    Xd = T(X, torch.float64, dev)
+    p1 = f.predict(Xd).cpu().numpy()
+    pl, leaves = f.predict(Xd, want_leaves=True)
+    np.testing.assert_array_equal(p1, pl.cpu().numpy())
+    ps = f.predict(Xd[:1000]).cpu().numpy()
+    np.testing.assert_array_equal(ps, p1[:1000])
+    sel = rng.choice(n, 5_000, replace=False)
+    np.testing.assert_array_equal(p1[sel], oracle.forest_predict(X[sel], arr, z["mean"], z["scale"]))
+    _, want_leaves = oracle.forest_predict(X[sel[:200]], arr, z["mean"], z["scale"], want_leaves=True)
+    np.testing.assert_array_equal(leaves.cpu().numpy()[sel[:200]], want_leaves)
+
+
 def test_refused_variant_leaves_the_forest_intact(dev):
     """a refused set_variant must leave the forest as it was.  The deployed model
     (rank layout v2, 22 threshold slots) cannot run v1 (a feature has 96k thresholds: the v1
