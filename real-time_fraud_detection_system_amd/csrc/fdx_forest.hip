@@ -1389,6 +1389,13 @@ static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
     for (const auto &ch : F->chunks) ok = ok && ch.t1 - ch.t0 <= std::min(8, kVariants[F->variant].group);
     return ok;
 }
+// Rows per k_forest_rank row range: the one-group tile loop addresses rank rows, running sums and
+// output slots by 32-bit byte offsets, so a larger batch is walked range by range (128M rows at
+// 32-B rank rows), each launch over base pointers moved to its range.
+static int64_t rank_range_rows(const fdx_forest_s *F) {
+    const int64_t row_bytes = kVariants[F->variant].p16 == 2 ? 64 : 32;
+    return ((int64_t)UINT32_MAX / row_bytes) & ~(int64_t)1023;
+}
 
 extern "C" int fdx_forest_traverse_launches(fdx_forest F, int64_t n, int32_t with_leaves, int32_t *launches) {
     FDX_REQUIRE(F && launches, "null pointer");
@@ -1398,8 +1405,13 @@ extern "C" int fdx_forest_traverse_launches(fdx_forest F, int64_t n, int32_t wit
         *launches = 0;
     else if (rank_mode(F) && nc > 1 && n <= concurrent_rows(F))
         *launches = 1;  // all chunks at once (grid.y = chunk), + k_tree_sum
-    else
-        *launches = one_launch_ok(F, n, with_leaves != 0) ? 1 : (int32_t)nc;
+    else if (!rank_mode(F))
+        *launches = (int32_t)nc;
+    else {
+        const int64_t rr = rank_range_rows(F), ranges = ceil_div(n, rr);
+        *launches = (int32_t)((ranges - 1) * (one_launch_ok(F, rr, with_leaves != 0) ? 1 : nc) +
+                              (one_launch_ok(F, n - (ranges - 1) * rr, with_leaves != 0) ? 1 : nc));
+    }
     return FDX_OK;
 }
 
@@ -1422,18 +1434,28 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         double *tv = nullptr;
         if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n))
             tv = reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + align_up(sizeof(double) * (size_t)n) + 256);
-        const bool one_launch = !tv && one_launch_ok(F, n, leaf_d != nullptr);
+        const int64_t rr = tv ? n : rank_range_rows(F);
+        const int64_t row_u16 = kVariants[F->variant].p16 == 2 ? 32 : 16;
+        for (int64_t q0 = 0; q0 < n; q0 += rr) {  // row ranges (one unless n > rank_range_rows)
+        const int64_t qn = std::min(rr, n - q0);
+        const uint16_t *zq = zr + q0 * row_u16;
+        double *accq = acc + q0;
+        // output slots: through out_perm (absolute) or at the row (moved with the range)
+        double *probaq = out_perm_d ? proba_d : proba_d + q0;
+        const int32_t *permq = out_perm_d ? out_perm_d + q0 : nullptr;
+        int32_t *leafq = leaf_d ? (out_perm_d ? leaf_d : leaf_d + q0 * F->n_trees) : nullptr;
+        const bool one_launch = !tv && one_launch_ok(F, qn, leaf_d != nullptr);
         const int32_t persist = one_launch ? (int32_t)nc : 0;
         for (size_t c = 0; c < (tv || one_launch ? 1 : nc); ++c) {
             const auto &ch = F->chunks[c];
             const int first = c == 0, last = c + 1 == nc;
 #define FDX_LAUNCH_RANK(B, R, G, P, PIPE)                                                                      \
     do {                                                                                                      \
-        const int64_t tiles_ = ceil_div(n, (int64_t)(B) * (R));                                               \
+        const int64_t tiles_ = ceil_div(qn, (int64_t)(B) * (R));                                              \
         const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu), tv ? (unsigned)nc : 1u); \
         hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,    \
-                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zr, flag, (int64_t)0, n,       \
-                           F->rlval_d, F->rml_d, acc, proba_d, out_perm_d, leaf_d, F->rorig_d, F->n_trees, first,  \
+                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag, (int64_t)0, qn,      \
+                           F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d, F->n_trees, first,        \
                            last, F->chunk_t_d, F->chunk_base_d, tv, n, persist);                                  \
     } while (0)
             switch (F->variant) {
@@ -1444,6 +1466,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             }
 #undef FDX_LAUNCH_RANK
             FDX_LAUNCHED("k_forest_rank");
+        }
         }
         if (tv) {
             hipLaunchKernelGGL(k_tree_sum, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, st, tv, n, F->n_trees,

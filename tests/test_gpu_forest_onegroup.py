@@ -128,6 +128,38 @@ def test_one_launch_chunk_loop(dev):
     np.testing.assert_array_equal(leaves.cpu().numpy()[sel[:200]], want_leaves)
 
 
+def test_row_ranges_past_32_bit_offsets(dev):
+    """A batch larger than one 32-bit-addressable row range (134,216,704 rows of 32-B rank rows:
+    the one-group tile loop's byte offsets) is walked range by range, each launch over base
+    pointers moved to its range.  Rows on both sides of the boundary == the oracle; with the
+    output permutation (absolute output slots) every row lands where the plain traversal puts it."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arr = _arrays(z)
+    f = ops.Forest(arr, 15, z["mean"], z["scale"])
+    rr = 134_216_704
+    n = rr + 3001
+    assert f.traverse_launches(n) == 2 and f.traverse_launches(rr) == 1
+    chk = T(z["check_X"], torch.float64, dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(21)
+    pick = torch.randint(0, chk.shape[0], (n,), device=dev, generator=g)
+    Xd = chk[pick]
+    del pick
+    p = f.predict(Xd)
+    rng = np.random.default_rng(21)
+    idx = np.concatenate([np.arange(rr - 2000, n), rng.choice(rr - 2000, 3000, replace=False)])
+    X = Xd[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    np.testing.assert_array_equal(p[torch.from_numpy(idx).to(dev)].cpu().numpy(),
+                                  oracle.forest_predict(X, arr, z["mean"], z["scale"]))
+    ws = torch.empty(f.workspace_size(n), dtype=torch.uint8, device=dev)
+    ops.forest_prepare(f, Xd, ws)
+    del Xd
+    perm = torch.randperm(n, device=dev, generator=g).to(torch.int32)
+    out = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+    ops.forest_traverse_perm(f, n, ws, out, perm)
+    assert torch.equal(out[perm.long()], p)
+
+
 def test_refused_variant_leaves_the_forest_intact(dev):
     """a refused set_variant must leave the forest as it was.  The deployed model
     (rank layout v2, 22 threshold slots) cannot run v1 (a feature has 96k thresholds: the v1
