@@ -160,6 +160,32 @@ def test_row_ranges_past_32_bit_offsets(dev):
     assert torch.equal(out[perm.long()], p)
 
 
+def test_prepare_row_major_spans(dev):
+    """fdx_forest_prepare of dense row-major X stages each wave's 64 rows as one contiguous span
+    (k_prepare_rows): a ragged last span, NaN rows, an X that starts 8 bytes off a 16-byte
+    boundary (a view from row 1) and a padded row stride (the per-lane kernel) all give the
+    oracle's probabilities."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arr = _arrays(z)
+    f = ops.Forest(arr, 15, z["mean"], z["scale"])
+    rng = np.random.default_rng(31)
+    n = 64 * 4099 + 37
+    X = np.vstack([z["check_X"]] * (n // len(z["check_X"]) + 2))[:n + 1]
+    X = X * (1 + rng.normal(scale=0.05, size=X.shape) * (rng.random(X.shape) < 0.5))
+    X[rng.random(X.shape) < 0.002] = np.nan
+    sel = np.concatenate([np.arange(0, 200), np.arange(n - 200, n), rng.choice(n, 3000, replace=False)])
+    want = oracle.forest_predict(X[1:][sel], arr, z["mean"], z["scale"])
+    Xall = T(X, torch.float64, dev)
+    p_view = f.predict(Xall[1:]).cpu().numpy()  # 120 B past the allocation: 8-B aligned
+    p_dense = f.predict(Xall[1:].contiguous()).cpu().numpy()
+    pad = torch.zeros((n, 16), dtype=torch.float64, device=dev)
+    pad[:, :15] = Xall[1:]
+    p_pad = f.predict(pad[:, :15]).cpu().numpy()
+    np.testing.assert_array_equal(p_dense[sel], want)
+    np.testing.assert_array_equal(p_view, p_dense)
+    np.testing.assert_array_equal(p_pad, p_dense)
+
+
 def test_refused_variant_leaves_the_forest_intact(dev):
     """a refused set_variant must leave the forest as it was.  The deployed model
     (rank layout v2, 22 threshold slots) cannot run v1 (a feature has 96k thresholds: the v1
