@@ -62,10 +62,20 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
             if (c > 0) {
                 const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
                 uint32_t k = 0;
-                for (int q = 0; q < rt.seg / 4; ++q) {
-                    const float4 w = sg[q];
-                    k += (uint32_t)(w.x < v[f]) + (uint32_t)(w.y < v[f]) + (uint32_t)(w.z < v[f]) +
-                         (uint32_t)(w.w < v[f]);
+                if (rt.seg == 16) {  // (uniform) the segment's 4 loads in flight together: one round trip
+                    float4 w[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w[q] = sg[q];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        k += (uint32_t)(w[q].x < v[f]) + (uint32_t)(w[q].y < v[f]) + (uint32_t)(w[q].z < v[f]) +
+                             (uint32_t)(w[q].w < v[f]);
+                } else {
+                    for (int q = 0; q < rt.seg / 4; ++q) {
+                        const float4 w = sg[q];
+                        k += (uint32_t)(w.x < v[f]) + (uint32_t)(w.y < v[f]) + (uint32_t)(w.z < v[f]) +
+                             (uint32_t)(w.w < v[f]);
+                    }
                 }
                 r = (uint32_t)(c - 1) * (uint32_t)rt.seg + k;
             }
