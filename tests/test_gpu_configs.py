@@ -91,6 +91,25 @@ def test_config2_full_size_fused_path_every_row(dev):
     np.testing.assert_array_equal(p64[sel], oracle.forest_predict(X[sel], arrays, z["mean"], z["scale"]))
 
 
+def test_fused_path_past_one_forest_row_range(dev):
+    """A fused step whose scoring slots exceed one forest row range (134,216,704 slots: the walk's
+    32-bit offsets; a configs[3] rank at N = 2 or 4 holds 177M-354M transactions): the traversal
+    runs range by range with proba scattered through the layout's irow, and every row's proba
+    equals the float64 path's (featurize + score) on the same data."""
+    arrays, z = _model()
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    g = synth.generate_device(400_000, 800_000, 183, seed=4242, device=dev)
+    args = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"])
+    n = args[0].numel()
+    pipe = FraudPipeline(forest=forest)
+    proba = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 400_000, 800_000, proba)
+    assert pipe.last_slots > 134_216_704
+    assert forest.traverse_launches(pipe.last_slots) == 2
+    p64 = pipe.score(pipe.featurize(*args, 400_000, 800_000).X)
+    assert torch.equal(proba, p64)
+
+
 def test_config3_rf100_d20_bench_model(dev):
     arrays, z = _model()
     forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
