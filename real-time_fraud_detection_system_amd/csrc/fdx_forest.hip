@@ -981,9 +981,10 @@ void build_chunks(fdx_forest_s *F) {
     F->chunks.clear();
     if (v.rank) {
         // rank layouts (every tree fits the budget): packed greedily from the LAST tree, so the
-        // partial chunk is the first launch and the last launch -- the one that scatters proba to
-        // the scoring slots' input rows, one random 8-byte store per row -- walks a full chunk
-        // beside those stores (same contiguous tree ranges in tree order, same float64 sums)
+        // partial chunk is walked first and the last chunk -- the one that scatters proba to the
+        // scoring slots' input rows, one random 8-byte store per row -- is a full one beside those
+        // stores (same contiguous tree ranges in tree order, same float64 sums; measured with one
+        // launch per chunk, profiles/r05ax_chunk_pack_ab.txt)
         for (int32_t u = F->n_trees; u > 0;) {
             int32_t t = u - 1;
             while (t > 0 && off[u] - off[t - 1] <= cap_nodes) --t;
