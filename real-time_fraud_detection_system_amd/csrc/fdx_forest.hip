@@ -603,7 +603,10 @@ __device__ __forceinline__ void stage_planes_u32(uint32_t *s_x, int r, const uin
     stage_words<BLOCK>(s_x, r, x);
 }
 
-template <int BLOCK, int R, int G, int P16, int PIPE>
+// CL: the chunk loop (persist > 0) -- its own instantiation, so that the loop's register pressure
+// stays out of the generic tile loop (small batches, leaf ids): one kernel holding both spilled
+// in the generic loop (stream micro-batches 0.157 -> 0.167 ms on the device, r05bk)
+template <int BLOCK, int R, int G, int P16, int PIPE, bool CL>
 __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const uint32_t *__restrict__ nodes, int64_t node_base, int32_t chunk_nodes, const int32_t *__restrict__ root,
     const int32_t *__restrict__ depth, int32_t t0, int32_t t1, const uint16_t *__restrict__ zr,
@@ -648,8 +651,13 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     if (persist > 0) chunk_params(0);
     auto fill_nodes = [&]() {
         const uint32_t *nb = nodes + node_base;
+        if constexpr (CL) {  // (rolled: the chunk loop's registers are tight)
 #pragma unroll 1
-        for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+        } else {  // several loads in flight: with one tile per block (small batches) the fill is a
+                  // large share of a block's work (rolled: stream micro-batches +8 us, r05bp)
+            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+        }
     };
     fill_nodes();
     uint16_t *s_x16 = reinterpret_cast<uint16_t *>(s_mem);
@@ -842,24 +850,27 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         fold();
     };
     // (9+ trees: register spills)
-    if (small && (persist > 0 || t1 - t0 <= (G < 8 ? G : 8))) {
-        // Chunk loop (persist > 0; the host checks that every chunk is one group): a block walks
-        // the same tiles (blockIdx.x + k * gridDim.x) in every chunk, so a row's running sum is
-        // only ever handed between chunks by the lane that holds it -- no grid-wide sync between
-        // chunks, only the block's own barrier around the node refill.
-        for (int c = 0;;) {
+    auto one_chunk = [&]() {
 #define FDX_ONE_GROUP(NT) \
     if constexpr (G >= NT) \
         if (t1 - t0 == NT) one_group(std::integral_constant<int, NT>{});
-            FDX_ONE_GROUP(1)
-            FDX_ONE_GROUP(2)
-            FDX_ONE_GROUP(3)
-            FDX_ONE_GROUP(4)
-            FDX_ONE_GROUP(5)
-            FDX_ONE_GROUP(6)
-            FDX_ONE_GROUP(7)
-            FDX_ONE_GROUP(8)
+        FDX_ONE_GROUP(1)
+        FDX_ONE_GROUP(2)
+        FDX_ONE_GROUP(3)
+        FDX_ONE_GROUP(4)
+        FDX_ONE_GROUP(5)
+        FDX_ONE_GROUP(6)
+        FDX_ONE_GROUP(7)
+        FDX_ONE_GROUP(8)
 #undef FDX_ONE_GROUP
+    };
+    if constexpr (CL) {
+        // Chunk loop (persist > 0, small; the host checks that every chunk is one group): a block
+        // walks the same tiles (blockIdx.x + k * gridDim.x) in every chunk, so a row's running sum
+        // is only ever handed between chunks by the lane that holds it -- no grid-wide sync
+        // between chunks, only the block's own barrier around the node refill.
+        for (int c = 0;;) {
+            one_chunk();
             if (++c >= persist) return;
             chunk_params(c);
             ml = mleft + node_base;
@@ -869,6 +880,9 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             fill_nodes();
             __syncthreads();
         }
+    } else if (small && t1 - t0 <= (G < 8 ? G : 8)) {
+        one_chunk();
+        return;
     }
     // the generic tile loop (leaf ids, per-tree values, chunks of more trees than one group):
     // two rows per lane walk groups of 3 trees (6 chains) to stay within the register budget
@@ -1454,10 +1468,16 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
     do {                                                                                                      \
         const int64_t tiles_ = ceil_div(qn, (int64_t)(B) * (R));                                              \
         const dim3 grid(tv ? (unsigned)tiles_ : (unsigned)std::min<int64_t>(tiles_, F->n_cu), tv ? (unsigned)nc : 1u); \
-        hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE>), grid, dim3(B), 0, st, F->rnodes_d, ch.node_base,    \
-                           (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag, (int64_t)0, qn,      \
-                           F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d, F->n_trees, first,        \
-                           last, F->chunk_t_d, F->chunk_base_d, tv, n, persist);                                  \
+        if (persist)                                                                                          \
+            hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, true>), grid, dim3(B), 0, st, F->rnodes_d,      \
+                               ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag,  \
+                               (int64_t)0, qn, F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d,     \
+                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, persist);          \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, false>), grid, dim3(B), 0, st, F->rnodes_d,     \
+                               ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag,  \
+                               (int64_t)0, qn, F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d,     \
+                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, 0);                \
     } while (0)
             switch (F->variant) {
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;

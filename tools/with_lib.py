@@ -11,5 +11,8 @@ sys.path.insert(0, ROOT)
 from fdx import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.abspath(sys.argv[1])
+_probe = __import__("ctypes").CDLL(_lib.LIB_PATH)
+for _name in [k for k in _lib.SIGNATURES if not hasattr(_probe, k)]:  # an older build: symbols it lacks
+    del _lib.SIGNATURES[_name]
 sys.argv = sys.argv[2:]
 runpy.run_path(sys.argv[0], run_name="__main__")
