@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "real-time_fraud_detection_system_amd", "csrc")
-KERNEL = "k_forest_rankILi1024ELi1ELi10ELi0ELi102E"
+KERNEL = "k_forest_rankILi1024ELi1ELi10ELi0ELi102ELb1E"  # the chunk-loop instantiation (large batches)
 
 
 def kernel_body(asm):
@@ -67,7 +67,7 @@ def main():
                            os.path.join(CSRC, "fdx_forest.hip")])
     asm = open(asm_path).read()
     body, summ = kernel_body(asm)
-    res = [f"k_forest_rank<1024, 1, 10, 0, 102> (default variant 1), gfx950, hipcc -O3", "register summary:"]
+    res = [f"k_forest_rank<1024, 1, 10, 0, 102, true> (default variant 1, chunk loop), gfx950, hipcc -O3", "register summary:"]
     res += ["  " + s for s in summ]
     res.append("")
     res.append("walk blocks (one v_med3_i32 per chain-step): per chain-step instruction counts")
