@@ -99,14 +99,16 @@ def walk_steps_per_row(arrays):
 
 
 def pmc_counters(name_part):
-    """The committed SQ counters of the first kernel whose name contains name_part, per
-    dispatch (profiles/pmc_kernels.json), or {}."""
+    """The committed SQ counters, per dispatch (profiles/pmc_kernels.json), of the busiest kernel
+    whose name contains name_part (the most wave-cycles: e.g. the forest's chunk-loop
+    instantiation, not the per-chunk one a small check batch runs), or {}."""
     p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     if not os.path.exists(p):
         return {}
     with open(p) as f:
         d = json.load(f)
-    return next((v for k, v in d["kernels"].items() if name_part in k), {})
+    hits = [v for k, v in d["kernels"].items() if name_part in k]
+    return max(hits, key=lambda v: v.get("SQ_WAVE_CYCLES", 0.0)) if hits else {}
 
 
 def pmc_table():
