@@ -128,6 +128,33 @@ def test_one_launch_chunk_loop(dev):
     np.testing.assert_array_equal(leaves.cpu().numpy()[sel[:200]], want_leaves)
 
 
+@pytest.mark.parametrize("variant", [0] + VARIANTS)
+def test_traverse_launch_count(dev, variant):
+    """fdx_forest_traverse_launches per layout: the wide layout launches once per chunk; a rank
+    layout walks every chunk in one launch when each is one walk group (else one per chunk), per
+    32-bit row range (128M rows of 32-B rank rows, 64M of 64-B v2 rows); one per chunk with leaf
+    ids; small batches run every chunk at once.  20 trees of depth 12: several chunks."""
+    rng = np.random.default_rng(77)
+    arr = random_forest(rng, 20, 12, p_leaf=0.05)
+    f = ops.Forest(arr, 15)
+    if not _set(f, variant):
+        pytest.skip("node format does not hold this forest")
+    nc = f.n_chunks
+    assert nc > 1
+    big = 3_000_000
+    assert f.traverse_launches(0) == 0
+    if variant == 0:
+        assert f.traverse_launches(big) == nc
+        return
+    k = f.traverse_launches(big)
+    assert k in (1, nc)
+    rows = (2**32 - 1) // (64 if variant in (2, 4) else 32) // 1024 * 1024
+    assert f.traverse_launches(rows) == k
+    assert f.traverse_launches(rows + 1) == 2 * k
+    assert f.traverse_launches(big, want_leaves=True) == nc
+    assert f.traverse_launches(1000) == 1
+
+
 def test_row_ranges_past_32_bit_offsets(dev):
     """A batch larger than one 32-bit-addressable row range (134,216,704 rows of 32-B rank rows:
     the one-group tile loop's byte offsets) is walked range by range, each launch over base
