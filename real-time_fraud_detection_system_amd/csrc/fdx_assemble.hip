@@ -515,6 +515,80 @@ constexpr int kW3Block = 1024;
 // (each pair took an s_nop for the VCC hazard: 8 per S-tree level, r05 ISA)
 __device__ __forceinline__ uint32_t lt_bit(float a, float x) { return __float_as_uint(a - x) >> 31; }
 
+// k_prepare<16, true> with the four kW3Search features ranked by their S-trees (the descent of
+// k_zfill_grouped_w3 below) instead of the binary search over every 16th threshold: those four
+// hold 17k-20k thresholds each in the bench model (11 dependent search rounds; 2.1 of the 9.4 ms
+// of configs[2]'s prepare, profiles/r05be_prepare_ab.txt), the S-tree takes 4 levels.  The other
+// features keep rank_row's search.  1,024-thread blocks: the S-trees (<= 112 KiB) + the samples
+// (32 KiB) in LDS.  Same ranks as k_prepare bit for bit (same thresholds, same compares).
+constexpr int kPrepStBlock = 1024;
+__global__ void __launch_bounds__(kPrepStBlock) k_prepare_st(const double *__restrict__ X, int64_t n, int64_t rs,
+                                                              int64_t cs, int32_t nf, const double *__restrict__ mean,
+                                                              const double *__restrict__ scale, void *__restrict__ z,
+                                                              int32_t *__restrict__ nan_flag, RankTab rt) {
+    __shared__ float s_smp[kMaxRankSamples];
+    __shared__ __align__(16) float s_t[kW3TreeFloats];
+    for (int e = threadIdx.x; e < rt.n_etab / 4; e += blockDim.x)
+        reinterpret_cast<float4 *>(s_t)[e] = reinterpret_cast<const float4 *>(rt.etab)[e];
+    stage_samples(s_smp, rt);  // (its barrier covers the S-trees too)
+    const int e_lmax = max(max(rt.elev[0], rt.elev[1]), max(rt.elev[2], rt.elev[3]));
+    uint32_t others = (1u << nf) - 1u;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) others &= ~(1u << kW3Search[s]);
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        float v[16];
+        bool nan = false;
+#pragma unroll
+        for (int f = 0; f < 16; ++f) {
+            if (f < nf) {
+                double x = X[r * rs + (int64_t)f * cs];
+                if (mean) x = x - mean[f];
+                if (scale) x = x / scale[f];
+                v[f] = (float)x;
+                nan |= x != x;
+            } else {
+                v[f] = 0.0f;
+            }
+        }
+        if (nan) *nan_flag = 1;
+        uint32_t q[16];
+#pragma unroll
+        for (int f = 0; f < 16; ++f) q[f] = 0u;
+        rank_row(v, nf, rt, s_smp, q, others);
+        int32_t ek[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+        for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (l < rt.elev[s]) {
+                    const float4 *nd = reinterpret_cast<const float4 *>(s_t) + 2 * (rt.eoff[s] + ek[s]);
+                    const float4 a = nd[0], b = nd[1];
+                    const float x = v[kW3Search[s]];
+                    const int32_t c = (int32_t)(lt_bit(a.x, x) + lt_bit(a.y, x) + lt_bit(a.z, x) + lt_bit(a.w, x) +
+                                                lt_bit(b.x, x) + lt_bit(b.y, x) + lt_bit(b.z, x) + lt_bit(b.w, x));
+                    cnt[s] = cnt[s] * 9 + c;
+                    ek[s] = ek[s] * 9 + 1 + c;
+                }
+            }
+        }
+        float4 sg[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)  // (unconditional: the host pads useg by one segment)
+            sg[s] = *reinterpret_cast<const float4 *>(rt.useg + rt.uoff[kW3Search[s]] +
+                                                      (int64_t)max(cnt[s] - 1, 0) * kW3Gap);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int f = kW3Search[s];
+            const float x = v[f];
+            const uint32_t kc = lt_bit(sg[s].x, x) + lt_bit(sg[s].y, x) + lt_bit(sg[s].z, x) + lt_bit(sg[s].w, x);
+            const uint32_t rk = cnt[s] > 0 ? (uint32_t)(cnt[s] - 1) * kW3Gap + kc : 0u;
+            q[f] = x != x ? 0xFFFFu : rk;
+        }
+        uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + r * 16);
+        dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
+        dst[1] = make_uint4(q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16);
+    }
+}
+
 struct PrepRow {
     int64_t t;
     double a;
@@ -946,6 +1020,14 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
         hipLaunchKernelGGL(k_prepare_v2, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride, F->n_features,
                            F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
         FDX_LAUNCHED("k_prepare_v2");
+        return FDX_OK;
+    }
+    if (rank_mode(F) && F->rnetab > 0 && F->n_features == 15) {  // the S-trees of the four searched features
+        const RankTab rt = rank_tab(F);
+        const unsigned g = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kPrepStBlock), (int64_t)F->n_cu * 2);
+        hipLaunchKernelGGL(k_prepare_st, dim3(g), dim3(kPrepStBlock), 0, st, X_d, n, row_stride, col_stride,
+                           F->n_features, F->mean_d, F->scale_d, (void *)z, flag, rt);
+        FDX_LAUNCHED("k_prepare_st");
         return FDX_OK;
     }
     FDX_PREP(k_prepare, dim3(grid), st, X_d, n, row_stride, col_stride, F->n_features, F->mean_d, F->scale_d,
