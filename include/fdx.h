@@ -435,7 +435,8 @@ int fdx_forest_predict(fdx_forest forest, const double *X_d, int64_t n, int64_t 
 
 /* The two halves of fdx_forest_predict, for callers that time or overlap them:
  * prepare = scale + float32 cast (+ threshold ranks) into the workspace; traverse = the tree
- * walk (one launch per LDS-sized chunk of trees) reading that workspace. */
+ * walk over the LDS-sized chunks of trees (one launch for all of them when each chunk is one walk
+ * group, see fdx_forest_traverse_launches) reading that workspace. */
 int fdx_forest_prepare(fdx_forest forest, const double *X_d, int64_t n, int64_t row_stride,
                        int64_t col_stride, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_traverse(fdx_forest forest, int64_t n, double *proba_d, int32_t *leaf_d,
