@@ -189,6 +189,26 @@ def plan_workload(world, rank, workload="auto", customers=None, terminals=None, 
             "n_customers_total": C, "n_terminals_total": T, "days": D}
 
 
+SCALE_REF = os.path.join(ROOT, "profiles", "configs3_n1.json")
+
+
+def scale_reference(wl):
+    """The N = 1 measurement of the configs[3] table (profiles/configs3_n1.json: the JSON line of
+    `bench.py --gpus 1 --workload configs3`), or why there is none."""
+    ref = {"n_gpus": 1, "workload": "configs3", "source": os.path.relpath(SCALE_REF, ROOT)}
+    if wl["name"] != "configs3":
+        return dict(ref, value=None, note="this line is not the configs[3] table")
+    try:
+        with open(SCALE_REF) as f:
+            line = json.load(f)
+    except (OSError, ValueError):
+        return dict(ref, value=None, note="no committed N = 1 line")
+    same = line.get("config", {}).get("global_tx")
+    ref.update(value=line.get("value"), ms_per_step=line.get("ms_per_step"), global_tx=same,
+               error=line.get("error"))
+    return ref
+
+
 def median(v):
     v = sorted(v)
     m = len(v) // 2
@@ -409,6 +429,7 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     json_out = stdout_to_stderr()
+    _STATE["json_out"] = json_out
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -439,10 +460,15 @@ def main():
     t_gen = time.perf_counter()
     # generated on the GPU (HIP Philox generator, csrc/fdx_synth.hip): the handbook
     # distributions of fdx.synth.generate, pinned by tests/test_gpu_synth.py; inputs resident
-    g = synth.generate_device(n_cl, n_terms, wl["days"], seed=1234 + rank, customer_offset=base, device=dev)
+    # one population for every N: rank r draws the rows of ITS customers of the same population
+    # (draws keyed by the global customer id, tests/test_gpu_synth.py), so the union over the
+    # ranks is the same table at N = 1, 2, 4, 8
+    g = synth.generate_device(n_cl, n_terms, wl["days"], seed=1234, customer_offset=base,
+                              n_customers_total=wl["n_customers_total"], device=dev)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
     n_local = g["ts"].numel()
+    _STATE.update(tx_per_gpu=n_local, workload=wl["name"], n_customers_local=n_cl, days=wl["days"])
     arrays, mean, scale, check_X, check_proba = load_model(args.model)
     forest = ops.Forest(arrays, 15, mean, scale)
     default_variant = forest.variant
@@ -574,9 +600,9 @@ def main():
         "setup_s": {"generate_on_gpu": round(t_gen, 2)},
         **({"rehearsal": "--rehearse-one-gpu: every rank on one GPU, host-staged gloo collectives; not a "
                          "measurement"} if args.rehearse_one_gpu else {}),
-        "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234+rank), "
-                "resident in HBM" + ("; each rank draws its customers' rows from its own seed, so the configs[3] "
-                                     "union differs per N (its distributions do not)" if world > 1 else ""),
+        "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234, "
+                "draws keyed by the global customer id: each rank's rows are the population's rows of its customer "
+                "range, the union is the same table at every N), resident in HBM",
         "config": {"workload": (f"configs[1]: {n_cl} customers / {n_terms // world} terminals / {wl['days']} days "
                                 f"per GPU" if wl["name"] == "configs1" else
                                 f"configs[3]: {wl['n_customers_total']} customers / {n_terms} terminals / "
@@ -716,6 +742,11 @@ def main():
                     "the two all-to-all phases (rows 16 B/row out, count records 24 B/row back); achieved = bytes "
                     "this rank sends to its peers / link_ms against min(world-1, 7) x 153 GB/s; hidden_share = "
                     "part of exchange_ms that overlaps the customer half (main-stream start to customer_walk end)"}
+    if world > 1 or wl["name"] == "configs3":
+        # the 1 -> N curve: configs[3] is strong scaling (the same 1M-customer table at every N), so
+        # every N > 1 line names the N = 1 run of that same table it scales against (a committed
+        # bench line: python bench.py --gpus 1 --workload configs3)
+        out["scales_against"] = scale_reference(wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         data = {k: g[k].cpu().numpy() for k in ("ts", "customer", "terminal", "amount", "fraud")}
         out["cpu_baseline"] = cpu_baseline(data, arrays, mean, scale, check_X, check_proba, args.cpu_score_rows)
@@ -759,5 +790,25 @@ def main():
         dist.destroy_process_group()
 
 
+def main_or_report_oom():
+    """main(); a run whose working set does not fit HBM (e.g. --gpus 1 --workload configs3: the
+    whole 1M-customer / 365-day table on one GPU) prints one JSON line with the error and the
+    byte counts instead of a traceback"""
+    import torch
+
+    try:
+        main()
+    except torch.cuda.OutOfMemoryError as e:
+        free, total = torch.cuda.mem_get_info()
+        line = {"metric": METRIC, "value": None, "unit": "tx/s", "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                "error": "out of HBM: " + str(e).splitlines()[0][:400], "hbm_bytes_free": free,
+                "hbm_bytes_total": total, "hbm_bytes_allocated_by_torch": torch.cuda.memory_allocated(),
+                **{k: v for k, v in _STATE.items() if k != "json_out"}}
+        print(json.dumps(line), file=_STATE.get("json_out") or sys.stdout, flush=True)
+        sys.exit(3)
+
+
+_STATE = {}
+
 if __name__ == "__main__":
-    main()
+    main_or_report_oom()

@@ -666,12 +666,16 @@ int fdx_card_precision_top_k(const int32_t *day_d, const int32_t *cust_d, const 
  * terminals within radius, :786-834 daily Poisson transactions, :1339-1371 time sort, :1732-1782
  * add_frauds).  Profiles, the terminal sampler's band-sorted arrays and the compromised lists
  * come from the host (fdx.synth.generate_device); every random draw is Philox4x32-10 keyed by
- * `seed` with counter (customer, day, slot, purpose) -- the distributions of the reference,
- * not its Python RNG stream.  Two phases: fdx_synth_plan (one host sync) returns the row count
- * n_tx; fdx_synth_fill writes the time-ordered rows (ts ns, customer + customer_offset,
- * terminal, amount, fraud; scenario_d / day_d optional).  comp_term_d: n_comp_term
- * (terminal id, first day) int32 pairs sorted by terminal (compromised for 28 days);
- * comp_cust_d: (customer, first day) pairs sorted by customer (14 days, 1/3 of the rows x5). */
+ * `seed` with counter (customer + customer_offset, day, slot, purpose) -- the distributions of
+ * the reference, not its Python RNG stream.  The descriptor describes customers
+ * [customer_offset, customer_offset + n_customers) of a population (profile arrays indexed by
+ * the local id): with the population's profiles and compromised lists, a range generates
+ * exactly the population's rows of those customers, in the same order.  Two phases:
+ * fdx_synth_plan (one host sync) returns the row count n_tx; fdx_synth_fill writes the
+ * time-ordered rows (ts ns, customer + customer_offset, terminal, amount, fraud; scenario_d /
+ * day_d optional).  comp_term_d: n_comp_term (terminal id, first day) int32 pairs sorted by
+ * terminal (compromised for 28 days); comp_cust_d: (LOCAL customer id, first day) pairs sorted
+ * by customer (14 days, 1/3 of the rows x5). */
 typedef struct {
     int64_t n_customers, n_terminals;
     int32_t n_days;

@@ -510,10 +510,15 @@ constexpr int kW3Block = 1024;
 
 // [a < x] as the sign bit of a - x: the S-tree / segment keys are finite or +inf and never -0.0
 // (build_search_trees and the segment table store +0.0 for -0.0: the same comparisons), f32
-// denormals are kept (a - x == 0 only for a == x), and a NaN x is routed by the caller (rank
-// 0xFFFF) -- so this is exactly the IEEE compare, without a v_cmp -> v_cndmask pair per key
+// denormals are kept (a - x == 0 only for a == x), and a NaN x never reaches it (nan_free; the
+// caller ranks a NaN as 0xFFFF) -- so this is exactly the IEEE compare, without a v_cmp -> v_cndmask pair per key
 // (each pair took an s_nop for the VCC hazard: 8 per S-tree level, r05 ISA)
 __device__ __forceinline__ uint32_t lt_bit(float a, float x) { return __float_as_uint(a - x) >> 31; }
+// The value a search descends with: a NaN replaced by 0.  a - NaN is that NaN, so with its sign
+// bit set (x86 0/0, inf - inf) lt_bit would be 1 for every key, +inf padding included: the descent
+// would count past the feature's samples and the segment load would read past its thresholds.
+// The rank of a NaN is 0xFFFF whatever the search finds.
+__device__ __forceinline__ float nan_free(float x) { return x == x ? x : 0.0f; }
 
 // k_prepare<16, true> with the four kW3Search features ranked by their S-trees (the descent of
 // k_zfill_grouped_w3 below) instead of the binary search over every 16th threshold: those four
@@ -556,13 +561,16 @@ __global__ void __launch_bounds__(kPrepStBlock) k_prepare_st(const double *__res
         for (int f = 0; f < 16; ++f) q[f] = 0u;
         rank_row(v, nf, rt, s_smp, q, others);
         int32_t ek[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+        float xs[4];  // the searched values, a NaN as 0 (see nan_free)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xs[s] = nan_free(v[kW3Search[s]]);
         for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 if (l < rt.elev[s]) {
                     const float4 *nd = reinterpret_cast<const float4 *>(s_t) + 2 * (rt.eoff[s] + ek[s]);
                     const float4 a = nd[0], b = nd[1];
-                    const float x = v[kW3Search[s]];
+                    const float x = xs[s];
                     const int32_t c = (int32_t)(lt_bit(a.x, x) + lt_bit(a.y, x) + lt_bit(a.z, x) + lt_bit(a.w, x) +
                                                 lt_bit(b.x, x) + lt_bit(b.y, x) + lt_bit(b.z, x) + lt_bit(b.w, x));
                     cnt[s] = cnt[s] * 9 + c;
@@ -578,10 +586,10 @@ __global__ void __launch_bounds__(kPrepStBlock) k_prepare_st(const double *__res
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int f = kW3Search[s];
-            const float x = v[f];
+            const float x = xs[s];
             const uint32_t kc = lt_bit(sg[s].x, x) + lt_bit(sg[s].y, x) + lt_bit(sg[s].z, x) + lt_bit(sg[s].w, x);
             const uint32_t rk = cnt[s] > 0 ? (uint32_t)(cnt[s] - 1) * kW3Gap + kc : 0u;
-            q[f] = x != x ? 0xFFFFu : rk;
+            q[f] = v[f] != v[f] ? 0xFFFFu : rk;
         }
         uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(z) + r * 16);
         dst[0] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
@@ -804,13 +812,16 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
         // the 4 continuous features: S-tree descents (cs = #samples < v: the digits c of the
         // levels in base 9), then the kW3Gap thresholds of the segment the count leaves
         int32_t ek[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
+        float xs[4];  // the searched values, a NaN as 0 (see nan_free)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xs[s] = nan_free(v[kW3Search[s]]);
         for (int l = 0; l < e_lmax; ++l) {  // uniform trip count
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 if (l < rt.elev[s]) {
                     const float4 *nd = reinterpret_cast<const float4 *>(s_t) + 2 * (rt.eoff[s] + ek[s]);
                     const float4 a = nd[0], b = nd[1];
-                    const float x = v[kW3Search[s]];
+                    const float x = xs[s];
                     const int32_t c = (int32_t)(lt_bit(a.x, x) + lt_bit(a.y, x) + lt_bit(a.z, x) + lt_bit(a.w, x) +
                                                 lt_bit(b.x, x) + lt_bit(b.y, x) + lt_bit(b.z, x) + lt_bit(b.w, x));
                     cs[s] = cs[s] * 9 + c;
@@ -830,7 +841,7 @@ __global__ void __launch_bounds__(kW3Block) k_zfill_grouped_w3(
             if constexpr (EMIT != 0) emit();
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const float x = v[kW3Search[s]];
+                const float x = xs[s];
                 kc[s] = lt_bit(sg[s].x, x) + lt_bit(sg[s].y, x) + lt_bit(sg[s].z, x) + lt_bit(sg[s].w, x);
             }
         }

@@ -12,9 +12,12 @@
 // third of their transactions x5 and fraudulent.
 //
 // Same distributions, not the reference's RNG stream (pure Python, ~100 s per 1.75M rows):
-// every draw comes from Philox4x32-10 keyed by the seed with counter (customer, day,
-// transaction slot, purpose), so the counting pass and the filling pass see the same draws
-// and the output does not depend on the launch shape.  Parity of the statistics with the
+// every draw comes from Philox4x32-10 keyed by the seed with counter (GLOBAL customer id =
+// local id + customer_offset, day, transaction slot, purpose), so the counting pass and the
+// filling pass see the same draws, the output does not depend on the launch shape, and a
+// rank generating customers [offset, offset + n) of a population gets exactly the rows the
+// whole population's generation holds for them, in the same order (the multi-GPU bench's
+// union is the same data at every N).  Parity of the statistics with the
 // reference generator at config 1: tests/test_gpu_synth.py vs tests/golden/config1_stats.json.
 #include <algorithm>
 #include <cmath>
@@ -112,11 +115,12 @@ __global__ void __launch_bounds__(256) k_synth_count(fdx_synth_desc s, const uin
     const int64_t total = s.n_customers * (int64_t)s.n_days;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t c = (uint32_t)(i / s.n_days), d = (uint32_t)(i - (int64_t)c * s.n_days);
+        const uint32_t cg = c + (uint32_t)s.customer_offset;  // the draws' counter: the global id
         uint32_t k_kept = 0;
         if (has[c]) {
-            const int n = day_count(g, c, d, s.mean_nb_d[c]);
+            const int n = day_count(g, cg, d, s.mean_nb_d[c]);
             for (int k = 0; k < n; ++k) {
-                const int32_t t = tx_time(g, c, d, (uint32_t)k);
+                const int32_t t = tx_time(g, cg, d, (uint32_t)k);
                 k_kept += (t > 0 && t < 86400) ? 1u : 0u;
             }
         }
@@ -143,17 +147,18 @@ __global__ void __launch_bounds__(256) k_synth_fill(fdx_synth_desc s, const uint
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t c = (uint32_t)(i / s.n_days), d = (uint32_t)(i - (int64_t)c * s.n_days);
         if (!has[c]) continue;
+        const uint32_t cg = c + (uint32_t)s.customer_offset;  // the draws' counter: the global id
         const double mean = s.mean_amount_d[c], px = s.cx_d[c], py = s.cy_d[c];
-        const int n = day_count(g, c, d, s.mean_nb_d[c]);
+        const int n = day_count(g, cg, d, s.mean_nb_d[c]);
         int64_t o = offsets[i];
         for (int k = 0; k < n; ++k) {
-            const int32_t t = tx_time(g, c, d, (uint32_t)k);
+            const int32_t t = tx_time(g, cg, d, (uint32_t)k);
             if (!(t > 0 && t < 86400)) continue;
             // amount: N(mean, mean / 2); negative -> U(0, 2 mean); np.round(a, 2) = rint(a * 100) / 100
-            const U4 r2 = g.at(c, d, (uint32_t)k + 1, kPurposeAmt);
+            const U4 r2 = g.at(cg, d, (uint32_t)k + 1, kPurposeAmt);
             double a = mean + 0.5 * mean * normal01(r2.x, r2.y, r2.z, r2.w);
             if (a < 0.0) {
-                const U4 rn = g.at(c, d, (uint32_t)k + 1, kPurposeNeg);
+                const U4 rn = g.at(cg, d, (uint32_t)k + 1, kPurposeNeg);
                 a = unit(rn.x, rn.y) * (mean * 2.0);
             }
             a = rint(a * 100.0) / 100.0;
@@ -162,7 +167,7 @@ __global__ void __launch_bounds__(256) k_synth_fill(fdx_synth_desc s, const uint
             const int32_t *lo = s.range_lo_d + 3 * (int64_t)c, *hi = s.range_hi_d + 3 * (int64_t)c;
             const int64_t s0 = hi[0] - lo[0], s1 = s0 + (hi[1] - lo[1]), s2 = s1 + (hi[2] - lo[2]);
             for (uint32_t att = 0; att < 64 && sel < 0; ++att) {
-                const U4 rt = g.at(c, d, (uint32_t)k + 1, kPurposeTerm + att);
+                const U4 rt = g.at(cg, d, (uint32_t)k + 1, kPurposeTerm + att);
                 const int64_t u = (int64_t)(unit(rt.x, rt.y) * (double)s2);  // in [0, s2] (unit may be 1)
                 const int64_t uu = u >= s2 ? s2 - 1 : u;
                 const int b = uu >= s0 ? (uu >= s1 ? 2 : 1) : 0;
@@ -173,7 +178,7 @@ __global__ void __launch_bounds__(256) k_synth_fill(fdx_synth_desc s, const uint
                 int64_t m = 0;
                 for (int b = 0; b < 3; ++b)
                     for (int32_t j = lo[b]; j < hi[b]; ++j) m += in_disk(s.tx_sorted_d[j], s.ty_sorted_d[j], px, py, s.radius);
-                const U4 rt = g.at(c, d, (uint32_t)k + 1, kPurposeTerm + 64);
+                const U4 rt = g.at(cg, d, (uint32_t)k + 1, kPurposeTerm + 64);
                 int64_t want = (int64_t)(unit(rt.x, rt.y) * (double)m);
                 if (want >= m) want = m - 1;
                 for (int b = 0; b < 3 && sel < 0; ++b)
@@ -196,7 +201,7 @@ __global__ void __launch_bounds__(256) k_synth_fill(fdx_synth_desc s, const uint
                  ++j) {
                 const int32_t d0 = s.comp_cust_d[2 * j + 1];
                 if ((int32_t)d >= d0 && (int32_t)d < d0 + 14) {
-                    const U4 rf = g.at(c, d, (uint32_t)k + 1, kPurposeFraud + (uint32_t)j);
+                    const U4 rf = g.at(cg, d, (uint32_t)k + 1, kPurposeFraud + (uint32_t)d0);
                     if (unit(rf.x, rf.y) <= 1.0 / 3.0) {
                         a = a * 5.0;
                         sc = 3;

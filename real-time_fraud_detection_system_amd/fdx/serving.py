@@ -100,10 +100,19 @@ def table_select(rows, n_slots: int, ts_ns: torch.Tensor, key: torch.Tensor, n_k
     if not isinstance(rows, ops.FeatureTable):
         raise TypeError("table_select reads an ops.FeatureTable (slot order)")
     ops._dev(ts_ns, torch.int64, "ts_ns"); ops._dev(key, torch.int32, "key")
+    n_slots = int(n_slots)
+    if not 0 <= n_slots <= rows.cap:
+        raise ValueError(f"n_slots {n_slots} outside the table's [0, {rows.cap}] slots")
+    if ts_ns.numel() != key.numel():
+        raise ValueError(f"ts_ns has {ts_ns.numel()} rows, key {key.numel()}")
     out = torch.empty(max(int(n_keys), 0), dtype=torch.int32, device=ts_ns.device)
     L = _lib.load()
     ws = ops.workspace(L.fdx_table_select_workspace_size(int(n_keys)), ts_ns.device)
     row = rows.columns(n_slots)["row"]
+    # the kernel reads ts_ns / key at every slot's row: a table from another frame would read out of
+    # bounds (one host read; snapshot export, not the scoring step)
+    if n_slots and int(row.max()) >= ts_ns.numel():
+        raise ValueError("the table's rows index past ts_ns / key: a table written for another frame?")
     check(L.fdx_table_select(ops._ptr(row), int(n_slots), ops._ptr(ts_ns), ops._ptr(key), int(n_keys), int(mode),
                              int(t_lo), int(t_hi), ops._ptr(out), ops._ptr(ws), ws.numel(), ops._s(stream)),
           "fdx_table_select")
@@ -114,18 +123,25 @@ def _windows_label(w):
     return f"{w}DAY_WINDOW"
 
 
+def _original_ids(dense: np.ndarray, ids) -> np.ndarray:
+    """dense key -> the frame's id (int64, the pandas dtype of the reference's id columns)"""
+    return (dense if ids is None else np.asarray(ids)[dense]).astype(np.int64)
+
+
 def latest_terminal_features_from_table(rows, n_slots: int, ts_ns: torch.Tensor, terminal: torch.Tensor,
-                                        n_terminals: int, windows_days=(1, 7, 30)) -> pd.DataFrame:
+                                        n_terminals: int, windows_days=(1, 7, 30), ids=None) -> pd.DataFrame:
     """feature_transformation.ipynb:2914-2918 on the table the scoring step wrote:
     df.loc[df.groupby('TERMINAL_ID').TX_DATETIME.idxmax()].filter(regex='TERMINAL_ID|TERMINAL_ID_RISK')
     -- index = the chosen input rows, rows in terminal order, the reference table's column
-    order and dtypes (counts as float64, as pandas' rolling count)."""
+    order and dtypes (counts as float64, as pandas' rolling count; ids int64).  terminal holds
+    the dense keys the step ran on; ids (optional): dense key -> the frame's TERMINAL_ID, when
+    the frame's ids are not already 0..n-1."""
     slots = table_select(rows, n_slots, ts_ns, terminal, n_terminals, _lib.FDX_SELECT_LATEST)
     keep = slots >= 0
     s = slots[keep].long()
     col = rows.columns(n_slots)
     r = col["row"][s].long()
-    out = {"TERMINAL_ID": terminal[r].cpu().numpy()}
+    out = {"TERMINAL_ID": _original_ids(terminal[r].cpu().numpy(), ids)}
     nb, rk = col["term_nb"][:, s].cpu().numpy(), col["term_risk"][:, s].cpu().numpy()
     for j, w in enumerate(windows_days):
         out[f"TERMINAL_ID_NB_TX_{_windows_label(w)}"] = nb[j].astype(np.float64)
@@ -134,10 +150,12 @@ def latest_terminal_features_from_table(rows, n_slots: int, ts_ns: torch.Tensor,
 
 
 def customer_features_on_from_table(rows, n_slots: int, ts_ns: torch.Tensor, customer: torch.Tensor,
-                                    n_customers: int, date: datetime.date, windows_days=(1, 7, 30)) -> pd.DataFrame:
+                                    n_customers: int, date: datetime.date, windows_days=(1, 7, 30),
+                                    ids=None) -> pd.DataFrame:
     """feature_transformation.ipynb:3606-3635 on the table the scoring step wrote: each
     customer's first transaction of `date` with its lower-cased customer columns and dt = date,
-    rows in frame (input) order, index = those input rows."""
+    rows in frame (input) order, index = those input rows.  ids (optional): dense key -> the
+    frame's CUSTOMER_ID (customer_id is int64 either way)."""
     lo = int(np.datetime64(date, "ns").astype(np.int64))
     slots = table_select(rows, n_slots, ts_ns, customer, n_customers, _lib.FDX_SELECT_FIRST_IN_RANGE, lo,
                          lo + NS_PER_DAY)
@@ -146,7 +164,7 @@ def customer_features_on_from_table(rows, n_slots: int, ts_ns: torch.Tensor, cus
     r = col["row"][s].long()
     o = torch.argsort(r)  # drop_duplicates keeps frame order
     s, r = s[o], r[o]
-    out = {"customer_id": customer[r].cpu().numpy()}
+    out = {"customer_id": _original_ids(customer[r].cpu().numpy(), ids)}
     nb, av = col["cust_nb"][:, s].cpu().numpy(), col["cust_avg"][:, s].cpu().numpy()
     for j, w in enumerate(windows_days):
         out[f"customer_id_nb_tx_{_windows_label(w).lower()}"] = nb[j].astype(np.float64)

@@ -154,10 +154,18 @@ def _profiles(n_customers, n_terminals, r, seed, terminal_seed):
 
 
 def generate_device(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, seed=0, customer_offset=0,
-                    frauds=True, terminal_seed=10_000, device=None, with_scenario=False, stream=None):
+                    frauds=True, terminal_seed=10_000, device=None, with_scenario=False, stream=None,
+                    n_customers_total=None):
     """generate() on the GPU: a dict of device tensors in global time order --
     ts int64 ns, customer int32 (+ customer_offset), terminal int32, amount float64, fraud uint8
-    (and scenario uint8, day int32 when with_scenario)."""
+    (and scenario uint8, day int32 when with_scenario).
+
+    The rows of customers [customer_offset, customer_offset + n_customers) of a population of
+    n_customers_total (default: customer_offset + n_customers): the profiles and the compromised
+    customers are drawn for the whole population and every transaction draw is keyed by the
+    global customer id, so a range's output is the population's generation filtered to its
+    customers, row for row -- the union over any split of the ids is the same data (the
+    multi-GPU bench's like-for-like 1 -> N curve)."""
     import ctypes
 
     import torch
@@ -166,7 +174,12 @@ def generate_device(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, see
     from ._lib import check
 
     dev = device or ops.require_gpu()
-    rng, cx, cy, mean_amount, mean_nb, tx, ty = _profiles(n_customers, n_terminals, r, seed, terminal_seed)
+    c0, n_customers = int(customer_offset), int(n_customers)
+    n_pop = c0 + n_customers if n_customers_total is None else int(n_customers_total)
+    if not (0 <= c0 and c0 + n_customers <= n_pop < 2**31):
+        raise ValueError(f"customers [{c0}, {c0 + n_customers}) outside the population [0, {n_pop})")
+    rng, cx, cy, mean_amount, mean_nb, tx, ty = _profiles(n_pop, n_terminals, r, seed, terminal_seed)
+    cx, cy, mean_amount, mean_nb = (a[c0:c0 + n_customers] for a in (cx, cy, mean_amount, mean_nb))
     sampler = _TerminalSampler(tx, ty, r)
     lo, hi = sampler.ranges(cx, cy)
     frng = np.random.default_rng([seed, 7919])
@@ -174,7 +187,7 @@ def generate_device(n_customers=5000, n_terminals=10000, nb_days=183, r=5.0, see
     if frauds:  # add_frauds: for day in range(max day): 2 terminals for 28 days, 3 customers for 14
         for d in range(nb_days - 1):
             ct += [(int(t), d) for t in frng.choice(n_terminals, 2, replace=False)]
-            cc += [(int(c), d) for c in frng.choice(n_customers, 3, replace=False)]
+            cc += [(int(c) - c0, d) for c in frng.choice(n_pop, 3, replace=False) if c0 <= c < c0 + n_customers]
     comp_t = np.array(sorted(ct), np.int32).reshape(-1, 2)
     comp_c = np.array(sorted(cc), np.int32).reshape(-1, 2)
 

@@ -278,3 +278,13 @@ def test_serving_snapshots_from_the_step_table(dev, config1):
         got_c = serving.customer_features_on_from_table(rows, m, g["ts"], g["customer"], 5_000, day)
         assert len(got_c) > 100, day
         pd.testing.assert_frame_equal(got_c, want_c, check_dtype=False, check_exact=True, check_index_type=False)
+    # the frame's own ids through a dense-key -> id map, int64 like pandas' id column;
+    # a slot count past the table, or ts / key of different lengths, are refused
+    ids = np.arange(10_000, dtype=np.int64) * 7 + 1_000
+    got_i = serving.latest_terminal_features_from_table(rows, m, g["ts"], g["terminal"], 10_000, ids=ids)
+    assert got_i["TERMINAL_ID"].dtype == np.int64
+    np.testing.assert_array_equal(got_i["TERMINAL_ID"].values, ids[want["TERMINAL_ID"].values])
+    with pytest.raises(ValueError, match="n_slots"):
+        serving.table_select(rows, rows.cap + 64, g["ts"], g["terminal"], 10_000, 0)
+    with pytest.raises(ValueError, match="rows"):
+        serving.table_select(rows, m, g["ts"][:-1], g["terminal"], 10_000, 0)

@@ -5,7 +5,8 @@ configs[1]  50k customers / 100k terminals / 183 days (~17.7M tx): the bench's f
             float64 path (featurize -> X -> Forest.predict), and the features of >= 100 sampled
             customers and terminals (all their rows) must equal the C oracle bit for bit.
 configs[2]  RandomForest(100 trees, depth 20) predict_proba: the bench model's 4,096 held-out
-            rows against sklearn's saved output, then 10M rows resampled from them.
+            rows against sklearn's saved output, then 140M rows resampled from them (past one
+            forest row range); the deployed model likewise at 20M rows.
 multi-rank  the exchange kernels (pack / unpack / owner records / reply) with world = 4 and 8
             record formats, the all-to-all simulated on the host: every rank's features must
             equal the single-GPU featurize of the union (the gloo test swaps these kernels for
@@ -110,17 +111,34 @@ def test_fused_path_past_one_forest_row_range(dev):
     assert torch.equal(proba, p64)
 
 
+def _resampled(n, n_src, seed, dev):
+    """n row indices into n_src rows, drawn on the device from a fixed seed"""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    return torch.randint(0, n_src, (n,), generator=g, device=dev, dtype=torch.int64)
+
+
 def test_config3_rf100_d20_bench_model(dev):
+    """configs[2]: RF(100, depth 20) predict_proba over 100M+ HBM-resident rows -- 140M rows
+    resampled from the bench model's 4,096 held-out rows, so sklearn's saved output of each
+    source row is the expectation of every copy.  140M is past one forest row range
+    (134,216,704 rows: the walk's 32-bit offsets into 32-B rank rows), so the traversal runs two
+    ranges and every row of the second is checked too."""
     arrays, z = _model()
     forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
     cx, cp = z["check_X"], z["check_proba"]
     np.testing.assert_array_equal(forest.predict(T(cx, torch.float64, dev)).cpu().numpy(), cp)
-    # 10M rows resampled (fixed seed) from the held-out rows, resident in HBM
-    idx = np.random.default_rng(7).integers(0, len(cx), 10_000_000)
-    Xd = T(cx, torch.float64, dev)[T(idx, torch.int64, dev)]
-    ws = ops.workspace(forest.workspace_size(len(idx)), dev)
-    got = forest.predict(Xd, ws=ws).cpu().numpy()
-    np.testing.assert_array_equal(got, cp[idx])
+    n = 140_000_000
+    idx = _resampled(n, len(cx), 7, dev)
+    Xd = T(cx, torch.float64, dev)[idx]
+    ws = ops.workspace(forest.workspace_size(n), dev)
+    assert forest.traverse_launches(n) == 2  # two row ranges, one chunk-loop launch each
+    got = forest.predict(Xd, ws=ws)
+    del Xd, ws
+    want = T(cp, torch.float64, dev)[idx]
+    bad = int((got != want).sum())
+    assert bad == 0, f"{bad} of {n} rows differ from sklearn"
+    assert torch.equal(got[134_216_704:], want[134_216_704:])
 
 
 def test_fused_path_rejects_ids_out_of_range(dev):
@@ -239,6 +257,25 @@ def test_deployed_model_rank_layout_v2(dev):
     Xd = T(X, torch.float64, dev)[T(idx, torch.int64, dev)]
     got = forest.predict(Xd, ws=ops.workspace(forest.workspace_size(len(idx)), dev)).cpu().numpy()
     np.testing.assert_array_equal(got, z["test_proba1"][idx])
+
+
+def test_deployed_model_20m_rows(dev):
+    """The deployed model (RF(100, unlimited depth), model_training.ipynb:2212) at the size of
+    bench_forest.py's line: 20M rows resampled from the notebook's 66,452 test rows, every row
+    against sklearn's saved predict_proba[:, 1]."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf_deployed.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    X = z["test_X"]
+    n = 20_000_000
+    idx = _resampled(n, len(X), 11, dev)
+    Xd = T(X, torch.float64, dev)[idx]
+    got = forest.predict(Xd, ws=ops.workspace(forest.workspace_size(n), dev))
+    del Xd
+    want = T(z["test_proba1"], torch.float64, dev)[idx]
+    bad = int((got != want).sum())
+    assert bad == 0, f"{bad} of {n} rows differ from sklearn"
 
 
 @pytest.mark.parametrize("base,n_c", [(375_000, 125_000), (0, 500_000)], ids=["rank3of8", "rank0of2"])

@@ -515,6 +515,48 @@ def test_fused_scoring_nan_amounts(dev):
     np.testing.assert_array_equal(p.cpu().numpy(), p_ref.cpu().numpy())
 
 
+def test_negative_nan_in_the_s_tree_searches(dev):
+    """a NaN with its sign bit set (what x86 0/0 or inf - inf give) in the four
+    features the S-trees rank (amount and the three customer averages), with the bench model
+    (whose four continuous features are searched by S-trees): through fdx_forest_predict
+    (k_prepare_st) against the oracle, and through the fused step (k_zfill_grouped_w3) against
+    the float64 path.  [a < NaN] by the sign of a - NaN was 1 for every key there, the descent
+    counted past the samples and the segment read left the feature's thresholds."""
+    import os
+
+    from fdx import synth
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    z = np.load(os.path.join(root, "bench_assets", "rf100_d20.npz"))
+    arrays = {k: z[k].astype(np.int64) if k in ("left", "right", "feature") else z[k]
+              for k in ("node_offsets", "left", "right", "feature", "threshold", "missing_left", "value1")}
+    forest = ops.Forest(arrays, 15, z["mean"], z["scale"])
+    neg_nan = np.copysign(np.nan, -1.0)
+    assert np.signbit(neg_nan)
+    X = z["check_X"].copy()
+    rng = np.random.default_rng(5)
+    for f in (0, 4, 6, 8):
+        X[rng.random(len(X)) < 0.1, f] = neg_nan
+    assert np.signbit(X[np.isnan(X)]).all()
+    got = forest.predict(T(X, torch.float64, dev)).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.forest_predict(X, arrays, z["mean"], z["scale"]))
+    # the fused step: -NaN amounts (and the customer averages they make NaN)
+    d = synth.generate(n_customers=300, n_terminals=400, nb_days=40, seed=44)
+    amt = d["amount"].copy()
+    amt[rng.choice(len(amt), 40, replace=False)] = neg_nan
+    args = (T(d["ts"], torch.int64, dev), T(d["customer"], torch.int32, dev), T(d["terminal"], torch.int32, dev),
+            T(amt, torch.float64, dev), T(d["fraud"], torch.uint8, dev))
+    n = len(d["ts"])
+    pipe = FraudPipeline(forest=forest)
+    f, p_ref = pipe.run(*args, 300, 400)
+    assert np.isnan(f.X.cpu().numpy()[:, 0]).sum() == 40
+    np.testing.assert_array_equal(p_ref.cpu().numpy(),
+                                  oracle.forest_predict(f.X.cpu().numpy(), arrays, z["mean"], z["scale"]))
+    p = torch.empty(n, dtype=torch.float64, device=dev)
+    pipe.run_fused(*args, 300, 400, p, ops.workspace(forest.workspace_size(n * 11 // 10), dev))
+    np.testing.assert_array_equal(p.cpu().numpy(), p_ref.cpu().numpy())
+
+
 @pytest.mark.parametrize("variant", [1, 3])
 def test_fused_scoring_every_rank_format(dev, golden, variant):
     """The fused scoring path (rank rows prepared in-pipeline) on each rank node format the

@@ -44,9 +44,10 @@ def test_gpu_generator_structure_and_determinism(dev):
     assert ((secs % 86400) > 0).all()
     assert h["customer"].min() >= 7000 and h["customer"].max() < 9000
     assert h["terminal"].min() >= 0 and h["terminal"].max() < 4000
-    # same profiles and terminal map as the host generator with this seed
-    _, cx, cy, mean_amount, _, tx, ty = synth._profiles(2000, 4000, 5.0, 11, 10_000)
-    c = h["customer"] - 7000
+    # same profiles and terminal map as the host generator with this seed (customers 7000..8999
+    # of a population of 9,000)
+    _, cx, cy, mean_amount, _, tx, ty = synth._profiles(9000, 4000, 5.0, 11, 10_000)
+    c = h["customer"]
     dist = np.sqrt((tx[h["terminal"]] - cx[c]) ** 2 + (ty[h["terminal"]] - cy[c]) ** 2)
     assert (dist < 5.0).all()
     cents = h["amount"] * 100
@@ -70,3 +71,26 @@ def test_gpu_generator_config4_rank_shard(dev):
     assert bool((d["ts"][1:] >= d["ts"][:-1]).all())
     assert int(d["customer"].min()) >= 375_000 and int(d["customer"].max()) < 500_000
     print(f"config-4 shard: {n} tx generated in {dt:.2f} s")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gpu_generator_customer_ranges_union_is_world1(dev, world):
+    """the bench's ranks generate contiguous customer ranges of one
+    population (every draw keyed by the global customer id, the profiles and compromised
+    customers drawn for the population).  Each range's output must be the world-1 generation
+    filtered to its customers, row for row, every column -- so the multi-GPU union is the same
+    data at every N."""
+    C, T, D = 24_000, 30_000, 90
+    whole = _host(synth.generate_device(C, T, D, seed=1234, device=dev, with_scenario=True))
+    n_seen = 0
+    for r in range(world):
+        lo, hi = r * C // world, (r + 1) * C // world
+        part = _host(synth.generate_device(hi - lo, T, D, seed=1234, customer_offset=lo, n_customers_total=C,
+                                           device=dev, with_scenario=True))
+        m = (whole["customer"] >= lo) & (whole["customer"] < hi)
+        assert m.sum() == len(part["ts"]) > 0
+        for k in whole:
+            np.testing.assert_array_equal(part[k], whole[k][m], err_msg=f"rank {r} of {world}: {k}")
+        n_seen += len(part["ts"])
+    assert n_seen == len(whole["ts"])
+    assert (whole["scenario"] == 3).sum() > 0  # the scenario-3 draws are covered
