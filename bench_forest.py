@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default=os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
     ap.add_argument("--variant", type=int, default=-1, help="forest walk variant (fdx.h; -1: the library's choice)")
+    ap.add_argument("--range-rows", type=int, default=-1, help="rows per traversal range (-1: the library's choice)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -54,6 +55,8 @@ def main():
     forest = ops.Forest(arrays, 15, mean, scale)
     if args.variant >= 0:
         forest.set_variant(args.variant)
+    if args.range_rows >= 0:
+        forest.set_range_rows(args.range_rows)
     n = args.rows
     g = torch.Generator(device=dev)
     g.manual_seed(20240601)

@@ -459,6 +459,9 @@ int fdx_forest_traverse_launches(fdx_forest forest, int64_t n, int32_t with_leav
  * prepared workspace depends on the layout: prepare again after switching layouts. */
 int fdx_forest_set_variant(fdx_forest forest, int32_t variant);
 int fdx_forest_get_variant(fdx_forest forest, int32_t *variant);
+/* Rows per traversal range (rounded down to a multiple of 1,024; 0 = the default, as many as
+ * the walk's 32-bit offsets allow): every chunk walks one range before the next range starts. */
+int fdx_forest_set_range_rows(fdx_forest forest, int64_t rows);
 
 /* Fused assemble + scale for the scoring pipeline: writes the forest's float32 feature
  * rows in the workspace straight from the window kernels' grouped outputs (same columns

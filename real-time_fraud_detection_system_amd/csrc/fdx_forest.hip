@@ -305,7 +305,37 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
+    // PW == 3, speculative children: with the node's rank read, a step also reads BOTH children
+    // (left = p + 1, right = p + offset; a leaf's "right child" is itself, offset 0), so the
+    // chain's next node is already in a register when the compare picks it -- ONE dependent LDS
+    // round trip per level instead of two (node -> rank), for 3 reads instead of 2.  For walks
+    // bound by read latency rather than by the LDS array: one chain per lane, as the deployed
+    // model's one-tree chunks (rank layout v2).  med3(d, 1, off) is 1 exactly for a left move
+    // (an internal node's right offset is >= 2), off for a right move, 0 at a leaf.
+    uint32_t cl[PW == 3 ? K : 1], cr[PW == 3 ? K : 1];
+    auto fetch_children = [&](int k) {
+        cl[k] = lds32(lds, pa[k] + 4u);
+        cr[k] = lds32(lds, pa[k] + ((nd[k] & kOffMask<P16>) << 2));
+    };
+    if constexpr (PW == 3) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) fetch_children(k);
+    }
     auto step = [&]() {
+        if constexpr (PW == 3) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int32_t d = P16 ? (int32_t)((x[k] << (P16 == 3 ? sh : 16u)) + nd[k]) : (int32_t)(x[k] - nd[k]);
+                uint32_t st;
+                asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
+                nd[k] = st == 1u ? cl[k] : cr[k];
+                pa[k] += st << 2;
+                x[k] = fetch_x(k);
+                fetch_children(k);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return;
+        }
         if constexpr (PW >= 100) {
             static_assert(PW == 102 && P16 == 0, "interleaved pairs: u32 planes");
 #pragma unroll
@@ -534,11 +564,22 @@ __device__ __forceinline__ void rank_tree_values(const double (&v)[R * GG], int 
 
 // proba[row] = (sum of the row's tree values in tree order) / n_trees: the same float64
 // additions, in the same order, as the chunk-sequential launches' running sum.
+// The loads go out kTreeSumBatch at a time before their additions (the rolled loop had one or
+// two in flight per lane: 27 us for a 64k-row stream batch of 100 trees, r06e trace).
+constexpr int kTreeSumBatch = 25;
 __global__ void __launch_bounds__(256) k_tree_sum(const double *__restrict__ tv, int64_t n, int32_t n_trees,
                                                   const int32_t *__restrict__ out_perm, double *__restrict__ proba) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         double a = 0.0;
-        for (int t = 0; t < n_trees; ++t) a += tv[(int64_t)t * n + r];
+        int t = 0;
+        for (; t + kTreeSumBatch <= n_trees; t += kTreeSumBatch) {
+            double v[kTreeSumBatch];
+#pragma unroll
+            for (int j = 0; j < kTreeSumBatch; ++j) v[j] = tv[(int64_t)(t + j) * n + r];
+#pragma unroll
+            for (int j = 0; j < kTreeSumBatch; ++j) a += v[j];  // tree order
+        }
+        for (; t < n_trees; ++t) a += tv[(int64_t)t * n + r];
         const int64_t dst = out_perm ? (int64_t)out_perm[r] : r;
         if (dst >= 0) proba[dst] = a / (double)n_trees;
     }
@@ -1409,7 +1450,15 @@ static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
 // 32-B rank rows), each launch over base pointers moved to its range.
 static int64_t rank_range_rows(const fdx_forest_s *F) {
     const int64_t row_bytes = kVariants[F->variant].p16 == 2 ? 64 : 32;
-    return ((int64_t)UINT32_MAX / row_bytes) & ~(int64_t)1023;
+    const int64_t rr = ((int64_t)UINT32_MAX / row_bytes) & ~(int64_t)1023;
+    return F->range_rows > 0 ? std::min(rr, std::max<int64_t>(F->range_rows & ~(int64_t)1023, 1024)) : rr;
+}
+
+extern "C" int fdx_forest_set_range_rows(fdx_forest F, int64_t rows) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(rows >= 0, "rows < 0");
+    F->range_rows = rows;
+    return FDX_OK;
 }
 
 extern "C" int fdx_forest_traverse_launches(fdx_forest F, int64_t n, int32_t with_leaves, int32_t *launches) {
@@ -1483,6 +1532,8 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
+                case 5: FDX_LAUNCH_RANK(1024, 1, 6, 2, 3); break;
+                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 0, 3); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -60,6 +60,7 @@ struct fdx_forest_s {
     std::vector<double> h_mean, h_scale;
     int32_t rn_slots = 0, rslot_feat[32] = {}, rslot_base[32] = {};
     int32_t n_cu = 256;  // compute units of the forest's device: one rank-kernel block per CU
+    int64_t range_rows = 0;  // rows per traversal range (0: as many as 32-bit offsets allow)
 };
 
 namespace fdx {
@@ -146,6 +147,8 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
+    {1024, 1, 6, 1, 2, 3},   // 5: v2, speculative children (one LDS round trip per level)
+    {1024, 1, 10, 1, 0, 3},  // 6: v1, speculative children
 };
 // (Round 5 also measured a one-round-trip study form (rank address from the node's address, wrong
 // results: 7.05 vs 6.70 ms) and two-level packets (commit 654bb3b: bit-exact, 12 % slower per

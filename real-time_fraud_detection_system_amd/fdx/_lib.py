@@ -154,6 +154,7 @@ SIGNATURES = {
     "fdx_forest_traverse_perm": (ctypes.c_int, [P, c_i64, P, P, P, P, c_sz, P]),
     "fdx_forest_set_variant": (ctypes.c_int, [P, c_i32]),
     "fdx_forest_get_variant": (ctypes.c_int, [P, P]),
+    "fdx_forest_set_range_rows": (ctypes.c_int, [P, ctypes.c_int64]),
     "fdx_forest_prepare_reply": (ctypes.c_int, [P, P, P, c_i64, c_i32, c_i32, P, c_sz, P]),
 }
 

@@ -626,6 +626,10 @@ class Forest:
         self.n_chunks = nc.value
         self.variant = int(variant)
 
+    def set_range_rows(self, rows: int) -> None:
+        """rows per traversal range (fdx_forest_set_range_rows; 0 = the default)"""
+        check(_lib.load().fdx_forest_set_range_rows(self._h, int(rows)), "fdx_forest_set_range_rows")
+
     def traverse_launches(self, n: int, want_leaves: bool = False) -> int:
         """tree-walk kernel launches of one traversal of n rows (fdx_forest_traverse_launches)"""
         k = ctypes.c_int32()

@@ -7,7 +7,9 @@ assembly, takes the default kernel (k_forest_rank<1024, 1, 10, 0, 102>), and pri
   * the text of the steady-state block of the chunk size the bench runs most (6 trees:
     the one-group loop, 6 chains in 3 interleaved pairs, 4 unrolled steps per exit test).
 
-usage: python3 tools/isa_excerpt.py [out.txt]
+usage: python3 tools/isa_excerpt.py [out.txt] [v2]
+  v2: the rank-layout-v2 chunk-loop instantiation the deployed model runs
+      (k_forest_rank<1024, 1, 6, 2, 2, true>: one-tree chunks, one chain per lane, u16 planes)
 """
 import collections
 import os
@@ -18,6 +20,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "real-time_fraud_detection_system_amd", "csrc")
 KERNEL = "k_forest_rankILi1024ELi1ELi10ELi0ELi102ELb1E"  # the chunk-loop instantiation (large batches)
+
+
+KERNEL_V2 = "k_forest_rankILi1024ELi1ELi6ELi2ELi2ELb1E"
 
 
 def kernel_body(asm):
@@ -60,14 +65,20 @@ def ops(block):
 
 
 def main():
+    global KERNEL
     out = sys.argv[1] if len(sys.argv) > 1 else None
+    v2 = len(sys.argv) > 2 and sys.argv[2] == "v2"
+    if v2:
+        KERNEL = KERNEL_V2
     asm_path = "/tmp/fdx_forest_isa.s"
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                            "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", "-o", asm_path,
                            os.path.join(CSRC, "fdx_forest.hip")])
     asm = open(asm_path).read()
     body, summ = kernel_body(asm)
-    res = [f"k_forest_rank<1024, 1, 10, 0, 102, true> (default variant 1, chunk loop), gfx950, hipcc -O3", "register summary:"]
+    res = [("k_forest_rank<1024, 1, 6, 2, 2, true> (variant 2, rank layout v2: the deployed model; chunk loop)" if v2 else
+            "k_forest_rank<1024, 1, 10, 0, 102, true> (default variant 1, chunk loop)") + ", gfx950, hipcc -O3",
+           "register summary:"]
     res += ["  " + s for s in summ]
     res.append("")
     res.append("walk blocks (one v_med3_i32 per chain-step): per chain-step instruction counts")
@@ -76,7 +87,7 @@ def main():
     for name, b in blocks(body):
         o = ops(b)
         n = sum(1 for x in o if x.startswith("v_med3_i32"))
-        if n < 4:
+        if n < (1 if v2 else 4):
             continue
         c = collections.Counter(x.split()[0] for x in o)
         ds = sum(v for k, v in c.items() if k.startswith("ds_read"))
@@ -89,10 +100,11 @@ def main():
         res.append(f"{name:>14} {n:5d} {ds / n:7.2f} {valu / n:5.2f} {salu / n:5.2f} {len(waits) / n:7.2f} "
                    + ", ".join(f"{k} x{v}" for k, v in sorted(lg.items())))
     # the 6-chain steady-state interval: 24 med3 (6 chains x 4 steps)
-    six = [w for w in walk if w[1] == 24]
+    six = [w for w in walk if w[1] == (4 if v2 else 24)]
     if six:
         name, n, o = six[0]
-        res += ["", f"steady-state interval of a 6-tree chunk ({name}: 6 chains x 4 steps), in issue order:"]
+        res += ["", f"steady-state interval ({name}: " + ("1 chain x 4 steps" if v2 else "6 chains x 4 steps")
+                + "), in issue order:"]
         res += ["  " + x for x in o]
     text = "\n".join(res) + "\n"
     if out:
