@@ -494,6 +494,12 @@ int fdx_forest_prepare_reply(fdx_forest forest, const int64_t *reply_d, const in
 #define FDX_PREP_VAL_IS_SUM 1   /* cust_avg_d holds rolling sums: average = sum / nb here      */
 #define FDX_PREP_TERM_COMPACT 4 /* term_rec_d holds COMPACT records (fdx_terminal_windows_
                                    grouped_compact; n_windows = 3, 16-byte aligned)          */
+#define FDX_PREP_FLAG_CLEARED 8 /* the workspace's NaN flag was cleared by fdx_forest_clear_flag
+                                   (earlier, e.g. on another stream): no clearing memset here   */
+/* Clears the NaN flag of a forest workspace sized for n rows (a 4-byte memset on `stream`): with
+ * FDX_PREP_FLAG_CLEARED, the prepare call that follows skips its own clearing -- the scoring step
+ * enqueues this off its critical path (fdx.pipeline). */
+int fdx_forest_clear_flag(fdx_forest forest, int64_t n, void *workspace_d, size_t workspace_bytes, void *stream);
 int fdx_forest_prepare_grouped(fdx_forest forest, int64_t n, int32_t n_windows, int32_t flags_mode,
                                int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                const int32_t *cust_nb_d, const double *cust_avg_d,

@@ -1116,6 +1116,19 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
     return FDX_OK;
 }
 
+extern "C" int fdx_forest_clear_flag(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, void *stream) {
+    FDX_REQUIRE(F, "null forest");
+    FDX_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return FDX_OK;
+    float *z;
+    double *acc;
+    int32_t *flag;
+    int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
+    if (rc) return rc;
+    FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), as_stream(stream)));
+    return FDX_OK;
+}
+
 extern "C" int fdx_forest_prepare_grouped(fdx_forest F, int64_t n, int32_t n_windows, int32_t flags_mode,
                                           int32_t cust_val_is_sum, const int64_t *cust_ts_d, const double *cust_amount_d,
                                           const int32_t *cust_nb_d, const double *cust_avg_d,
@@ -1148,7 +1161,8 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
                 3 + 4 * n_windows);
     if (n == 0) return FDX_OK;
     FDX_REQUIRE(cust_ts_d && cust_amount_d && cust_nb_d && cust_avg_d && term_rec_d, "null pointer");
-    FDX_REQUIRE((cust_val_is_sum & ~5) == 0, "cust_val_is_sum: FDX_PREP_VAL_IS_SUM | FDX_PREP_TERM_COMPACT only");
+    FDX_REQUIRE((cust_val_is_sum & ~13) == 0,
+                "cust_val_is_sum: FDX_PREP_VAL_IS_SUM | FDX_PREP_TERM_COMPACT | FDX_PREP_FLAG_CLEARED only");
     FDX_REQUIRE(!(cust_val_is_sum & 4) || (n_windows == 3 && ((uintptr_t)term_rec_d & 15) == 0),
                 "compact terminal records: W = 3 and a 16-byte aligned record array");
     float *z;
@@ -1157,7 +1171,8 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
     int rc = forest_ws(F, n, ws, ws_bytes, &z, &acc, &flag);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
-    FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
+    if (!(cust_val_is_sum & FDX_PREP_FLAG_CLEARED)) FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
+    cust_val_is_sum &= ~FDX_PREP_FLAG_CLEARED;
     const unsigned grid = stream_grid(n, 256);
     const RankTab rt = rank_tab(F);
     if (rank_mode(F) && n_windows == 3 && rt.rat && rt.etab) {

@@ -305,37 +305,7 @@ __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = fetch_x(k);
-    // PW == 3, speculative children: with the node's rank read, a step also reads BOTH children
-    // (left = p + 1, right = p + offset; a leaf's "right child" is itself, offset 0), so the
-    // chain's next node is already in a register when the compare picks it -- ONE dependent LDS
-    // round trip per level instead of two (node -> rank), for 3 reads instead of 2.  For walks
-    // bound by read latency rather than by the LDS array: one chain per lane, as the deployed
-    // model's one-tree chunks (rank layout v2).  med3(d, 1, off) is 1 exactly for a left move
-    // (an internal node's right offset is >= 2), off for a right move, 0 at a leaf.
-    uint32_t cl[PW == 3 ? K : 1], cr[PW == 3 ? K : 1];
-    auto fetch_children = [&](int k) {
-        cl[k] = lds32(lds, pa[k] + 4u);
-        cr[k] = lds32(lds, pa[k] + ((nd[k] & kOffMask<P16>) << 2));
-    };
-    if constexpr (PW == 3) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) fetch_children(k);
-    }
     auto step = [&]() {
-        if constexpr (PW == 3) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int32_t d = P16 ? (int32_t)((x[k] << (P16 == 3 ? sh : 16u)) + nd[k]) : (int32_t)(x[k] - nd[k]);
-                uint32_t st;
-                asm("v_med3_i32 %0, %1, 1, %2" : "=v"(st) : "v"(d), "v"(nd[k] & kOffMask<P16>));
-                nd[k] = st == 1u ? cl[k] : cr[k];
-                pa[k] += st << 2;
-                x[k] = fetch_x(k);
-                fetch_children(k);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            return;
-        }
         if constexpr (PW >= 100) {
             static_assert(PW == 102 && P16 == 0, "interleaved pairs: u32 planes");
 #pragma unroll
@@ -1532,8 +1502,6 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
-                case 5: FDX_LAUNCH_RANK(1024, 1, 6, 2, 3); break;
-                case 6: FDX_LAUNCH_RANK(1024, 1, 10, 0, 3); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -147,9 +147,13 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
-    {1024, 1, 6, 1, 2, 3},   // 5: v2, speculative children (one LDS round trip per level)
-    {1024, 1, 10, 1, 0, 3},  // 6: v1, speculative children
 };
+// (Round 6 measured and removed: speculative children -- the node's rank read AND both children's
+// reads issued together, one dependent LDS round trip per level for 3 reads instead of 2:
+// bit-exact, deployed model 42.4 -> 48.9 ms and bench model 6.57 -> 10.57 ms; the level-1 node
+// from SGPR words of the root's children (one read and one round trip less per tree): 6.48-6.55
+// -> 6.61-6.62 ms; the deployed model's 64-B rank rows read as 48 B: 42.4 -> 41.8 ms, i.e. not
+// bound by the rows' re-stream; profiles/r06_forest_studies.txt.)
 // (Round 5 also measured a one-round-trip study form (rank address from the node's address, wrong
 // results: 7.05 vs 6.70 ms) and two-level packets (commit 654bb3b: bit-exact, 12 % slower per
 // tree-step; profiles/r05uz_forest_walk_studies.txt) and removed them.)

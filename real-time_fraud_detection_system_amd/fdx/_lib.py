@@ -148,6 +148,7 @@ SIGNATURES = {
     "fdx_forest_prepare": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, c_sz, P]),
     "fdx_forest_traverse": (ctypes.c_int, [P, c_i64, P, P, P, c_sz, P]),
     "fdx_forest_prepare_features": (ctypes.c_int, [P, c_i64, c_i32, P, P, P, P, P, P, P, P, P, P, c_sz, P]),
+    "fdx_forest_clear_flag": (ctypes.c_int, [P, c_i64, P, c_sz, P]),
     "fdx_forest_prepare_grouped": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_forest_prepare_grouped_rows": (ctypes.c_int, [P, c_i64, c_i32, c_i32, c_i32, P, P, P, P, P, P, P, P, c_i64,
                                                        c_i32, P, c_sz, P]),

@@ -687,16 +687,23 @@ def forest_prepare_reply(forest: "Forest", reply: torch.Tensor, perm: torch.Tens
                                                _ptr(ws), ws.numel(), _s(stream)), "fdx_forest_prepare_reply")
 
 
+def forest_clear_flag(forest: "Forest", n: int, ws: torch.Tensor, stream=None) -> None:
+    """clear the NaN flag of a workspace for n rows (for forest_prepare_grouped(flag_cleared=True))"""
+    check(_lib.load().fdx_forest_clear_flag(forest._h, int(n), _ptr(ws), ws.numel(), _s(stream)),
+          "fdx_forest_clear_flag")
+
+
 def forest_prepare_grouped(forest: "Forest", flags_mode: int, cts, camt, cnb, cavg, cperm, term_inv, term_rec,
                            ws: torch.Tensor, stream=None, n=None, val_is_sum: bool = False, term_compact: bool = False,
-                           rows_out=None):
+                           rows_out=None, flag_cleared: bool = False):
     """cavg holds averages, or rolling sums when val_is_sum (interleaved customer path);
     term_compact: term_rec is terminal_windows_compact's array; rows_out: the featurized table
     written by the same pass -- a FeatureRecords (by input row) or a FeatureTable (columns by
-    scoring slot, capacity >= n)."""
+    scoring slot, capacity >= n); flag_cleared: forest_clear_flag ran on this workspace before
+    (stream-ordered before this call), so the call does not clear it itself."""
     n = cts.numel() if n is None else int(n)
     W = cnb.shape[0]
-    opts = (1 if val_is_sum else 0) | (4 if term_compact else 0)
+    opts = (1 if val_is_sum else 0) | (4 if term_compact else 0) | (8 if flag_cleared else 0)
     out, cap, order = None, 0, 0
     if rows_out is not None:
         if not isinstance(rows_out, (FeatureRecords, FeatureTable)):

@@ -55,6 +55,9 @@ class FraudPipeline:
     crit_priority = 0
     side_priority = -1
     terminal_after_customer_rekey = True
+    # the assembly and the forest on the terminal half's stream (the half that ends last), the NaN
+    # flag cleared on the main stream beforehand (tools/step_ab.py measures it against 0)
+    tail_on_side = 1
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
@@ -239,15 +242,28 @@ class FraudPipeline:
                 else:
                     inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, main)
                 mk("customer_walk", main)
-                main.wait_stream(side)
-                trec.record_stream(main)
                 ws = self._forest_ws(lay.n_slots, ws, amount.device)
-                ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow, None, trec,
-                                           ws, main, n=lay.n_slots, val_is_sum=True, term_compact=compact,
-                                           rows_out=rows_out)
-                mk("assemble_rows", main)
-                ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, main)
-                mk("forest_traverse", main)
+                # the assembly and the forest run on the stream that finishes its half LAST -- the
+                # terminal half since round 5's reorder (it ends ~0.3 ms after the walk,
+                # profiles/r05br_step_timeline.txt) -- so that no cross-stream wait (~20 us) sits
+                # on the critical path; the workspace's NaN flag is cleared here, off it (5 us)
+                tail = side if overlap and self.tail_on_side else main
+                if tail is not main:
+                    ops.forest_clear_flag(self.forest, lay.n_slots, ws, main)
+                    tail.wait_stream(main)
+                    for t in (lay.its, lay.iamt, lay.irow, inb, isum, ws, proba, amount) + \
+                            ((rows_out.buf,) if rows_out is not None else ()):
+                        t.record_stream(tail)
+                else:
+                    main.wait_stream(side)
+                    trec.record_stream(main)
+                with torch.cuda.stream(tail):
+                    ops.forest_prepare_grouped(self.forest, self.flags_mode, lay.its, lay.iamt, inb, isum, lay.irow,
+                                               None, trec, ws, tail, n=lay.n_slots, val_is_sum=True,
+                                               term_compact=compact, rows_out=rows_out, flag_cleared=tail is not main)
+                    mk("assemble_rows", tail)
+                    ops.forest_traverse_perm(self.forest, lay.n_slots, ws, proba, lay.irow, tail)
+                    mk("forest_traverse", tail)
                 if validate:  # read once everything is enqueued (the counts ran in the re-keys)
                     for c in rc:
                         c.check()

@@ -19,8 +19,7 @@ from forest_gen import random_forest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = [1, 2, 3, 4, 5, 6]  # v1 (10 chains per lane, interleaved pairs), v2 (6), compact v2 (6), v2 (10),
-#                               v2 / v1 with speculative children (one LDS round trip per level)
+VARIANTS = [1, 2, 3, 4]  # v1 (10 chains per lane, interleaved pairs), v2 (6), compact v2 (6), v2 (10)
 
 
 def T(a, dt, dev):
@@ -149,7 +148,7 @@ def test_traverse_launch_count(dev, variant):
         return
     k = f.traverse_launches(big)
     assert k in (1, nc)
-    rows = (2**32 - 1) // (64 if variant in (2, 4, 5) else 32) // 1024 * 1024
+    rows = (2**32 - 1) // (64 if variant in (2, 4) else 32) // 1024 * 1024
     assert f.traverse_launches(rows) == k
     assert f.traverse_launches(rows + 1) == 2 * k
     assert f.traverse_launches(big, want_leaves=True) == nc
@@ -231,9 +230,8 @@ def test_refused_variant_leaves_the_forest_intact(dev):
             f.set_variant(bad)
         assert f.variant == v0
         np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
-    for v in (4, 5):
-        f.set_variant(v)
-        np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+    f.set_variant(4)
+    np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
     f.set_variant(2)
     assert f.n_chunks == nc0
     np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
