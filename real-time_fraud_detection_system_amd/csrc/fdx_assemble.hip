@@ -1027,7 +1027,7 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     hipStream_t st = as_stream(stream);
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
-    if (rank_mode(F) && kVariants[F->variant].p16 == 2) {
+    if (rank_mode(F) && v2_rows(kVariants[F->variant].p16)) {
         hipLaunchKernelGGL(k_prepare_v2, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride, F->n_features,
                            F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
         FDX_LAUNCHED("k_prepare_v2");
@@ -1069,7 +1069,7 @@ extern "C" int fdx_forest_prepare_features(fdx_forest F, int64_t n, int32_t n_wi
                                            const int32_t *term_nb_d, const double *term_risk_d, void *ws,
                                            size_t ws_bytes, void *stream) {
     FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+    FDX_REQUIRE(!(rank_mode(F) && v2_rows(kVariants[F->variant].p16)),
                 "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(F->n_features == 3 + 4 * n_windows, "forest has %d features, expected %d", F->n_features,
@@ -1098,7 +1098,7 @@ extern "C" int fdx_forest_prepare_reply(fdx_forest F, const int64_t *reply_d, co
                                         int32_t n_windows, int32_t col0, void *ws, size_t ws_bytes,
                                         void *stream) {
     FDX_REQUIRE(F, "null forest");
-    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+    FDX_REQUIRE(!(rank_mode(F) && v2_rows(kVariants[F->variant].p16)),
                 "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(col0 >= 0 && col0 + 2 * n_windows <= F->n_features, "columns out of range");
@@ -1153,7 +1153,7 @@ extern "C" int fdx_forest_prepare_grouped_rows(fdx_forest F, int64_t n, int32_t 
                 "slot-order feature table: out_cap %lld must be >= n = %lld and a multiple of 64",
                 (long long)out_cap, (long long)n);
     FDX_REQUIRE(!rows_out_d || ((uintptr_t)rows_out_d & 15) == 0, "feature output must be 16-byte aligned");
-    FDX_REQUIRE(!(rank_mode(F) && kVariants[F->variant].p16 == 2),
+    FDX_REQUIRE(!(rank_mode(F) && v2_rows(kVariants[F->variant].p16)),
                 "the fused scoring rows need the v1 row format (one slot per feature)");
     FDX_REQUIRE(n >= 0 && n_windows >= 1 && n_windows <= FDX_MAX_WINDOWS, "bad argument");
     FDX_REQUIRE(flags_mode == FDX_FLAGS_NOTEBOOK || flags_mode == FDX_FLAGS_SPARK, "bad flags mode");

@@ -198,14 +198,29 @@ __device__ __forceinline__ uint32_t lds16(const char *lds, uint32_t byte_addr) {
 // offset (rank layout v1); 2 = rank layout v2: u16 planes of 1,024 rows, a 5-bit SLOT field and
 // an 11-bit right offset (see build_rank_layout).
 template <int P16>
-constexpr uint32_t kSlotMask = (P16 == 2 || P16 == 3) ? 0xF800u : 0xF000u;
+constexpr uint32_t kSlotMask = P16 >= 2 ? 0xF800u : 0xF000u;
 template <int P16>
-constexpr uint32_t kOffMask = (P16 == 2 || P16 == 3) ? 0x7FFu : 0xFFFu;
+constexpr uint32_t kOffMask = P16 >= 2 ? 0x7FFu : 0xFFFu;
 // 3 = the v2 node format over 16 u16 planes of 1,024 rows (32 KiB): forests whose every feature
 // fits one slot (slot = feature, the v1 row format); the node region starts at 32 KiB, so a
 // chunk holds a third more nodes than with 64 KiB of planes (fewer chunk launches per batch)
+// 4 = the v2 node format, TWO rows per lane (2,048 rows per 1,024-lane block): plane s holds one
+// dword per lane -- its first row's u16 rank in the low half, its second row's in the high half --
+// and only the forest's n_slots planes are staged, at the TOP of the LDS (byte pb = kLdsTotal -
+// 4,096 n_slots); the nodes start at byte 0.  A rank address is 2 (node & 0xF800) + pb + 4 lane
+// (+ 2 for the second row): one VALU more than the OR form, and lanes read 64 different banks
+// whatever slots they test.  The deployed model (22 slots, trees up to 16.9k nodes) walks one
+// tree per chunk: with one row per lane that is ONE dependency chain per lane (latency-bound,
+// r06d PMC: 67 % of wave time in s_waitcnt); two rows double the chains in flight per CU.
 template <int P16>
-constexpr uint32_t kNodeB = P16 == 3 ? 32768u : kRankNodeB;
+constexpr uint32_t kNodeB = P16 == 3 ? 32768u : (P16 == 4 ? 0u : kRankNodeB);
+template <int P16>
+__device__ __forceinline__ uint32_t plane_addr(uint32_t nd, uint32_t lane_base) {
+    if constexpr (P16 == 4)
+        return ((nd & 0xF800u) << 1) + lane_base;
+    else
+        return (nd & kSlotMask<P16>) | lane_base;
+}
 
 // Compact planes (P16 = 3) are read a DWORD at a time: the lane's u16 rank is the low half
 // (lanes 0-31 of the wave) or the high half (lanes 32-63) of the dword it shares with lane
@@ -231,7 +246,7 @@ __device__ __forceinline__ void rank_step(const char *lds, const uint32_t (&lane
     uint32_t x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        x[k] = rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]);
+        x[k] = rank_x<P16>(lds, plane_addr<P16>(nd[k], lane_base[k]));
         if (P16 == 3) x[k] = (x[k] >> (16u - sh)) & 0xFFFFu;  // this lane's half
     }
 #pragma unroll
@@ -300,7 +315,7 @@ __device__ __forceinline__ void il_node1(uint32_t &p0, uint32_t x0, uint32_t n0)
 template <int P16, int K, int PW>
 __device__ __forceinline__ int rank_walk_pipe(const char *lds, const uint32_t (&lane_base)[K], uint32_t (&pa)[K],
                                               uint32_t (&nd)[K], int depth, int pre = 0) {
-    auto fetch_x = [&](int k) -> uint32_t { return rank_x<P16>(lds, (nd[k] & kSlotMask<P16>) | lane_base[k]); };
+    auto fetch_x = [&](int k) -> uint32_t { return rank_x<P16>(lds, plane_addr<P16>(nd[k], lane_base[k])); };
     const uint32_t sh = plane_shift<P16>();
     uint32_t x[K];
 #pragma unroll
@@ -625,12 +640,18 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     const uint8_t *__restrict__ mleft, double *__restrict__ acc, double *__restrict__ proba,
     const int32_t *__restrict__ out_perm, int32_t *__restrict__ leaf_out, const int32_t *__restrict__ orig,
     int32_t n_trees, int first, int last, const int32_t *__restrict__ chunk_t,
-    const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n, int32_t persist) {
-    // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots
+    const int64_t *__restrict__ chunk_base, double *__restrict__ tv, int64_t tv_n, int32_t persist,
+    int32_t n_slots) {
+    // u32 planes: 1,024 rows x 16 slots; v2: u16, 1,024 rows x 32 slots; compact v2: u16, 16 slots;
+    // paired v2 (P16 = 4): n_slots dword planes of 1,024 lanes x 2 rows at the top of the LDS
     constexpr int kPlaneRows = kRankPlaneRows;
-    constexpr int kRowU16 = P16 == 2 ? 32 : 16;  // u16 slots per rank row in HBM
-    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS
+    constexpr int kRowU16 = (P16 == 2 || P16 == 4) ? 32 : 16;  // u16 slots per rank row in HBM
+    constexpr int kXW = P16 == 3 ? kRankXWords / 2 : kRankXWords;  // row-plane words in LDS (below the nodes)
+    constexpr int kNodeW0 = P16 == 4 ? 0 : kXW;                    // first node word
     constexpr uint32_t kNB = kNodeB<P16>;
+    static_assert(P16 != 4 || (R == 2 && BLOCK == kPlaneRows), "paired planes: two rows per lane, 1,024 lanes");
+    // paired planes: plane s at byte pb + 4,096 s (uniform)
+    const uint32_t pb = P16 == 4 ? (uint32_t)(kLdsTotal - 4096 * n_slots) & ~15u : 0u;
     if (tv) {  // all chunks at once (blockIdx.y = chunk): per-tree values out, summed by k_tree_sum
         const int c = blockIdx.y;
         t0 = chunk_t[c];
@@ -640,13 +661,12 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         first = 1;
         last = 0;
     }
-    static_assert(BLOCK * R <= kPlaneRows, "row planes hold 1024 (u32) / 2048 (u16) rows");
+    static_assert(BLOCK * R <= kPlaneRows * (P16 == 4 ? 2 : 1), "row planes hold 1024 rows (2048 paired)");
     static_assert(BLOCK % 64 == 0, "whole waves (the u16 plane swizzle)");
     constexpr int K = R * G;  // chains per lane of one walk group
     (void)K;
     constexpr int kRowsPerBlock = BLOCK * R;
-    constexpr int kNodeWords = (kLdsTotal - kXW * 4) / 4;
-    __shared__ __align__(16) uint32_t s_mem[kXW + kNodeWords];
+    __shared__ __align__(16) uint32_t s_mem[kLdsTotal / 4];
     uint32_t *s_x = s_mem;
     const char *lds = reinterpret_cast<const char *>(s_mem);
     const int tid = threadIdx.x;
@@ -664,10 +684,10 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         const uint32_t *nb = nodes + node_base;
         if constexpr (CL) {  // (rolled: the chunk loop's registers are tight)
 #pragma unroll 1
-            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kNodeW0 + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
         } else {  // several loads in flight: with one tile per block (small batches) the fill is a
                   // large share of a block's work (rolled: stream micro-batches +8 us, r05bp)
-            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kXW + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kNodeW0 + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
         }
     };
     fill_nodes();
@@ -684,11 +704,31 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     // groups -- and the 32 lanes of a group read 32 different banks whatever features they test
     // (natural order put rows 2i, 2i+1 in one group: a 2-way conflict whenever their features
     // differ).  u32 planes are conflict-free in natural order.
+    // (paired planes: the lane's own dword, natural order -- 64 lanes, 64 banks)
     const int pslot = (P16 == 2 || P16 == 3) ? ((tid & ~63) | ((tid & 31) << 1) | ((tid >> 5) & 1)) : tid;
     uint32_t lrow[R];
 #pragma unroll
     for (int r = 0; r < R; ++r)  // compact planes: the byte address of the dword holding the lane's u16
-        lrow[r] = (uint32_t)(P16 == 3 ? ((r * BLOCK + pslot) & ~1) * 2 : (r * BLOCK + pslot) * (P16 ? 2 : 4));
+        lrow[r] = P16 == 4 ? pb + (uint32_t)tid * 4u + 2u * r
+                           : (uint32_t)(P16 == 3 ? ((r * BLOCK + pslot) & ~1) * 2 : (r * BLOCK + pslot) * (P16 ? 2 : 4));
+    // paired planes: the lane's two rank rows (32 u16 slots each, as q0..q3 hold them) as n_slots
+    // dwords, row 0 in the low halves
+    auto stage_paired = [&](const uint4 (&a0)[R], const uint4 (&a1)[R], const uint4 (&a2)[R], const uint4 (&a3)[R]) {
+        if constexpr (P16 == 4) {
+            const uint32_t u[16] = {a0[0].x, a0[0].y, a0[0].z, a0[0].w, a1[0].x, a1[0].y, a1[0].z, a1[0].w,
+                                    a2[0].x, a2[0].y, a2[0].z, a2[0].w, a3[0].x, a3[0].y, a3[0].z, a3[0].w};
+            const uint32_t v[16] = {a0[1].x, a0[1].y, a0[1].z, a0[1].w, a1[1].x, a1[1].y, a1[1].z, a1[1].w,
+                                    a2[1].x, a2[1].y, a2[1].z, a2[1].w, a3[1].x, a3[1].y, a3[1].z, a3[1].w};
+            uint32_t *pl = s_mem + (pb >> 2) + tid;
+#pragma unroll
+            for (int f = 0; f < 32; ++f) {
+                if (f >= n_slots) break;  // (uniform)
+                const uint32_t w = (f & 1) ? __builtin_amdgcn_perm(v[f >> 1], u[f >> 1], 0x07060302u)   // high halves
+                                           : __builtin_amdgcn_perm(v[f >> 1], u[f >> 1], 0x05040100u);  // low halves
+                pl[f * kPlaneRows] = w;
+            }
+        }
+    };
     const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
     int64_t base = r0 + (int64_t)blockIdx.x * kRowsPerBlock;
     uint4 q0[R], q1[R], q2[R], q3[R];
@@ -701,7 +741,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             const uint4 *src = reinterpret_cast<const uint4 *>(zr + (okr ? rw : r0) * kRowU16);
             q0[r] = src[0];
             q1[r] = src[1];
-            if (P16 == 2) {
+            if (P16 == 2 || P16 == 4) {
                 q2[r] = src[2];
                 q3[r] = src[3];
             }
@@ -718,7 +758,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
             const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(zr) + ro * (kRowU16 * 2u));
             q0[r] = src[0];
             q1[r] = src[1];
-            if (P16 == 2) {
+            if (P16 == 2 || P16 == 4) {
                 q2[r] = src[2];
                 q3[r] = src[3];
             }
@@ -808,11 +848,13 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
         double a[R];
         int32_t dst[R];
         auto stage_tile = [&]() {
+            stage_paired(q0, q1, q2, q3);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 row[r] = (uint32_t)(base + r * BLOCK + tid);
                 ok[r] = row[r] < (uint32_t)r1;
-                if constexpr (P16 == 2) {
+                if constexpr (P16 == 4) {
+                } else if constexpr (P16 == 2) {
                     const uint32_t w16[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                               q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
@@ -897,16 +939,18 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     }
     // the generic tile loop (leaf ids, per-tree values, chunks of more trees than one group):
     // two rows per lane walk groups of 3 trees (6 chains) to stay within the register budget
-    constexpr int GG = R == 2 ? 3 : G;
+    constexpr int GG = R == 2 ? (G < 3 ? G : 3) : G;
     for (; base < r1; base += stride) {
         int64_t row[R];
         bool ok[R];
         double a[R];
+        stage_paired(q0, q1, q2, q3);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             row[r] = base + r * BLOCK + tid;
             ok[r] = row[r] < r1;
-            if constexpr (P16 == 2) {
+            if constexpr (P16 == 4) {
+            } else if constexpr (P16 == 2) {
                 const uint32_t w[16] = {q0[r].x, q0[r].y, q0[r].z, q0[r].w, q1[r].x, q1[r].y, q1[r].z, q1[r].w,
                                         q2[r].x, q2[r].y, q2[r].z, q2[r].w, q3[r].x, q3[r].y, q3[r].z, q3[r].w};
 #pragma unroll
@@ -989,7 +1033,7 @@ namespace fdx {
 namespace {
 int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st);
 // node format a variant runs on: 1 = rank layout v1, 2 = v2
-int variant_format(const Variant &v) { return v.p16 == 2 || v.p16 == 3 ? 2 : 1; }
+int variant_format(const Variant &v) { return v.p16 >= 2 ? 2 : 1; }
 int forest_format(const fdx_forest_s *F) { return F->rank_v2 ? 2 : 1; }
 int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F->variant].group : 4; }
 
@@ -999,7 +1043,8 @@ int variant_group(const fdx_forest_s *F) { return F->zstride == 16 ? kVariants[F
 // (wide layout only: a rank-layout forest has every tree within the budget by construction).
 void build_chunks(fdx_forest_s *F) {
     const Variant v = F->zstride == 16 ? kVariants[F->variant] : kVariants[0];
-    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact : kRankNodeCap)
+    const int64_t cap_nodes = v.rank ? (v.p16 == 3 ? kRankNodeCapCompact
+                                                   : (v.p16 == 4 ? rank_node_cap_paired(F->rn_slots) : kRankNodeCap))
                                      : lds_node_bytes(F->zstride, v.block, v.rows) / 8;
     const int G = variant_group(F);
     const auto &off = v.rank ? F->rank_offsets : F->node_offsets;
@@ -1293,6 +1338,14 @@ extern "C" int fdx_forest_create(const fdx_forest_desc *d, fdx_forest *out, void
     F->variant = !F->rank_ok ? 0
                              : (!F->rank_v2 ? kDefaultRankVariant
                                             : (F->rank_identity ? kDefaultRankCompactVariant : kDefaultRankV2Variant));
+    if (F->variant == kDefaultRankV2Variant) {
+        // paired planes when every tree fits below the forest's slot planes: the deployed model
+        // (22 slots, one tree per chunk) 42.7 -> 39.2 ms for 20M rows (profiles/r06l_*)
+        bool fits = true;
+        for (int32_t t = 0; t < F->n_trees && fits; ++t)
+            fits = F->rank_offsets[t + 1] - F->rank_offsets[t] <= rank_node_cap_paired(F->rn_slots);
+        if (fits) F->variant = kPairedRankV2Variant;
+    }
     build_chunks(F);
     if ((e = hipMalloc(&F->nodes_d, sizeof(uint64_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&F->orig_d, sizeof(int32_t) * total)) != hipSuccess) return fail(e, "hipMalloc");
@@ -1410,7 +1463,7 @@ int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, dou
 // 10.16 vs 10.28 ms/step at configs[1], the 18 launches' drain and ramp gone
 // (profiles/r05ba_one_launch_ab.txt)
 static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
-    const int64_t row_bytes = kVariants[F->variant].p16 == 2 ? 64 : 32;  // (the kernel's 32-bit offsets)
+    const int64_t row_bytes = v2_rows(kVariants[F->variant].p16) ? 64 : 32;  // (the kernel's 32-bit offsets)
     bool ok = rank_mode(F) && !leaves && F->chunks.size() > 1 && n * row_bytes <= (int64_t)UINT32_MAX;
     for (const auto &ch : F->chunks) ok = ok && ch.t1 - ch.t0 <= std::min(8, kVariants[F->variant].group);
     return ok;
@@ -1419,7 +1472,7 @@ static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
 // output slots by 32-bit byte offsets, so a larger batch is walked range by range (128M rows at
 // 32-B rank rows), each launch over base pointers moved to its range.
 static int64_t rank_range_rows(const fdx_forest_s *F) {
-    const int64_t row_bytes = kVariants[F->variant].p16 == 2 ? 64 : 32;
+    const int64_t row_bytes = v2_rows(kVariants[F->variant].p16) ? 64 : 32;
     const int64_t rr = ((int64_t)UINT32_MAX / row_bytes) & ~(int64_t)1023;
     return F->range_rows > 0 ? std::min(rr, std::max<int64_t>(F->range_rows & ~(int64_t)1023, 1024)) : rr;
 }
@@ -1469,7 +1522,7 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
         if (nc > 1 && n <= concurrent_rows(F) && ws_bytes >= fdx_forest_workspace_size(F, n))
             tv = reinterpret_cast<double *>(reinterpret_cast<char *>(acc) + align_up(sizeof(double) * (size_t)n) + 256);
         const int64_t rr = tv ? n : rank_range_rows(F);
-        const int64_t row_u16 = kVariants[F->variant].p16 == 2 ? 32 : 16;
+        const int64_t row_u16 = v2_rows(kVariants[F->variant].p16) ? 32 : 16;
         for (int64_t q0 = 0; q0 < n; q0 += rr) {  // row ranges (one unless n > rank_range_rows)
         const int64_t qn = std::min(rr, n - q0);
         const uint16_t *zq = zr + q0 * row_u16;
@@ -1491,17 +1544,18 @@ static int forest_traverse(fdx_forest F, int64_t n, double *proba_d, const int32
             hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, true>), grid, dim3(B), 0, st, F->rnodes_d,      \
                                ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag,  \
                                (int64_t)0, qn, F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d,     \
-                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, persist);          \
+                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, persist, F->rn_slots);\
         else                                                                                                  \
             hipLaunchKernelGGL((k_forest_rank<B, R, G, P, PIPE, false>), grid, dim3(B), 0, st, F->rnodes_d,     \
                                ch.node_base, (int32_t)ch.nodes, F->rroot_d, F->rdepth_d, ch.t0, ch.t1, zq, flag,  \
                                (int64_t)0, qn, F->rlval_d, F->rml_d, accq, probaq, permq, leafq, F->rorig_d,     \
-                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, 0);                \
+                               F->n_trees, first, last, F->chunk_t_d, F->chunk_base_d, tv, n, 0, F->rn_slots);      \
     } while (0)
             switch (F->variant) {
                 case 2: FDX_LAUNCH_RANK(1024, 1, 6, 2, 2); break;
                 case 3: FDX_LAUNCH_RANK(1024, 1, 6, 3, 2); break;
                 case 4: FDX_LAUNCH_RANK(1024, 1, 10, 2, 2); break;
+                case 5: FDX_LAUNCH_RANK(1024, 2, 2, 4, 2); break;
                 default: FDX_LAUNCH_RANK(1024, 1, 10, 0, 102); break;
             }
 #undef FDX_LAUNCH_RANK

@@ -147,7 +147,10 @@ constexpr Variant kVariants[] = {
     {1024, 1, 6, 1, 2, 2},   // 2: rank layout v2 (forests v1 cannot hold: the deployed model)
     {1024, 1, 6, 1, 3, 2},   // 3: v2 nodes over 16 u16 planes (a third more nodes per LDS chunk)
     {1024, 1, 10, 1, 2, 2},  // 4: v2, 10 chains
+    {1024, 2, 2, 1, 4, 2},   // 5: v2 over paired planes (two rows per lane, the forest's slots only)
 };
+// the variant's rank rows in HBM are v2's 32 u16 slots (64 B)
+constexpr bool v2_rows(int p16) { return p16 == 2 || p16 == 4; }
 // (Round 6 measured and removed: speculative children -- the node's rank read AND both children's
 // reads issued together, one dependent LDS round trip per level for 3 reads instead of 2:
 // bit-exact, deployed model 42.4 -> 48.9 ms and bench model 6.57 -> 10.57 ms; the level-1 node
@@ -168,6 +171,7 @@ constexpr Variant kVariants[] = {
 constexpr int kDefaultRankVariant = 1;
 constexpr int kDefaultRankV2Variant = 2;
 constexpr int kDefaultRankCompactVariant = 3;
+constexpr int kPairedRankV2Variant = 5;  // the v2 default when every tree fits its node budget
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
@@ -175,6 +179,8 @@ constexpr int lds_node_bytes(int fs, int block, int rows) { return kLdsTotal - f
 
 constexpr int64_t kRankNodeCap = (kLdsTotal - kRankXWords * 4) / 4 - 1;  // - the parking leaf
 constexpr int64_t kRankNodeCapCompact = (kLdsTotal - kRankXWords * 2) / 4 - 1;  // 32 KiB of planes
+// paired planes (variant 5): n_slots planes of 4 KiB at the top of the LDS, nodes below them
+constexpr int64_t rank_node_cap_paired(int n_slots) { return ((kLdsTotal - 4096 * n_slots) & ~15) / 4 - 1; }
 
 // ---- shared helpers (definitions: fdx_forest_layout.cpp, fdx_forest.hip, fdx_assemble.hip)
 float round_down_f32(double t);  // largest float <= t

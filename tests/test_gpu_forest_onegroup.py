@@ -19,7 +19,7 @@ from forest_gen import random_forest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = [1, 2, 3, 4]  # v1 (10 chains per lane, interleaved pairs), v2 (6), compact v2 (6), v2 (10)
+VARIANTS = [1, 2, 3, 4, 5]  # v1 (10 chains per lane, interleaved pairs), v2 (6), compact v2 (6), v2 (10), paired v2
 
 
 def T(a, dt, dev):
@@ -148,7 +148,7 @@ def test_traverse_launch_count(dev, variant):
         return
     k = f.traverse_launches(big)
     assert k in (1, nc)
-    rows = (2**32 - 1) // (64 if variant in (2, 4) else 32) // 1024 * 1024
+    rows = (2**32 - 1) // (64 if variant in (2, 4, 5) else 32) // 1024 * 1024
     assert f.traverse_launches(rows) == k
     assert f.traverse_launches(rows + 1) == 2 * k
     assert f.traverse_launches(big, want_leaves=True) == nc
@@ -215,14 +215,14 @@ def test_prepare_row_major_spans(dev):
 
 def test_refused_variant_leaves_the_forest_intact(dev):
     """a refused set_variant must leave the forest as it was.  The deployed model
-    (rank layout v2, 22 threshold slots) cannot run v1 (a feature has 96k thresholds: the v1
+    (rank layout v2, 22 threshold slots; default variant 5, paired planes) cannot run v1 (a feature has 96k thresholds: the v1
     rebuild fails after the v2 buffers were freed) nor compact v2 (more slots than features);
     after each refusal the forest is back in v2 with its variant and chunks, and predict is
     still sklearn's on the notebook's test rows."""
     z = np.load(os.path.join(ROOT, "bench_assets", "rf_deployed.npz"))
     f = ops.Forest(_arrays(z), 15, z["mean"], z["scale"])
     v0, nc0 = f.variant, f.n_chunks
-    assert v0 == 2
+    assert v0 == 5  # paired planes: every tree fits below its 22 slot planes
     X = T(z["test_X"][:20_000], torch.float64, dev)
     want = z["test_proba1"][:20_000]
     for bad in (1, 3, 1):
@@ -232,7 +232,14 @@ def test_refused_variant_leaves_the_forest_intact(dev):
         np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
     f.set_variant(4)
     np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+    f.set_variant(5)  # paired planes: 22 slots at the top of the LDS, every tree below them
+    np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
+    Xn = z["test_X"][:20_000].copy()
+    Xn[np.random.default_rng(3).random(Xn.shape) < 0.02] = np.nan
     f.set_variant(2)
+    pn2 = f.predict(T(Xn, torch.float64, dev)).cpu().numpy()
+    f.set_variant(5)
+    np.testing.assert_array_equal(f.predict(T(Xn, torch.float64, dev)).cpu().numpy(), pn2)
     assert f.n_chunks == nc0
     np.testing.assert_array_equal(f.predict(X).cpu().numpy(), want)
 

@@ -352,7 +352,7 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     assert lay.n_slots <= n + (64 // len(windows)) * (np.diff(seg).max())
 
 
-@pytest.mark.parametrize("variant", list(range(5)))
+@pytest.mark.parametrize("variant", list(range(6)))
 def test_forest_variants_bit_identical(dev, golden, variant):
     """Every traversal kernel shape gives sklearn's leaves and probabilities."""
     z = golden("forest_rf3.npz")
