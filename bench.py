@@ -538,6 +538,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    mem0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
@@ -546,6 +547,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    mem1 = torch.cuda.memory_stats(dev)
+    # the caching allocator inside the timed steps: device allocations / frees / OOM retries there
+    # mean the steps paid hipMalloc / hipFree (each hipFree synchronises the device)
+    allocator = {k: int(mem1.get(k, 0) - mem0.get(k, 0)) for k in ("num_device_alloc", "num_device_free",
+                                                                  "num_alloc_retries")}
+    allocator.update(peak_reserved_GB=round(mem1.get("reserved_bytes.all.peak", 0) / 1e9, 2),
+                     peak_allocated_GB=round(mem1.get("allocated_bytes.all.peak", 0) / 1e9, 2),
+                     conf=os.environ.get("PYTORCH_HIP_ALLOC_CONF") or os.environ.get("PYTORCH_CUDA_ALLOC_CONF"))
     if world > 1:
         t = torch.tensor([dt, float(n_local)], dtype=torch.float64, device=cdev)
         dtm = t[:1].clone()
@@ -598,6 +607,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "setup_s": {"generate_on_gpu": round(t_gen, 2)},
+        "allocator_in_timed_steps": allocator,
         **({"rehearsal": "--rehearse-one-gpu: every rank on one GPU, host-staged gloo collectives; not a "
                          "measurement"} if args.rehearse_one_gpu else {}),
         "data": "synthetic: handbook-distribution generator on the GPU (fdx.synth.generate_device, seed 1234, "

@@ -49,6 +49,43 @@ def workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
+def _fresh(device):
+    """The default allocator of the ops below: a new tensor per call (torch's caching allocator)."""
+    return lambda _name, numel, dtype: torch.empty(max(int(numel), 0), dtype=dtype, device=device)
+
+
+class Arena:
+    """Device buffers kept across calls of a repeated step (FraudPipeline.run_fused): alloc(name,
+    numel, dtype) returns a view of the buffer `name`, reallocated only when a larger one is
+    needed, so a steady stream of same-sized steps allocates nothing.  At configs[3] on one GPU
+    (708M tx, ~240 GB live) the caching allocator otherwise freed and re-mapped blocks inside
+    every step (2 OOM retries and 14 hipMallocs per 3 steps: 2.5 s per step instead of ~0.5,
+    profiles/r06n_*).  The caller orders the reuse: a buffer is handed out again only to work
+    that the stream joins place after every use of its previous contents."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._buf = {}
+
+    def __call__(self, name: str, numel: int, dtype) -> torch.Tensor:
+        esz = torch.empty((), dtype=dtype).element_size()
+        nbytes = max(int(numel), 1) * esz
+        t = self._buf.get(name)
+        if t is None or t.numel() < nbytes:
+            self._buf.pop(name, None)  # (freed first: the old and the new one need not coexist)
+            t = self._buf[name] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return t[:int(numel) * esz].view(dtype)
+
+    def scope(self, prefix: str, shared=()):
+        """alloc for one call site: names get `prefix.`, except those in `shared` (buffers two call
+        sites may reuse because their uses are ordered, e.g. the two re-keys' scratch)."""
+        return lambda name, numel, dtype: self(name if name in shared else f"{prefix}.{name}", numel, dtype)
+
+    @property
+    def nbytes(self) -> int:
+        return sum(t.numel() for t in self._buf.values())
+
+
 def key_bits_for(n_keys: int) -> int:
     return max(int(n_keys) - 1, 0).bit_length()
 
@@ -82,13 +119,14 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
 
 
 def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
-                  flag: torch.Tensor | None = None, stream=None, seg_off: bool = True, bad: torch.Tensor | None = None):
+                  flag: torch.Tensor | None = None, stream=None, seg_off: bool = True, bad: torch.Tensor | None = None,
+                  alloc=None):
     """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
     grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
     bad (int32 device scalar): receives the number of keys outside [0, n_keys), counted in the
     first radix pass (fdx_rekey_payload_checked; see KeyRangeCheck.from_count).
     -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False), pay0 grouped | None,
-    pay1 grouped | None)."""
+    pay1 grouped | None).  alloc: see Arena (outputs "perm", "seg", "pay0", "pay1", scratch "rekey_ws")."""
     _dev(keys, torch.int32, "keys")
     n = keys.numel()
     dev = keys.device
@@ -101,12 +139,14 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
     if flag is not None:
         _dev(flag, torch.uint8, "flag")
     kb = max(key_bits_for(n_keys), 1)
-    perm = torch.empty(n, dtype=torch.int32, device=dev)
-    seg = torch.empty(n_keys + 1, dtype=torch.int64, device=dev) if seg_off else None
-    o0 = torch.empty_like(pay0) if pay0 is not None else None
-    o1 = torch.empty_like(pay1) if pay1 is not None else None
+    A = alloc or _fresh(dev)
+    perm = A("perm", n, torch.int32)
+    seg = A("seg", n_keys + 1, torch.int64) if seg_off else None
+    o0 = A("pay0", n, pay0.dtype) if pay0 is not None else None
+    o1 = A("pay1", n, pay1.dtype) if pay1 is not None else None
     L = _lib.load()
-    ws = workspace(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), dev)
+    ws = A("rekey_ws", max(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), 1),
+           torch.uint8)
     if bad is not None:
         _dev(bad, torch.int32, "bad")
         check(L.fdx_rekey_payload_checked(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1),
@@ -399,15 +439,16 @@ class PendingPlan:
     # it is enqueued at config 2 (behind the customer re-key), so the poll usually ends first
     SPIN_S = 5e-3
 
-    def __init__(self, seg_off, n_windows, stream):
+    def __init__(self, seg_off, n_windows, stream, alloc=None):
         self.seg_off, self.n_windows, self.stream = seg_off, int(n_windows), stream
         n_seg = seg_off.numel() - 1
         S = 64 // self.n_windows
         dev = seg_off.device
         L = _lib.load()
-        self.sorder = torch.empty(max(n_seg, 1), dtype=torch.int32, device=dev)
-        self.goff = torch.empty(-(-n_seg // S) + 1, dtype=torch.int32, device=dev)
-        self.ws = workspace(L.fdx_customer_layout_workspace_size(n_seg), dev)
+        A = alloc or _fresh(dev)
+        self.sorder = A("sorder", max(n_seg, 1), torch.int32)
+        self.goff = A("goff", -(-n_seg // S) + 1, torch.int32)
+        self.ws = A("plan_ws", max(L.fdx_customer_layout_workspace_size(n_seg), 1), torch.uint8)
         # [slot count, status], -1 until the stream's copy lands (result() polls for it)
         self.host = torch.full((2,), -1, dtype=torch.int32, pin_memory=True)
         self._hv = self.host.numpy()
@@ -437,14 +478,15 @@ class PendingPlan:
         return customer_layout_plan(self.seg_off, self.n_windows, self.stream)
 
 
-def customer_layout_plan_async(seg_off, n_windows: int, stream=None) -> PendingPlan:
-    """Enqueue the layout plan without waiting for it (see PendingPlan)."""
+def customer_layout_plan_async(seg_off, n_windows: int, stream=None, alloc=None) -> PendingPlan:
+    """Enqueue the layout plan without waiting for it (see PendingPlan; alloc: see Arena)."""
     _dev(seg_off, torch.int64, "seg_off")
-    return PendingPlan(seg_off, n_windows, stream)
+    return PendingPlan(seg_off, n_windows, stream, alloc)
 
 
-def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_days, stream=None) -> CustomerLayout:
-    """The second half: slots and window starts of a plan from GROUPED ts / amount."""
+def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_days, stream=None,
+                         alloc=None) -> CustomerLayout:
+    """The second half: slots and window starts of a plan from GROUPED ts / amount (alloc: see Arena)."""
     _dev(seg_off, torch.int64, "seg_off"); _dev(cperm, torch.int32, "cperm")
     _dev(gts, torch.int64, "ts_ns"); _dev(gamt, torch.float64, "amount")
     W = plan.n_windows
@@ -454,10 +496,11 @@ def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_da
     if m > (64 // W) * max(gts.numel(), 1):  # every group pads to its longest segment: <= S slots per row
         raise FdxError(f"customer layout: {m} slots for {gts.numel()} rows -- inconsistent segment offsets "
                        "(keys outside [0, n_keys)?)")
-    its = torch.empty(m, dtype=torch.int64, device=dev)
-    iamt = torch.empty(m, dtype=torch.float64, device=dev)
-    irow = torch.empty(m, dtype=torch.int32, device=dev)
-    starts = torch.empty(W * m, dtype=torch.int32, device=dev)
+    A = alloc or _fresh(dev)
+    its = A("its", m, torch.int64)
+    iamt = A("iamt", m, torch.float64)
+    irow = A("irow", m, torch.int32)
+    starts = A("starts", W * m, torch.int32)
     if m:
         check(_lib.load().fdx_customer_layout_fill_starts_grouped(
             _ptr(seg_off), seg_off.numel() - 1, _ptr(cperm), _ptr(gts), _ptr(gamt), _win_ns(windows_days), W,
@@ -466,15 +509,16 @@ def customer_layout_fill(plan: LayoutPlan, seg_off, cperm, gts, gamt, windows_da
     return CustomerLayout(plan.sorder, plan.goff, its, iamt, irow, m, starts, tuple(windows_days))
 
 
-def customer_windows_walk(lay: CustomerLayout, seg_off, stream=None):
+def customer_windows_walk(lay: CustomerLayout, seg_off, stream=None, alloc=None):
     """The windows of a layout built with windows_days: (nb int32 [W, n_slots], rolling SUM
-    float64 [W, n_slots]) indexed by slot."""
+    float64 [W, n_slots]) indexed by slot (alloc: see Arena)."""
     if lay.starts is None:
         raise FdxError("layout was built without window starts")
     W = len(lay.windows_days)
     dev = lay.its.device
-    nb = torch.empty((W, lay.n_slots), dtype=torch.int32, device=dev)
-    sm = torch.empty((W, lay.n_slots), dtype=torch.float64, device=dev)
+    A = alloc or _fresh(dev)
+    nb = A("nb", W * lay.n_slots, torch.int32).view(W, lay.n_slots)
+    sm = A("sum", W * lay.n_slots, torch.float64).view(W, lay.n_slots)
     if lay.n_slots == 0:
         return nb, sm
     check(_lib.load().fdx_customer_windows_walk(_ptr(lay.iamt), _ptr(seg_off), _ptr(lay.sorder), _ptr(lay.goff),
@@ -499,11 +543,11 @@ def customer_windows_interleaved(lay: CustomerLayout, seg_off, windows_days=(1, 
 
 
 def terminal_windows_compact(gts, seg_off, rows=None, gfraud=None, delay_days=7, windows_days=(1, 7, 30),
-                             runs: bool = False, stream=None):
+                             runs: bool = False, stream=None, alloc=None):
     """terminal_windows_grouped's count records by row in the COMPACT format (3 windows): an
     int64 [5 n] array, row r's 16-byte record at words [2 r, 2 r + 2), the overflow area
     [2 n, 5 n) (fdx.h fdx_terminal_windows_grouped_compact).  compact_records_unpack turns it
-    into the [n, 3] records."""
+    into the [n, 3] records (alloc: see Arena)."""
     _dev(gts, torch.int64, "gts"); _dev(seg_off, torch.int64, "seg_off")
     if rows is not None:
         _dev(rows, torch.int32, "rows")
@@ -514,8 +558,9 @@ def terminal_windows_compact(gts, seg_off, rows=None, gfraud=None, delay_days=7,
     if len(windows_days) != 3:
         raise FdxError("compact records hold 3 windows")
     n = gts.numel()
-    rec = torch.empty(max(5 * n, 2), dtype=torch.int64, device=gts.device)  # 256-byte aligned
-    scratch = torch.empty(max(n, 1), dtype=torch.int32, device=gts.device)
+    A = alloc or _fresh(gts.device)
+    rec = A("rec", max(5 * n, 2), torch.int64)  # 256-byte aligned
+    scratch = A("scratch", max(n, 1), torch.int32)
     check(_lib.load().fdx_terminal_windows_grouped_compact(_ptr(gts), _ptr(gfraud), _ptr(rows), _ptr(seg_off),
                                                            seg_off.numel() - 1, n, int(delay_days) * NS_PER_DAY,
                                                            _win_ns(windows_days), 3, int(bool(runs)), _ptr(rec),

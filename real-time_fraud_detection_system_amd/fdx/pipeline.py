@@ -172,8 +172,17 @@ class FraudPipeline:
             self._crit = torch.cuda.Stream(device=ts_ns.device, priority=self.crit_priority)
         main = self._crit if overlap else caller
         side = self._side if overlap else caller
+        # the step's intermediates live in an arena of the pipeline's own (ops.Arena): a repeated
+        # step allocates nothing; its buffers are reused by the next step, which the joins below
+        # order after every use (main waits for the caller and for the side stream's last step)
+        if getattr(self, "_arena", None) is None or self._arena.device != ts_ns.device:
+            self._arena = ops.Arena(ts_ns.device)
+        ar = self._arena
+        # the two re-keys' scratch is one buffer when the terminal re-key starts after the customer one
+        rk_shared = ("rekey_ws",) if self.terminal_after_customer_rekey else ()
         if main is not caller:
             main.wait_stream(caller)
+            main.wait_stream(side)
             for t in (ts_ns, customer, terminal, amount, fraud, proba) + ((ws,) if ws is not None else ()) + \
                 ((rows_out.buf,) if rows_out is not None else ()):
                 t.record_stream(main)
@@ -189,15 +198,17 @@ class FraudPipeline:
                 walk = W >= 3  # the two-kernel walk serves >= 3 windows; fewer use the one-pass ring kernel
                 # the id range checks ride on the re-keys' first histogram pass (bad counts), read once
                 # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
-                bad = torch.empty(2, dtype=torch.int32, device=ts_ns.device) if validate else None
+                bad = ar("bad", 2, torch.int32) if validate else None
                 cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
-                                                           bad=bad[0:1] if validate else None)
+                                                           bad=bad[0:1] if validate else None,
+                                                           alloc=ar.scope("cust", rk_shared))
                 mk("rekey_customer", main)
                 if self.terminal_after_customer_rekey:
                     side.wait_stream(main)
                 # the walk's layout plan goes right behind the re-key; its slot count is read only
                 # after the terminal half is enqueued (no host wait between the two)
-                pending = ops.customer_layout_plan_async(cseg, W, main) if (walk and not scan) else None
+                pending = ops.customer_layout_plan_async(cseg, W, main, alloc=ar.scope("plan")) \
+                    if (walk and not scan) else None
                 if validate:  # (its pinned copy behind the plan, not in front of it: up to 38 us)
                     rc = [ops.KeyRangeCheck.from_count(bad[0:1], n_customers, "customer ids", main)]
                 # terminal half (side stream): the re-key carries ts (and TX_FRAUD in bit 31 of the
@@ -208,13 +219,15 @@ class FraudPipeline:
                 with torch.cuda.stream(side):
                     mk("start", side)
                     tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side,
-                                                             bad=bad[1:2] if validate else None)
+                                                             bad=bad[1:2] if validate else None,
+                                                             alloc=ar.scope("term", rk_shared))
                     if validate:
                         rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
                     mk("rekey_terminal", side)
                     if compact:
                         trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
-                                                            windows_days=self.windows_days, stream=side)
+                                                            windows_days=self.windows_days, stream=side,
+                                                            alloc=ar.scope("trec"))
                     else:
                         trec = ops.terminal_windows_grouped(tgts, tseg, rows=tperm, delay_days=self.delay_days,
                                                             windows_days=self.windows_days, stream=side)
@@ -223,7 +236,8 @@ class FraudPipeline:
                     t.record_stream(side)  # inputs in use on the side stream
                 try:
                     if pending is not None:
-                        lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main)
+                        lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main,
+                                                       alloc=ar.scope("lay"))
                     else:
                         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,
                                                   self.windows_days if walk else None, grouped=True)
@@ -238,7 +252,7 @@ class FraudPipeline:
                 if scan:  # the windows straight from the grouped rows into the layout's slots
                     inb, isum = ops.customer_windows_scan(gts, gamt, cseg, self.windows_days, lay=lay, stream=main)
                 elif walk:
-                    inb, isum = ops.customer_windows_walk(lay, cseg, main)
+                    inb, isum = ops.customer_windows_walk(lay, cseg, main, alloc=ar.scope("walk"))
                 else:
                     inb, isum = ops.customer_windows_interleaved(lay, cseg, self.windows_days, main)
                 mk("customer_walk", main)

@@ -180,6 +180,51 @@ class StreamScorer:
         """Wait for the last batch's status bits and raise if it reported a problem."""
         self.state.poll(block=True)
 
+    def score_graph(self, ts, customer, amount, terminal, fraud, out_host=None, replay: bool = True):
+        """score() replayed from a HIP graph: the batch's kernels (state update, row assembly,
+        forest walk, tree sums), its status-word copy and -- with out_host (pinned, float64,
+        >= n) -- the probabilities' copy to the host are captured once per (batch size, buffer
+        addresses) and then launched as ONE graph per batch, so the host enqueues one call
+        instead of ~10 (fused mode only).  Inputs must live at the same addresses on every call
+        with that size (a consumer's staging buffers).  Same results and status semantics as
+        score(); -> the device view of the probabilities.  replay=False: capture only (a consumer
+        that knows its batch sizes captures them before the first batch arrives)."""
+        if not self.fused:
+            raise FdxError("score_graph needs the fused scorer")
+        if replay:
+            self.state.poll()
+        n = ts.numel()
+        key = (n,) + tuple(t.data_ptr() for t in (ts, customer, amount, terminal, fraud)) + \
+            ((out_host.data_ptr(),) if out_host is not None else ())
+        graphs = self.__dict__.setdefault("_graphs", {})
+        g = graphs.get(key)
+        if g is None:
+            st = self.state
+            if getattr(st, "_pin", None) is None:  # watch()'s pinned status word, captured below
+                st._pin = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                st._ev = torch.cuda.Event()
+            W = st.W
+            cnb, csum = self.cnb[:W * n].view(W, n), self.csum[:W * n].view(W, n)
+            trec = self.trec[:n * W].view(n, W)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st.update(ts, customer, amount, terminal, fraud, term_records=trec, cust_nb=cnb, cust_sum=csum)
+                ops.forest_prepare_grouped(self.forest, self.flags_mode, ts, amount, cnb, csum, None, None, trec,
+                                           self.ws, n=n, val_is_sum=True)
+                ops.forest_traverse(self.forest, n, self.ws, self.proba[:n])
+                check(_lib.load().fdx_stream_status_async(st._h, ctypes.c_void_p(st._pin.data_ptr()), ops._s()),
+                      "fdx_stream_status_async")
+                if out_host is not None:
+                    out_host[:n].copy_(self.proba[:n], non_blocking=True)
+            graphs[key] = g
+        if not replay:
+            return None
+        g.replay()
+        self.state._ev.record(torch.cuda.current_stream())
+        self.state._watching = True
+        return self.proba[:n]
+
     def score_cdc(self, tx_id, customer_id, terminal_id, amount_bytes, amount_offsets, tx_datetime_us, kafka_ts,
                   fraud=None):
         """One Debezium micro-batch scored from its wire columns, device-resident end to end --

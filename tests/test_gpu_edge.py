@@ -193,3 +193,48 @@ def test_sharded_rank_without_rows(dev, golden):
         assert X.shape == (0, 15)
     finally:
         dist.destroy_process_group()
+
+
+def test_arena_reuse_across_steps(dev, golden):
+    """run_fused keeps its intermediates in an arena of the pipeline's own (ops.Arena): steps of
+    different sizes enqueued back to back on one pipeline (the arena grows, then serves smaller
+    steps from larger buffers, the two re-keys share one scratch buffer) give every table the
+    probabilities and featurized table of a fresh pipeline; a steady run allocates nothing."""
+    from fdx import synth
+
+    forest, _, _ = _forest(golden)
+    tabs = [synth.generate_device(n_c, 2 * n_c, days, seed=s, device=dev)
+            for n_c, days, s in ((3000, 60, 1), (800, 20, 2), (3000, 60, 3))]
+    n_max = max(g["ts"].numel() for g in tabs)
+    ws = ops.workspace(forest.workspace_size(n_max * 2 + 4096), dev)
+    want = []
+    for g in tabs:  # fresh pipeline per table
+        n = g["ts"].numel()
+        p = torch.empty(n, dtype=torch.float64, device=dev)
+        rows = ops.FeatureTable(n * 2 + 4096, dev)
+        pf = FraudPipeline(forest=forest)
+        pf.run_fused(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 3000, 6000, p, ws, rows_out=rows)
+        torch.cuda.synchronize()
+        want.append((p.cpu().numpy(), table_as_X(rows, pf.last_slots, g["amount"].cpu().numpy())))
+    pipe = FraudPipeline(forest=forest)
+    outs = []
+    for g in tabs + tabs:  # no host synchronisation between the steps
+        n = g["ts"].numel()
+        p = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+        rows = ops.FeatureTable(n * 2 + 4096, dev)
+        pipe.run_fused(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 3000, 6000, p,
+                       ops.workspace(forest.workspace_size(n * 2 + 4096), dev), rows_out=rows)
+        outs.append((p, rows, pipe.last_slots, g))
+    torch.cuda.synchronize()
+    for k, (p, rows, slots, g) in enumerate(outs):
+        np.testing.assert_array_equal(p.cpu().numpy(), want[k % 3][0], err_msg=f"step {k}")
+        assert_same_features(table_as_X(rows, slots, g["amount"].cpu().numpy()), want[k % 3][1], f"step {k}")
+    nb = pipe._arena.nbytes
+    g = tabs[0]
+    p = torch.empty(g["ts"].numel(), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    stats0 = torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
+    pipe.run_fused(g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 3000, 6000, p, ws)
+    torch.cuda.synchronize()
+    assert pipe._arena.nbytes == nb
+    assert torch.cuda.memory_stats(dev).get("num_device_alloc", 0) == stats0

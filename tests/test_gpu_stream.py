@@ -230,3 +230,41 @@ def test_stream_scorer_raises_without_explicit_check(dev, golden):
     sc.score(*args)
     with pytest.raises(_lib.FdxUnsupported, match="ring overflow"):
         sc.finish()
+
+
+def test_stream_scorer_graph_equals_score(dev, golden):
+    """score_graph (one HIP graph per batch size: the state update, row assembly, forest walk,
+    status copy and the probabilities' copy to pinned host memory) == score(), batch for batch:
+    inputs staged through one device buffer (fixed addresses), a ragged last batch (a second
+    graph), one size captured before use; and a ring overflow in a graphed batch still raises."""
+    g, cols = _golden_cols(golden)
+    n = len(cols["ts"])
+    forest = _forest(golden)
+    n_c, n_t = int(cols["customer"].max()) + 1, int(cols["terminal"].max()) + 1
+    ref_sc = StreamScorer(forest, n_c, n_t, max_batch=2048)
+    sc = StreamScorer(forest, n_c, n_t, max_batch=2048)
+    keys = (("ts", torch.int64), ("customer", torch.int32), ("amount", torch.float64), ("terminal", torch.int32),
+            ("fraud", torch.uint8))
+    stage = {k: torch.empty(2048, dtype=dt, device=dev) for k, dt in keys}
+    out_h = torch.empty(2048, dtype=torch.float64).pin_memory()
+    sc.score_graph(*(stage[k][:2048] for k, _ in keys), out_host=out_h, replay=False)
+    for a in range(0, n, 2048):
+        b = min(a + 2048, n)
+        args = [T(cols[k][a:b], dt, dev) for k, dt in keys]
+        want = ref_sc.score(*args).cpu().numpy()
+        for (k, _), t in zip(keys, args):
+            stage[k][:b - a].copy_(t)
+        p = sc.score_graph(*(stage[k][:b - a] for k, _ in keys), out_host=out_h)
+        torch.cuda.current_stream().synchronize()
+        np.testing.assert_array_equal(p.cpu().numpy(), want)
+        np.testing.assert_array_equal(out_h[:b - a].numpy(), want)
+    assert len(sc._graphs) == (1 if n % 2048 == 0 else 2)
+    sc.finish()
+    small = StreamScorer(forest, 4, 4, customer_ring=4, terminal_ring=4, max_batch=64)
+    base = 1_717_200_000_000_000_000
+    ts = base + np.arange(10, dtype=np.int64) * 3_600 * 10**9
+    z = np.zeros(10, np.int32)
+    small.score_graph(T(ts, torch.int64, dev), T(z, torch.int32, dev), T(np.ones(10), torch.float64, dev),
+                      T(z, torch.int32, dev), T(np.zeros(10), torch.uint8, dev))
+    with pytest.raises(_lib.FdxUnsupported, match="ring overflow"):
+        small.finish()
