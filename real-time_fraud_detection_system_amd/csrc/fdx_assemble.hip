@@ -533,33 +533,55 @@ __global__ void __launch_bounds__(kPrepStBlock) k_prepare_st(const double *__res
                                                               int32_t *__restrict__ nan_flag, RankTab rt) {
     __shared__ float s_smp[kMaxRankSamples];
     __shared__ __align__(16) float s_t[kW3TreeFloats];
+    __shared__ uint16_t s_itab[16 * kIntTab];
     for (int e = threadIdx.x; e < rt.n_etab / 4; e += blockDim.x)
         reinterpret_cast<float4 *>(s_t)[e] = reinterpret_cast<const float4 *>(rt.etab)[e];
-    stage_samples(s_smp, rt);  // (its barrier covers the S-trees too)
+    for (int e = threadIdx.x; e < 16 * kIntTab; e += blockDim.x) s_itab[e] = rt.itab[e];
+    stage_samples(s_smp, rt);  // (its barrier covers the S-trees and the integer table too)
     const int e_lmax = max(max(rt.elev[0], rt.elev[1]), max(rt.elev[2], rt.elev[3]));
     uint32_t others = (1u << nf) - 1u;
 #pragma unroll
     for (int s = 0; s < 4; ++s) others &= ~(1u << kW3Search[s]);
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         float v[16];
+        uint32_t q[16];
+        uint32_t need = others;
         bool nan = false;
+        double xp = -1.0;  // the previous column's raw value
 #pragma unroll
         for (int f = 0; f < 16; ++f) {
+            q[f] = 0u;
             if (f < nf) {
-                double x = X[r * rs + (int64_t)f * cs];
+                const double x0 = X[r * rs + (int64_t)f * cs];
+                double x = x0;
                 if (mean) x = x - mean[f];
                 if (scale) x = x / scale[f];
                 v[f] = (float)x;
                 nan |= x != x;
+                // Exact shortcuts for the searched features, bit-identical to the search (the host
+                // built both tables with the same float64 scaling, float32 cast and lower_bound):
+                // a small non-negative integer (the flags and window counts of the reference's
+                // layout) -> RankTab::itab in LDS; a value that IS fr / nb for small integers with nb
+                // the previous column (the terminal risks after their counts) -> RankTab::rat (L2)
+                if ((others >> f) & 1u) {
+                    const bool pint = xp >= 0.0 && xp < (double)kRatN && xp == (double)(int32_t)xp;
+                    const int32_t nb = pint ? (int32_t)xp : 0;
+                    const int32_t fr = (int32_t)__builtin_rint(x0 * (double)nb);
+                    if (x0 >= 0.0 && x0 < (double)kIntTab && x0 == (double)(int32_t)x0) {
+                        q[f] = s_itab[f * kIntTab + (int32_t)x0];
+                        need &= ~(1u << f);
+                    } else if (pint && nb > 0 && fr >= 0 && fr <= nb && (double)fr / (double)nb == x0) {
+                        q[f] = rt.rat[((int64_t)f * kRatN + nb) * kRatN + fr];
+                        need &= ~(1u << f);
+                    }
+                }
+                xp = x0;
             } else {
                 v[f] = 0.0f;
             }
         }
         if (nan) *nan_flag = 1;
-        uint32_t q[16];
-#pragma unroll
-        for (int f = 0; f < 16; ++f) q[f] = 0u;
-        rank_row(v, nf, rt, s_smp, q, others);
+        rank_row(v, nf, rt, s_smp, q, need);
         int32_t ek[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
         float xs[4];  // the searched values, a NaN as 0 (see nan_free)
 #pragma unroll

@@ -276,3 +276,34 @@ def test_one_group_degenerate_depths(dev, kinds):
     for Xi in (np.nan_to_num(X, nan=0.5), X):
         p = f.predict(T(Xi, torch.float64, dev)).cpu().numpy()
         np.testing.assert_array_equal(p, oracle.forest_predict(Xi, arr))
+
+
+def test_prepare_integer_and_ratio_shortcuts(dev):
+    """fdx_forest_prepare (k_prepare_st) ranks a small non-negative integer through the integer
+    table and a value that is exactly fr / nb (nb = the previous column, a small integer) through
+    the ratio table -- the terminal counts and risks of the reference's layout.  Both must equal
+    the search bit for bit: the bench model's check rows, the same rows with every value moved one
+    ulp either way (no longer an integer / a ratio), -0.0, counts past the tables (256, 128), and
+    NaN, all against the wide-layout kernel and the oracle."""
+    z = np.load(os.path.join(ROOT, "bench_assets", "rf100_d20.npz"))
+    arr = _arrays(z)
+    f = ops.Forest(arr, 15, z["mean"], z["scale"])
+    g = ops.Forest(arr, 15, z["mean"], z["scale"])
+    g.set_variant(0)
+    rng = np.random.default_rng(8)
+    base = np.vstack([z["check_X"]] * 8)
+    up, dn = np.nextafter(base, np.inf), np.nextafter(base, -np.inf)
+    X = np.vstack([base, up, dn])
+    m = rng.random(X.shape) < 0.02
+    X[m] = -0.0
+    big = rng.random(len(X)) < 0.01
+    X[big, 9] = 256.0 + rng.integers(0, 3, big.sum())  # past both tables
+    X[big, 10] = np.round(X[big, 10] * X[big, 9]) / X[big, 9]
+    X[rng.random(X.shape) < 0.002] = np.nan
+    Xd = T(X, torch.float64, dev)
+    p = f.predict(Xd).cpu().numpy()
+    np.testing.assert_array_equal(p, g.predict(Xd).cpu().numpy())
+    sel = rng.choice(len(X), 3000, replace=False)
+    np.testing.assert_array_equal(p[sel], oracle.forest_predict(X[sel], arr, z["mean"], z["scale"]))
+    pc = f.predict(T(z["check_X"], torch.float64, dev)).cpu().numpy()  # unperturbed: sklearn's own output
+    np.testing.assert_array_equal(pc, z["check_proba"])
