@@ -58,6 +58,9 @@ class FraudPipeline:
     # the assembly and the forest on the terminal half's stream (the half that ends last), the NaN
     # flag cleared on the main stream beforehand (tools/step_ab.py measures it against 0)
     tail_on_side = 1
+    # the step's intermediates in the pipeline's own arena (ops.Arena; 0: torch's caching allocator
+    # per call, as before round 6 -- tools/step_ab.py measures the two)
+    use_arena = 1
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
@@ -177,7 +180,7 @@ class FraudPipeline:
         # order after every use (main waits for the caller and for the side stream's last step)
         if getattr(self, "_arena", None) is None or self._arena.device != ts_ns.device:
             self._arena = ops.Arena(ts_ns.device)
-        ar = self._arena
+        ar = self._arena if self.use_arena else _NoArena()
         # the two re-keys' scratch is one buffer when the terminal re-key starts after the customer one
         rk_shared = ("rekey_ws",) if self.terminal_after_customer_rekey else ()
         if main is not caller:
@@ -294,6 +297,16 @@ class FraudPipeline:
         if self._ws is None or self._ws.numel() < need:
             self._ws = ops.workspace(need, device)
         return self._ws
+
+
+class _NoArena:
+    """use_arena = 0: every alloc() a fresh tensor from torch's caching allocator."""
+
+    def __call__(self, _name, numel, dtype):
+        return torch.empty(max(int(numel), 1), dtype=dtype, device=torch.cuda.current_device())[:int(numel)]
+
+    def scope(self, _prefix, _shared=()):
+        return None  # (the ops allocate fresh tensors themselves)
 
 
 def check_rows_out(rows_out, ts_ns: torch.Tensor) -> None:
