@@ -451,7 +451,10 @@ int fdx_forest_traverse_launches(fdx_forest forest, int64_t n, int32_t with_leav
  *   1 = rank layout v1, 1,024 threads x 10 trees per lane (the default when the forest fits v1),
  *   2 = rank layout v2, 32 threshold slots (the default for forests v1 cannot hold),
  *   3 = v2 nodes over 16 compact u16 planes (every feature in one slot),
- *   4 = rank layout v2 with 10 trees per lane.
+ *   4 = rank layout v2 with 10 trees per lane,
+ *   5 = rank layout v2 over paired planes: two rows per lane, only the forest's threshold slots
+ *       staged (the v2 default when every tree fits the node budget left beside them: the
+ *       reference's deployed RF(100, unlimited depth), 22 slots).
  * Variants > 0 need <= 15 features (the rank rows' 16th slot is the v1 sentinel) and the
  * rank layout (FDX_E_UNSUPPORTED otherwise; a
  * refused call leaves the forest's node format, variant and chunks as they were).
