@@ -461,14 +461,14 @@ class PendingPlan:
         self.ev = torch.cuda.Event()
         self.ev.record(st)
 
-    def result(self) -> LayoutPlan:
+    def result(self, spin_s: float | None = None) -> LayoutPlan:
         if self.ok:
             # poll the pinned words for a bounded while before the blocking wait: the step's
             # critical stream idles until the host has read the slot count and launched the
             # layout fill, and waking from hipEventSynchronize took ~70 us (profiles/r03ad)
             # (bounded by wall time, not a poll count: a Python poll costs 0.1-0.2 us and holds the GIL)
             hv = self._hv
-            t_end = time.perf_counter() + self.SPIN_S
+            t_end = time.perf_counter() + (self.SPIN_S if spin_s is None else spin_s)
             while hv[0] == -1 or hv[1] == -1:
                 if time.perf_counter() > t_end:
                     self.ev.synchronize()

@@ -61,6 +61,11 @@ class FraudPipeline:
     # the step's intermediates in the pipeline's own arena (ops.Arena; 0: torch's caching allocator
     # per call, as before round 6 -- tools/step_ab.py measures the two)
     use_arena = 1
+    # how long the host polls for the layout plan's slot count before a blocking wait: the plan of
+    # step k lands only after step k - 1's forest (6.6 ms at configs[1]) when steps are queued back
+    # to back, and a blocking hipEventSynchronize woke up ~150 us after it (profiles/r06t trace: plan
+    # done at 0.64 ms, layout fill at 0.81 ms)
+    plan_spin_s = 0.05
 
     def __init__(self, windows_days: Sequence[int] = (1, 7, 30), delay_days: int = 7,
                  flags_mode: int = _lib.FDX_FLAGS_NOTEBOOK, forest: Optional[ops.Forest] = None,
@@ -239,7 +244,8 @@ class FraudPipeline:
                     t.record_stream(side)  # inputs in use on the side stream
                 try:
                     if pending is not None:
-                        lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, self.windows_days, main,
+                        lay = ops.customer_layout_fill(pending.result(self.plan_spin_s), cseg, cperm, gts, gamt,
+                                                       self.windows_days, main,
                                                        alloc=ar.scope("lay"))
                     else:
                         lay = ops.customer_layout(cseg, cperm, gts, gamt, W, main, self._slots_hint,

@@ -39,7 +39,8 @@ def main():
     args_ = (g["ts"], g["customer"], g["terminal"], g["amount"], g["fraud"], 50_000, 100_000, proba, ws)
     parsed = []
     for s in args.settings:
-        parsed.append({kv.split("=")[0]: int(kv.split("=")[1]) for kv in s.split(",")})
+        parsed.append({kv.split("=")[0]: (float if "." in kv.split("=")[1] else int)(kv.split("=")[1])
+                       for kv in s.split(",")})
     ref = None
     res = {s: [] for s in args.settings}
     for rnd in range(args.rounds):
