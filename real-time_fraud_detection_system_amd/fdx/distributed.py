@@ -296,15 +296,21 @@ class ShardedPipeline:
             state = exchange_begin(GpuKernels, terminal, self.world, self.group)
             mk("exchange_splits", side)
         cust = ops.key_map(customer, _lib.FDX_KEY_SUB, base) if base else customer
+        # the customer half's intermediates in the pipeline's arena (as FraudPipeline.run_fused; they
+        # are used on this stream only, so stream order is the reuse order)
+        if getattr(p, "_arena", None) is None or p._arena.device != ts.device:
+            p._arena = ops.Arena(ts.device)
+        ar = p._arena if p.use_arena else None
+        A = (lambda name: ar.scope("sh." + name)) if ar is not None else (lambda name: None)
         bad = torch.empty(1, dtype=torch.int32, device=ts.device)  # counted in the re-key's first pass
-        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount, bad=bad)
+        cperm, cseg, gts, gamt = ops.rekey_payload(cust, n_local, ts, amount, bad=bad, alloc=A("cust"))
         rc = ops.KeyRangeCheck.from_count(bad, n_local, "customer ids of this shard")  # read after the layout's sync
         mk("rekey_customer", main)
         scan = p.avg_mode == "scan"
         walk = W >= 3
         # the walk's layout plan right behind the re-key (no host wait): it runs while the host
         # waits for the exchange's split sizes below
-        pending = ops.customer_layout_plan_async(cseg, W) if (walk and not scan) else None
+        pending = ops.customer_layout_plan_async(cseg, W, alloc=A("plan")) if (walk and not scan) else None
         # the exchange's split-size sync waits only for the (short) owner re-key on the side
         # stream; enqueueing the whole exchange before the layout's host sync keeps the side
         # stream busy while the customer re-key runs
@@ -314,7 +320,8 @@ class ShardedPipeline:
                                               mark=lambda name: mk(name, side), stats=stats)
             sinv = ops.invert_perm(send_perm)   # local row -> send position (= reply record)
         if pending is not None:
-            lay = ops.customer_layout_fill(pending.result(), cseg, cperm, gts, gamt, p.windows_days)
+            lay = ops.customer_layout_fill(pending.result(p.plan_spin_s), cseg, cperm, gts, gamt, p.windows_days,
+                                           alloc=A("lay"))
         else:
             lay = ops.customer_layout(cseg, cperm, gts, gamt, W, None, p._slots_hint,
                                       p.windows_days if walk else None, grouped=True)  # (host sync on main)
@@ -325,7 +332,7 @@ class ShardedPipeline:
         if scan:
             inb, isum = ops.customer_windows_scan(gts, gamt, cseg, p.windows_days, lay=lay)
         elif walk:
-            inb, isum = ops.customer_windows_walk(lay, cseg)
+            inb, isum = ops.customer_windows_walk(lay, cseg, alloc=A("walk"))
         else:
             inb, isum = ops.customer_windows_interleaved(lay, cseg, p.windows_days)
         mk("customer_walk", main)
