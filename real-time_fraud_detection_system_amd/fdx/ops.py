@@ -656,6 +656,10 @@ class Forest:
         v = ctypes.c_int32()
         check(L.fdx_forest_get_variant(h, ctypes.byref(v)), "fdx_forest_get_variant")
         self.variant = v.value  # the library default (rank layout when the forest fits it)
+        # bumped by every call that may re-lay the device buffers (a refused set_variant re-installs
+        # the previous layout too): a captured HIP graph (StreamScorer.score_graph) holds their
+        # addresses and is captured again when the epoch moved
+        self.epoch = 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -664,6 +668,7 @@ class Forest:
             self._h = None
 
     def set_variant(self, variant: int) -> None:
+        self.epoch += 1
         L = _lib.load()
         check(L.fdx_forest_set_variant(self._h, int(variant)), "fdx_forest_set_variant")
         nt, nf, nn, nc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
@@ -673,6 +678,7 @@ class Forest:
 
     def set_range_rows(self, rows: int) -> None:
         """rows per traversal range (fdx_forest_set_range_rows; 0 = the default)"""
+        self.epoch += 1
         check(_lib.load().fdx_forest_set_range_rows(self._h, int(rows)), "fdx_forest_set_range_rows")
 
     def traverse_launches(self, n: int, want_leaves: bool = False) -> int:

@@ -185,7 +185,7 @@ class FraudPipeline:
         # order after every use (main waits for the caller and for the side stream's last step)
         if getattr(self, "_arena", None) is None or self._arena.device != ts_ns.device:
             self._arena = ops.Arena(ts_ns.device)
-        ar = self._arena if self.use_arena else _NoArena()
+        ar = self._arena if self.use_arena else _NoArena(ts_ns.device)
         # the two re-keys' scratch is one buffer when the terminal re-key starts after the customer one
         rk_shared = ("rekey_ws",) if self.terminal_after_customer_rekey else ()
         if main is not caller:
@@ -308,8 +308,11 @@ class FraudPipeline:
 class _NoArena:
     """use_arena = 0: every alloc() a fresh tensor from torch's caching allocator."""
 
+    def __init__(self, device):
+        self.device = device
+
     def __call__(self, _name, numel, dtype):
-        return torch.empty(max(int(numel), 1), dtype=dtype, device=torch.cuda.current_device())[:int(numel)]
+        return torch.empty(max(int(numel), 1), dtype=dtype, device=self.device)[:int(numel)]
 
     def scope(self, _prefix, _shared=()):
         return None  # (the ops allocate fresh tensors themselves)

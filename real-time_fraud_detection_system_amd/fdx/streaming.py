@@ -194,11 +194,13 @@ class StreamScorer:
         if replay:
             self.state.poll()
         n = ts.numel()
-        key = (n,) + tuple(t.data_ptr() for t in (ts, customer, amount, terminal, fraud)) + \
+        key = (n, self.forest.epoch) + tuple(t.data_ptr() for t in (ts, customer, amount, terminal, fraud)) + \
             ((out_host.data_ptr(),) if out_host is not None else ())
         graphs = self.__dict__.setdefault("_graphs", {})
         g = graphs.get(key)
         if g is None:
+            for k in [k for k in graphs if k[1] != self.forest.epoch]:
+                del graphs[k]  # captured over a forest layout that no longer exists
             st = self.state
             if getattr(st, "_pin", None) is None:  # watch()'s pinned status word, captured below
                 st._pin = torch.zeros(1, dtype=torch.int32, pin_memory=True)

@@ -260,6 +260,19 @@ def test_stream_scorer_graph_equals_score(dev, golden):
         np.testing.assert_array_equal(out_h[:b - a].numpy(), want)
     assert len(sc._graphs) == (1 if n % 2048 == 0 else 2)
     sc.finish()
+    # a forest whose layout changed (set_variant re-lays its device buffers) is captured again:
+    # the old graphs held the freed buffers' addresses
+    forest.set_variant(0)
+    sc2 = StreamScorer(forest, n_c, n_t, max_batch=2048)
+    ref2 = StreamScorer(forest, n_c, n_t, max_batch=2048)
+    args = [T(cols[k][:2048], dt, dev) for k, dt in keys]
+    for (k, _), t in zip(keys, args):
+        stage[k][:2048].copy_(t)
+    sc2.score_graph(*(stage[k][:2048] for k, _ in keys), out_host=out_h, replay=False)
+    forest.set_variant(forest.variant if forest.variant != 0 else 1)
+    p2 = sc2.score_graph(*(stage[k][:2048] for k, _ in keys), out_host=out_h).cpu().numpy()
+    np.testing.assert_array_equal(p2, ref2.score(*args).cpu().numpy())
+    assert len(sc2._graphs) == 1
     small = StreamScorer(forest, 4, 4, customer_ring=4, terminal_ring=4, max_batch=64)
     base = 1_717_200_000_000_000_000
     ts = base + np.arange(10, dtype=np.int64) * 3_600 * 10**9
