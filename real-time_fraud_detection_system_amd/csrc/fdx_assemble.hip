@@ -62,14 +62,22 @@ __device__ __forceinline__ void rank_row(const float (&v)[16], int nf, const Ran
             if (c > 0) {
                 const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
                 uint32_t k = 0;
-                if (rt.seg == 16) {  // (uniform) the segment's 4 loads in flight together: one round trip
-                    float4 w[4];
+                auto seg_count = [&](auto nq) {  // the segment's loads all in flight: one round trip
+                    constexpr int NQ = decltype(nq)::value;
+                    float4 w[NQ];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) w[q] = sg[q];
+                    for (int q = 0; q < NQ; ++q) w[q] = sg[q];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
+                    for (int q = 0; q < NQ; ++q)
                         k += (uint32_t)(w[q].x < v[f]) + (uint32_t)(w[q].y < v[f]) + (uint32_t)(w[q].z < v[f]) +
                              (uint32_t)(w[q].w < v[f]);
+                };
+                if (rt.seg == 16) {  // (uniform)
+                    seg_count(std::integral_constant<int, 4>{});
+                } else if (rt.seg == 32) {
+                    seg_count(std::integral_constant<int, 8>{});
+                } else if (rt.seg == 64) {  // (forests with ~300k thresholds: the deployed RF, rank layout v2)
+                    seg_count(std::integral_constant<int, 16>{});
                 } else {
                     for (int q = 0; q < rt.seg / 4; ++q) {
                         const float4 w = sg[q];
@@ -192,61 +200,62 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ X, i
     }
 }
 
-// rank of v in feature f (lower_bound over U_f), two-level search as rank_row, one feature
-__device__ __forceinline__ uint32_t rank_one(float v, int f, const RankTab &rt, const float *s_smp) {
-    int32_t lo = rt.soff[f], n = rt.scnt[f];
-    if (n <= 0) return 0u;
-    while (n > 1) {
-        const int32_t h = n >> 1;
-        lo = (s_smp[lo + h] < v) ? lo + h : lo;
-        n -= h;
-    }
-    const int32_t c = lo - rt.soff[f] + (s_smp[lo] < v ? 1 : 0);
-    if (c <= 0) return 0u;
-    const float4 *sg = reinterpret_cast<const float4 *>(rt.useg + rt.uoff[f] + (int64_t)(c - 1) * rt.seg);
-    uint32_t k = 0;
-    for (int q = 0; q < rt.seg / 4; ++q) {
-        const float4 w = sg[q];
-        k += (uint32_t)(w.x < v) + (uint32_t)(w.y < v) + (uint32_t)(w.z < v) + (uint32_t)(w.w < v);
-    }
-    return (uint32_t)(c - 1) * (uint32_t)rt.seg + k;
-}
-
 // Rank layout v2 rows: 32 u16 slots per row (64 B), slot s = the clamped rank of its
-// feature (build_rank_layout), 0xFFFF for a NaN feature; unused slots 0.
-__global__ void __launch_bounds__(256) k_prepare_v2(const double *__restrict__ X, int64_t n, int64_t rs, int64_t cs,
-                                                    int32_t nf, const double *__restrict__ mean,
-                                                    const double *__restrict__ scale, uint16_t *__restrict__ z,
-                                                    int32_t *__restrict__ nan_flag, RankTab rt) {
-    __shared__ float s_smp[kMaxRankSamples];
-    __shared__ __align__(16) uint16_t s_row[256][32];
-    stage_samples(s_smp, rt);
+// feature (build_rank_layout), 0xFFFF for a NaN feature; unused slots 0.  One 512-thread block
+// per CU (the v2 sample table, up to kMaxRankSamplesV2 floats, + the threads' slot rows in LDS;
+// the lockstep search of 15 features takes ~210 VGPRs: 1,024 threads spilled 208); every feature's
+// rank at once (rank_row: the searches advance together, each 16-float segment read in one round
+// trip), then the slots through the thread's LDS row.  (One feature after the other over 64-float
+// segments: 7.7 ms for 20M deployed-model rows, r06k.)
+constexpr int kPrepV2Block = 512;
+__global__ void __launch_bounds__(kPrepV2Block) k_prepare_v2(const double *__restrict__ X, int64_t n, int64_t rs,
+                                                             int64_t cs, int32_t nf, const double *__restrict__ mean,
+                                                             const double *__restrict__ scale, uint16_t *__restrict__ z,
+                                                             int32_t *__restrict__ nan_flag, RankTab rt) {
+    __shared__ float s_smp[kMaxRankSamplesV2];
+    __shared__ __align__(16) uint16_t s_row[kPrepV2Block][32];  // the thread's slot row (64 B)
+    __shared__ int32_t s_sf[32], s_sb[32];                       // slot -> feature, slot base
+    for (int i = threadIdx.x; i < rt.n_smp; i += blockDim.x) s_smp[i] = rt.smp[i];
+    if (threadIdx.x < 32) {
+        s_sf[threadIdx.x] = (int)threadIdx.x < rt.n_slots ? rt.slot_feat[threadIdx.x] : -1;
+        s_sb[threadIdx.x] = rt.slot_base[threadIdx.x];
+    }
+    __syncthreads();
     uint16_t *mine = s_row[threadIdx.x];
-    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = r0 + threadIdx.x;
-        if (r < n) {
-            bool any_nan = false;
-            for (int s = 0; s < 32; ++s) mine[s] = 0;
-            for (int f = 0; f < nf; ++f) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        bool any_nan = false;
+        float v[16];
+#pragma unroll
+        for (int f = 0; f < 16; ++f) {
+            v[f] = 0.0f;
+            if (f < nf) {
                 double x = X[r * rs + (int64_t)f * cs];
                 if (mean) x = x - mean[f];
                 if (scale) x = x / scale[f];
-                const float v = (float)x;
-                const bool isn = v != v;
-                any_nan |= isn;
-                const uint32_t rk = isn ? 0u : rank_one(v, f, rt, s_smp);
-                for (int s = 0; s < rt.n_slots; ++s) {
-                    if (rt.slot_feat[s] != f) continue;
-                    const int64_t c = (int64_t)rk - rt.slot_base[s];
+                v[f] = (float)x;
+                any_nan |= v[f] != v[f];
+            }
+        }
+        uint32_t rk[16];
+        rank_row(v, nf, rt, s_smp, rk, (1u << nf) - 1u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4 *>(mine)[q] = make_uint4(0, 0, 0, 0);
+        // slots in feature order (build_rank_layout): feature f's slots follow one another
+        int s = 0;
+#pragma unroll
+        for (int f = 0; f < 16; ++f) {
+            if (f < nf) {
+                const bool isn = v[f] != v[f];
+                for (; s < 32 && s_sf[s] == f; ++s) {  // (uniform)
+                    const int64_t c = (int64_t)rk[f] - s_sb[s];
                     mine[s] = isn ? (uint16_t)0xFFFFu : (uint16_t)(c < 0 ? 0 : (c > 32767 ? 32767 : c));
                 }
             }
-            if (any_nan) *nan_flag = 1;
-            const uint4 *src = reinterpret_cast<const uint4 *>(mine);
-            uint4 *dst = reinterpret_cast<uint4 *>(z + r * 32);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) dst[q] = src[q];
         }
+        if (any_nan) *nan_flag = 1;
+        uint4 *dst = reinterpret_cast<uint4 *>(z + r * 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = reinterpret_cast<const uint4 *>(mine)[q];
     }
 }
 
@@ -1050,8 +1059,10 @@ extern "C" int fdx_forest_prepare(fdx_forest F, const double *X_d, int64_t n, in
     FDX_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
     unsigned grid = stream_grid(n, 256);
     if (rank_mode(F) && v2_rows(kVariants[F->variant].p16)) {
-        hipLaunchKernelGGL(k_prepare_v2, dim3(grid), dim3(256), 0, st, X_d, n, row_stride, col_stride, F->n_features,
-                           F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
+        FDX_REQUIRE(F->rnsmp <= kMaxRankSamplesV2, "v2 sample table of %d floats exceeds the LDS budget", F->rnsmp);
+        const unsigned g2 = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kPrepV2Block), (int64_t)F->n_cu * 4);
+        hipLaunchKernelGGL(k_prepare_v2, dim3(g2), dim3(kPrepV2Block), 0, st, X_d, n, row_stride, col_stride,
+                           F->n_features, F->mean_d, F->scale_d, reinterpret_cast<uint16_t *>(z), flag, rank_tab(F));
         FDX_LAUNCHED("k_prepare_v2");
         return FDX_OK;
     }

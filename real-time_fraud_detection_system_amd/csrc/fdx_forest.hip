@@ -1207,7 +1207,7 @@ int install_rank_layout(fdx_forest_s *F, bool v2, hipStream_t st) {
     for (;; seg *= 2) {
         int64_t m = 0;
         for (int f = 0; f < nfs; ++f) m += ceil_div(F->rthr_cnt[f], seg);
-        if (m <= kMaxRankSamples) break;
+        if (m <= (v2 ? kMaxRankSamplesV2 : kMaxRankSamples)) break;
     }
     F->rseg = seg;
     for (int f = 0; f < nfs; ++f) {

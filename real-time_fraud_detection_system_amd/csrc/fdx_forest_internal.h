@@ -124,6 +124,9 @@ struct RankTab {
 };
 constexpr int kW3Search[4] = {0, 4, 6, 8};  // TX_AMOUNT, CUSTOMER_ID_AVG_AMOUNT_{1,7,30}DAY_WINDOW
 constexpr int kMaxRankSamples = 8192;  // LDS sample table of the prepare kernels (32 KiB)
+// rank layout v2 (only k_prepare_v2 reads its tables): 80 KiB of samples, so that the deployed
+// model's 313k thresholds take 16-float segments (64 B per feature and row) instead of 64-float ones
+constexpr int kMaxRankSamplesV2 = 20480;
 constexpr int kW3Gap = 4;              // thresholds per S-tree sample (one 16-byte segment read)
 constexpr int kW3TreeFloats = 28672;   // LDS budget of the S-trees (112 KiB)
 constexpr int kIntTab = 256;           // integer rank table entries per feature (8 KiB in LDS)
