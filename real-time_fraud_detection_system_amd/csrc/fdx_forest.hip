@@ -682,9 +682,17 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     if (persist > 0) chunk_params(0);
     auto fill_nodes = [&]() {
         const uint32_t *nb = nodes + node_base;
-        if constexpr (CL) {  // (rolled: the chunk loop's registers are tight)
+        if constexpr (CL) {  // 4 loads in flight per thread (the chunk loop's registers are tight):
+                             // the deployed model refills a one-tree chunk (~17k nodes) 100 times
 #pragma unroll 1
-            for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kNodeW0 + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
+            for (int i0 = tid; i0 < chunk_nodes; i0 += 4 * BLOCK) {
+                uint32_t v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = nb[min(i0 + j * BLOCK, chunk_nodes - 1)];  // (clamped: no branch)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (i0 + j * BLOCK < chunk_nodes) s_mem[kNodeW0 + i0 + j * BLOCK] = P16 ? v[j] ^ 0xFFFF0000u : v[j];
+            }
         } else {  // several loads in flight: with one tile per block (small batches) the fill is a
                   // large share of a block's work (rolled: stream micro-batches +8 us, r05bp)
             for (int i = tid; i < chunk_nodes; i += BLOCK) s_mem[kNodeW0 + i] = P16 ? nb[i] ^ 0xFFFF0000u : nb[i];
@@ -905,7 +913,7 @@ __global__ void __launch_bounds__(BLOCK, 1) k_forest_rank(
     // (9+ trees: register spills)
     auto one_chunk = [&]() {
 #define FDX_ONE_GROUP(NT) \
-    if constexpr (G >= NT) \
+    if constexpr (G >= NT && (!CL || NT <= kClMaxTrees)) \
         if (t1 - t0 == NT) one_group(std::integral_constant<int, NT>{});
         FDX_ONE_GROUP(1)
         FDX_ONE_GROUP(2)
@@ -1465,7 +1473,7 @@ int forest_ws(fdx_forest F, int64_t n, void *ws, size_t ws_bytes, float **z, dou
 static bool one_launch_ok(const fdx_forest_s *F, int64_t n, bool leaves) {
     const int64_t row_bytes = v2_rows(kVariants[F->variant].p16) ? 64 : 32;  // (the kernel's 32-bit offsets)
     bool ok = rank_mode(F) && !leaves && F->chunks.size() > 1 && n * row_bytes <= (int64_t)UINT32_MAX;
-    for (const auto &ch : F->chunks) ok = ok && ch.t1 - ch.t0 <= std::min(8, kVariants[F->variant].group);
+    for (const auto &ch : F->chunks) ok = ok && ch.t1 - ch.t0 <= std::min(kClMaxTrees, kVariants[F->variant].group);
     return ok;
 }
 // Rows per k_forest_rank row range: the one-group tile loop addresses rank rows, running sums and

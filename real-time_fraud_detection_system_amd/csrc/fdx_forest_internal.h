@@ -175,6 +175,9 @@ constexpr int kDefaultRankVariant = 1;
 constexpr int kDefaultRankV2Variant = 2;
 constexpr int kDefaultRankCompactVariant = 3;
 constexpr int kPairedRankV2Variant = 5;  // the v2 default when every tree fits its node budget
+// trees per chunk the one-launch chunk loop walks as one group: the bench forest's chunks hold <= 6
+// (3.9k-node trees in 94 KiB), and the loop instantiated for 7-8 as well spilled 17 VGPRs
+constexpr int kClMaxTrees = 6;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 constexpr int kLdsTotal = 160 * 1024 - 2048;  // leave room for the static bookkeeping
 
