@@ -67,8 +67,12 @@ class Arena:
         self.device = torch.device(device)
         self._buf = {}
 
+    _esz = {}
+
     def __call__(self, name: str, numel: int, dtype) -> torch.Tensor:
-        esz = torch.empty((), dtype=dtype).element_size()
+        esz = Arena._esz.get(dtype)
+        if esz is None:
+            esz = Arena._esz[dtype] = torch.empty((), dtype=dtype).element_size()
         nbytes = max(int(numel), 1) * esz
         t = self._buf.get(name)
         if t is None or t.numel() < nbytes:
@@ -258,11 +262,18 @@ def scatter(src: torch.Tensor, perm: torch.Tensor, out: torch.Tensor | None = No
 
 
 # --------------------------------------------------------------------------- windows
+_WIN_NS = {}
+
+
 def _win_ns(days: Sequence[int]):
-    days = [int(d) for d in days]
-    if not 1 <= len(days) <= _lib.MAX_WINDOWS:
-        raise FdxError(f"1..{_lib.MAX_WINDOWS} windows supported")
-    return (ctypes.c_int64 * len(days))(*[d * NS_PER_DAY for d in days])
+    key = tuple(days)
+    w = _WIN_NS.get(key)
+    if w is None:  # (built once per window set: the step's host path calls this several times)
+        days = [int(d) for d in days]
+        if not 1 <= len(days) <= _lib.MAX_WINDOWS:
+            raise FdxError(f"1..{_lib.MAX_WINDOWS} windows supported")
+        w = _WIN_NS[key] = (ctypes.c_int64 * len(days))(*[d * NS_PER_DAY for d in days])
+    return w
 
 
 def customer_windows(ts_ns, amount, seg_off, windows_days=(1, 7, 30), stream=None):
