@@ -9,7 +9,7 @@ assembly, takes the default kernel (k_forest_rank<1024, 1, 10, 0, 102>), and pri
 
 usage: python3 tools/isa_excerpt.py [out.txt] [v2]
   v2: the rank-layout-v2 chunk-loop instantiation the deployed model runs
-      (k_forest_rank<1024, 1, 6, 2, 2, true>: one-tree chunks, one chain per lane, u16 planes)
+      (k_forest_rank<1024, 2, 2, 4, 2, true>: paired planes, one-tree chunks, two rows per lane)
 """
 import collections
 import os
@@ -22,7 +22,7 @@ CSRC = os.path.join(ROOT, "real-time_fraud_detection_system_amd", "csrc")
 KERNEL = "k_forest_rankILi1024ELi1ELi10ELi0ELi102ELb1E"  # the chunk-loop instantiation (large batches)
 
 
-KERNEL_V2 = "k_forest_rankILi1024ELi1ELi6ELi2ELi2ELb1E"
+KERNEL_V2 = "k_forest_rankILi1024ELi2ELi2ELi4ELi2ELb1E"  # variant 5 (paired planes), the deployed default since r06
 
 
 def kernel_body(asm):
