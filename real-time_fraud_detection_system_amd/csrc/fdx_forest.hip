@@ -216,9 +216,12 @@ template <int P16>
 constexpr uint32_t kNodeB = P16 == 3 ? 32768u : (P16 == 4 ? 0u : kRankNodeB);
 template <int P16>
 __device__ __forceinline__ uint32_t plane_addr(uint32_t nd, uint32_t lane_base) {
-    if constexpr (P16 == 4)
-        return ((nd & 0xF800u) << 1) + lane_base;
-    else
+    if constexpr (P16 == 4) {
+        // 2 VALU (the compiler's own form was shift, and, add: 3 -- r06ag ISA)
+        uint32_t t, a;
+        asm("v_and_b32 %0, 0xf800, %2\n\tv_lshl_add_u32 %1, %0, 1, %3" : "=&v"(t), "=v"(a) : "v"(nd), "v"(lane_base));
+        return a;
+    } else
         return (nd & kSlotMask<P16>) | lane_base;
 }
 

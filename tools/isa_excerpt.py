@@ -76,7 +76,7 @@ def main():
                            os.path.join(CSRC, "fdx_forest.hip")])
     asm = open(asm_path).read()
     body, summ = kernel_body(asm)
-    res = [("k_forest_rank<1024, 1, 6, 2, 2, true> (variant 2, rank layout v2: the deployed model; chunk loop)" if v2 else
+    res = [("k_forest_rank<1024, 2, 2, 4, 2, true> (variant 5, rank layout v2 over paired planes: the deployed model; chunk loop)" if v2 else
             "k_forest_rank<1024, 1, 10, 0, 102, true> (default variant 1, chunk loop)") + ", gfx950, hipcc -O3",
            "register summary:"]
     res += ["  " + s for s in summ]
