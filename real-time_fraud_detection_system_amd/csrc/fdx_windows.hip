@@ -813,17 +813,40 @@ __global__ void __launch_bounds__(64) k_customer_walk(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (t0 + kChunk < Lw) fetch(t0 + kChunk);  // in flight while this chunk is walked
         const int32_t oldest = t0 + kChunk - kRing;  // first row still in the ring
+        // every row's amount and the first row it removes (its predecessor's start), read for the
+        // whole chunk before the walk: the reads leave the add/remove chain, which otherwise waited
+        // for an LDS round trip per row (the first removal from the miss slot stays in the loop)
+        double pv[kChunk], pr[kChunk];
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const int32_t r = j == 0 ? tail : cst[j - 1];
+            pv[j] = r_amt[((t0 + j) & (kRing - 1)) * S_MAX + l];
+            pr[j] = r_amt[r >= oldest ? (r & (kRing - 1)) * S_MAX + l : kRing * S_MAX + lane];
+        }
+        // (issued ahead of the next chunk's fetch: the branch around it keeps the compiler from
+        // sinking row 0's reads into row 0's block, behind a full wait)
+        if (t0 + kChunk < Lw) fetch(t0 + kChunk);  // in flight while this chunk is walked
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             const int32_t t = t0 + j;
             if (t < L) {
-                const double v = r_amt[(t & (kRing - 1)) * S_MAX + l];
+                const double v = pv[j];
                 const int32_t st = cst[j];
                 if (st >= t) {  // start[i] >= end[i-1] (or i == 0): pandas re-initialises
                     sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
                 } else {
+                    if (tail < st && tail >= oldest) {  // the first row leaving: read above
+                        const double a = pr[j];
+                        if (a == a) {
+                            nobs -= 1;
+                            const double y = -a - c_rem;
+                            const double tt = sum + y;
+                            c_rem = (tt - sum) - y;
+                            sum = tt;
+                        }
+                        tail += 1;
+                    }
                     for (int32_t k = tail; k < st; ++k) {  // rows leaving the window (Kahan remove)
                         int e = (k & (kRing - 1)) * S_MAX + l;
                         if (k < oldest) {  // older than the ring: via this lane's miss slot
