@@ -836,8 +836,8 @@ __global__ void __launch_bounds__(64) k_customer_walk(
                 if (st >= t) {  // start[i] >= end[i-1] (or i == 0): pandas re-initialises
                     sum = 0.0; c_add = 0.0; c_rem = 0.0; nobs = 0; nsame = 0; prev = v;
                 } else {
-                    if (tail < st && tail >= oldest) {  // the first row leaving: read above
-                        const double a = pr[j];
+                    // rows [tail, st) leave the window (Kahan remove, in row order)
+                    auto remove = [&](double a) {
                         if (a == a) {
                             nobs -= 1;
                             const double y = -a - c_rem;
@@ -845,21 +845,22 @@ __global__ void __launch_bounds__(64) k_customer_walk(
                             c_rem = (tt - sum) - y;
                             sum = tt;
                         }
-                        tail += 1;
-                    }
-                    for (int32_t k = tail; k < st; ++k) {  // rows leaving the window (Kahan remove)
-                        int e = (k & (kRing - 1)) * S_MAX + l;
-                        if (k < oldest) {  // older than the ring: via this lane's miss slot
-                            e = kRing * S_MAX + lane;
-                            r_amt[e] = g_amt[(int64_t)k * S];
-                        }
-                        const double a = r_amt[e];
-                        if (a == a) {
-                            nobs -= 1;
-                            const double y = -a - c_rem;
-                            const double tt = sum + y;
-                            c_rem = (tt - sum) - y;
-                            sum = tt;
+                    };
+                    int32_t k = tail;
+                    for (; k < st && k < oldest; ++k) remove(g_amt[(int64_t)k * S]);  // older than the ring (rare)
+                    if (k < st) {
+                        // the ring rows, software-pipelined and branch-free: the next row's amount is
+                        // read (in bounds whatever k) while this one is removed; the first was read
+                        // with the chunk unless out-of-ring rows came before it
+                        double a = k == tail ? pr[j] : r_amt[(k & (kRing - 1)) * S_MAX + l];
+                        // settle it here: a read carried into the loop as pending makes the wait-count
+                        // pass put lgkmcnt(0) -- the next read's too -- ahead of every trip's adds
+                        __builtin_amdgcn_s_waitcnt(0xC07F);
+                        for (; k < st; ++k) {
+                            const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
+                            __builtin_amdgcn_sched_barrier(0);  // keep the read ahead of the adds
+                            remove(a);
+                            a = an;
                         }
                     }
                 }
