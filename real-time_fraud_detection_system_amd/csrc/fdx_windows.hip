@@ -794,6 +794,9 @@ __global__ void __launch_bounds__(64) k_customer_walk(
                 if (t0 + j < L) pst[j] = nb[(int64_t)(t0 + j) * S];
         }
     };
+    // wave-uniform: has any amount this wave staged been NaN?  Every row a lane removes was staged
+    // before (ring or not), so until then the removes need no NaN select (5 of the loop's 14 VALU)
+    bool nan_seen = false;
     auto commit = [&](int32_t t0) {
         const int n_el = min(kChunk, Lw - t0) * Sw;
         const int ring0 = (t0 & (kRing - 1)) * S_MAX;
@@ -802,6 +805,10 @@ __global__ void __launch_bounds__(64) k_customer_walk(
             const int e = lane + j * kWave;  // past the chunk, a ring row may still hold a live older row
             r_amt[e < n_el ? ring0 + e_ring[j] : kRing * S_MAX + lane] = pam[j];
         }
+        bool nan_l = false;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) nan_l |= pam[j] != pam[j];
+        nan_seen |= __builtin_amdgcn_ballot_w64(nan_l) != 0;
     };
     double sum = 0.0, c_add = 0.0, c_rem = 0.0, prev = 0.0;
     int32_t nobs = 0, nsame = 0, tail = 0;
@@ -856,11 +863,24 @@ __global__ void __launch_bounds__(64) k_customer_walk(
                         // settle it here: a read carried into the loop as pending makes the wait-count
                         // pass put lgkmcnt(0) -- the next read's too -- ahead of every trip's adds
                         __builtin_amdgcn_s_waitcnt(0xC07F);
-                        for (; k < st; ++k) {
-                            const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
-                            __builtin_amdgcn_sched_barrier(0);  // keep the read ahead of the adds
-                            remove(a);
-                            a = an;
+                        if (!nan_seen) {
+                            for (; k < st; ++k) {
+                                const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
+                                __builtin_amdgcn_sched_barrier(0);  // keep the read ahead of the adds
+                                nobs -= 1;
+                                const double y = -a - c_rem;
+                                const double tt = sum + y;
+                                c_rem = (tt - sum) - y;
+                                sum = tt;
+                                a = an;
+                            }
+                        } else {
+                            for (; k < st; ++k) {
+                                const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
+                                __builtin_amdgcn_sched_barrier(0);
+                                remove(a);
+                                a = an;
+                            }
                         }
                     }
                 }

@@ -331,6 +331,27 @@ def test_customer_interleaved_layout_matches_oracle(dev, max_len, windows):
     """The pipeline's lane-major customer layout: same bits as the oracle for every row."""
     rng = np.random.default_rng(max_len + len(windows))
     ts, amt, _, seg = _edge_segments(rng, 700 if max_len < 1000 else 60, max_len)
+    _check_interleaved(dev, rng, ts, amt, seg, windows)
+
+
+@pytest.mark.parametrize("max_len", [300, 2500])
+def test_customer_walk_nan_amounts_matches_oracle(dev, max_len):
+    """NaN amounts (pandas leaves them out of count and sum) arriving mid-segment: a walk wave
+    takes the NaN-free remove loop until it first stages a NaN, the NaN-skipping one after; the
+    NaN rows then leave the windows from the LDS ring and, past 128 / 256 rows, from HBM.  -NaN
+    (sign bit set) in half the segments that get NaNs; two thirds of the segments get none."""
+    rng = np.random.default_rng(11 + max_len)
+    ts, amt, _, seg = _edge_segments(rng, 700 if max_len < 1000 else 60, max_len)
+    for s in range(0, len(seg) - 1, 3):
+        a, b = int(seg[s]), int(seg[s + 1])
+        if b - a >= 3:
+            pos = rng.integers(a + (b - a) // 3, b, size=max(1, (b - a) // 20))
+            amt[pos] = np.nan if s % 2 else np.copysign(np.nan, -1.0)
+    assert np.isnan(amt).any()
+    _check_interleaved(dev, rng, ts, amt, seg, (1, 7, 30))
+
+
+def _check_interleaved(dev, rng, ts, amt, seg, windows):
     n = len(ts)
     perm = rng.permutation(n).astype(np.int32)          # grouped position -> "time row"
     ts_time = np.empty_like(ts); ts_time[perm] = ts
