@@ -864,16 +864,26 @@ __global__ void __launch_bounds__(64) k_customer_walk(
                         // pass put lgkmcnt(0) -- the next read's too -- ahead of every trip's adds
                         __builtin_amdgcn_s_waitcnt(0xC07F);
                         if (!nan_seen) {
-                            for (; k < st; ++k) {
-                                const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
-                                __builtin_amdgcn_sched_barrier(0);  // keep the read ahead of the adds
-                                nobs -= 1;
-                                const double y = -a - c_rem;
+                            auto kahan = [&](double x) {
+                                const double y = -x - c_rem;
                                 const double tt = sum + y;
                                 c_rem = (tt - sum) - y;
                                 sum = tt;
-                                a = an;
+                            };
+                            nobs -= st - k;
+                            // two rows a trip, the next two read ahead of the eight adds (rows past st
+                            // are read in bounds and left unused)
+                            double a1 = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
+                            for (; k + 1 < st; k += 2) {
+                                const double n0 = r_amt[((k + 2) & (kRing - 1)) * S_MAX + l];
+                                const double n1 = r_amt[((k + 3) & (kRing - 1)) * S_MAX + l];
+                                __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the adds
+                                kahan(a);
+                                kahan(a1);
+                                a = n0;
+                                a1 = n1;
                             }
+                            if (k < st) kahan(a);
                         } else {
                             for (; k < st; ++k) {
                                 const double an = r_amt[((k + 1) & (kRing - 1)) * S_MAX + l];
