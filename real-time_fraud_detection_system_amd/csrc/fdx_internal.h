@@ -45,6 +45,13 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
         }                                                                                 \
     } while (0)
 
+// Integer min / max for device code.  HIP's min<int64_t>(a, b) with either argument not already
+// int64_t converts both to double (v_cvt + v_ldexp + v_min_f64 + v_cvt back): slow, and a VGPR
+// result where the operands were wave-uniform -- a buffer descriptor built from one made every
+// buffer store of k_customer_walk a readfirstlane loop.
+__device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ? a : b; }
+
 // Terminal count record word (fdx_terminal_windows_packed): NB | FRAUD << 32.
 __device__ __forceinline__ int64_t term_word(int32_t nb, int32_t fraud) {
     return (int64_t)(((uint64_t)(uint32_t)fraud << 32) | (uint32_t)nb);

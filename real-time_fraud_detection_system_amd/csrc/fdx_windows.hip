@@ -219,10 +219,10 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     if (tid == 0) s_nlong = 0;
     __syncthreads();
     const int64_t per = (n_seg + kPlanWaves - 1) / kPlanWaves;
-    const int64_t lo = wv * per, hi = min<int64_t>(n_seg, lo + per);
+    const int64_t lo = wv * per, hi = imin64(n_seg, lo + per);
     // (lengths clamped at 0: out-of-range ids, rejected after the step, can leave the offsets
     // out of order -- never an out-of-bounds counter)
-    auto len_of = [&](int64_t sg) -> int64_t { return max<int64_t>(seg_off[sg + 1] - seg_off[sg], 0); };
+    auto len_of = [&](int64_t sg) -> int64_t { return imax64(seg_off[sg + 1] - seg_off[sg], 0); };
     // 1. bins of this wave's chunks (kept in registers, two u16 per VGPR: 0xFFFF = none, 0 =
     // long), wave-private counts
     uint32_t binp[kPlanChunks / 2] = {};
@@ -232,22 +232,22 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     };
     constexpr int kBatch = 8;  // chunks whose offsets are loaded together (one load per segment:
                                 // the next offset comes from the next lane, lane 63 loads it)
-    const int n_chunks = (int)((max<int64_t>(hi - lo, 0) + kWave - 1) / kWave);  // this wave's
+    const int n_chunks = (int)((imax64(hi - lo, 0) + kWave - 1) / kWave);  // this wave's
 #pragma unroll
     for (int c0 = 0; c0 < kPlanChunks; c0 += kBatch) {
         if (c0 >= n_chunks) continue;  // (uniform; phase 3 skips these chunks too)
         int64_t a[kBatch], e63[kBatch];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
-            const int64_t sg = min<int64_t>(lo + (int64_t)(c0 + j) * kWave + lane, n_seg);
+            const int64_t sg = imin64(lo + (int64_t)(c0 + j) * kWave + lane, n_seg);
             a[j] = seg_off[sg];
-            e63[j] = lane == kWave - 1 ? seg_off[min<int64_t>(sg + 1, n_seg)] : 0;
+            e63[j] = lane == kWave - 1 ? seg_off[imin64(sg + 1, n_seg)] : 0;
         }
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             const int64_t sg = lo + (int64_t)(c0 + j) * kWave + lane;
             const int64_t nx = __shfl_down(a[j], 1, kWave);
-            const int64_t L = max<int64_t>((lane == kWave - 1 ? e63[j] : nx) - a[j], 0);
+            const int64_t L = imax64((lane == kWave - 1 ? e63[j] : nx) - a[j], 0);
             const int32_t bn = sg >= hi ? 0xFFFF : (L >= kPlanBins - 1 ? 0 : (int32_t)(kPlanBins - 1 - L));
             binp[(c0 + j) >> 1] |= (uint32_t)bn << (16 * ((c0 + j) & 1));
             if (sg < hi) {
@@ -294,11 +294,11 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     // long segments: exact rank by (length desc, index asc), lengths clamped as the radix key
     for (int i = tid; i < n_long; i += kT) {
         const int32_t si = s_long[i];
-        const int64_t li = min<int64_t>(len_of(si), 65535);
+        const int64_t li = imin64(len_of(si), 65535);
         int r = 0;
         for (int j = 0; j < n_long; ++j) {
             const int32_t sj = s_long[j];
-            const int64_t lj = min<int64_t>(len_of(sj), 65535);
+            const int64_t lj = imin64(len_of(sj), 65535);
             r += (lj > li) || (lj == li && sj < si);
         }
         sorder[r] = si;
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     __syncthreads();
     // 4. exclusive scan of the group slot counts (goff[n_groups] = total)
     const int64_t gper = (n_groups + kT - 1) / kT;
-    const int64_t g0 = tid * gper, g1 = min<int64_t>(n_groups, g0 + gper);
+    const int64_t g0 = tid * gper, g1 = imin64(n_groups, g0 + gper);
     uint32_t gs = 0;
     for (int64_t g = g0; g < g1; ++g) gs += s_gs[g];
     // (a wave scan, then the 16 wave totals: 1 barrier instead of 20)
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256) k_interleave(
                 x_rw[xi[j]] = okv[j] ? vr[j] : -1;
             }
             __syncthreads();
-            const int64_t lim = min<int64_t>(R, Lg - t0) * S;
+            const int64_t lim = imin64(R, Lg - t0) * S;
 #pragma unroll
             for (int j = 0; j < E; ++j) {
                 const int e = j * 256 + (int)threadIdx.x;
@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     const int32_t Lg = (int32_t)(seg_off[s0 + 1] - seg_off[s0]);
     if (Lg < lg_min || Lg >= lg_max) return;  // another launch's length class
     if (seg0 >= S || g * S + seg0 >= n_seg) return;
-    const int Sw = min(Sh, (int)min<int64_t>(S - seg0, n_seg - g * S - seg0));
+    const int Sw = min(Sh, (int)imin64(S - seg0, n_seg - g * S - seg0));
     const int64_t sw0 = sorder[g * S + seg0];
     const int32_t Lw = (int32_t)(seg_off[sw0 + 1] - seg_off[sw0]);
     const int l = lane / n_win, wi = lane - l * n_win;
@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(64) k_customer_walk(
     const double *g_amt = iamt + gbase + seg0 + l;  // row t of this lane's segment: g_amt[t * S]
     int32_t *nb = nb_out + (int64_t)wi * n_slots + gbase + seg0 + l;
     double *sm = sum_out + (int64_t)wi * n_slots + gbase + seg0 + l;
-    const int32_t n_out = (int32_t)min<int64_t>((int64_t)n_win * n_slots, INT32_MAX / 8);
+    const int32_t n_out = (int32_t)imin64((int64_t)n_win * n_slots, INT32_MAX / 8);
     const __amdgpu_buffer_rsrc_t rnb = __builtin_amdgcn_make_buffer_rsrc(nb_out, (short)0, n_out * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsm = __builtin_amdgcn_make_buffer_rsrc(sum_out, (short)0, n_out * 8, 0x00020000);
     // chunk element e = lane + j * 64 of this wave's Sw segments: row e / Sw, segment e % Sw --
@@ -1487,7 +1487,7 @@ __global__ void __launch_bounds__(kTermBlock) k_terminal_short(
     auto load = [&](int64_t b, int64_t L) {
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-            const int64_t j = min<int64_t>(c * kWave + lane, L - 1);  // clamped: no branch
+            const int64_t j = imin64(c * kWave + lane, L - 1);  // clamped: no branch
             pts[c] = gts[b + j];
             prw[c] = rows ? rows[b + j] : (int32_t)(b + j);
             pfr[c] = gfraud ? gfraud[b + j] : 0u;
