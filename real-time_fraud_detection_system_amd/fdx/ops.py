@@ -404,14 +404,16 @@ def customer_layout(seg_off, cperm, ts_ns, amount, n_windows: int, stream=None, 
                               None if windows_days is None else tuple(windows_days))
 
 
-def key_segments(keys, n_keys: int, stream=None, bad: torch.Tensor | None = None) -> torch.Tensor:
+def key_segments(keys, n_keys: int, stream=None, bad: torch.Tensor | None = None, alloc=None) -> torch.Tensor:
     """seg_off int64 [n_keys + 1] of the stable grouping by key (rekey's seg_off for keys in
-    [0, n_keys)) from a key histogram, no sort; bad (int32 [1], optional): out-of-range count."""
+    [0, n_keys)) from a key histogram, no sort; bad (int32 [1], optional): out-of-range count.
+    alloc: see Arena (output "seg", scratch "ksws")."""
     _dev(keys, torch.int32, "keys")
     L = _lib.load()
     dev = keys.device
-    seg = torch.empty(int(n_keys) + 1, dtype=torch.int64, device=dev)
-    ws = workspace(L.fdx_key_segments_workspace_size(int(n_keys)), dev)
+    A = alloc or _fresh(dev)
+    seg = A("seg", int(n_keys) + 1, torch.int64)
+    ws = A("ksws", max(L.fdx_key_segments_workspace_size(int(n_keys)), 1), torch.uint8)
     check(L.fdx_key_segments(_ptr(keys), keys.numel(), int(n_keys), _ptr(seg), _ptr(bad) if bad is not None else None,
                              _ptr(ws), ws.numel(), _s(stream)), "fdx_key_segments")
     return seg
