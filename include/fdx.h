@@ -265,6 +265,20 @@ int fdx_rekey_payload_checked(const int32_t *keys_d, int64_t n, int32_t key_bits
                               const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
                               int64_t *seg_off_d, uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d,
                               void *workspace_d, size_t workspace_bytes, void *stream);
+/* fdx_rekey_payload_checked (bad_d optional here) with the sorted keys written to the caller's
+ * sorted_keys_d (int32 [n], 16-byte aligned) instead of the segment offsets: the workspace is
+ * free again when the call's last pass ends, so a second re-key sharing it can start before
+ * the offsets are derived (fdx_segment_offsets_sorted, from sorted_keys_d, on any stream
+ * ordered after this call). */
+int fdx_rekey_payload_keys(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
+                           const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int32_t *sorted_keys_d,
+                           uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
+                           size_t workspace_bytes, void *stream);
+/* seg_off_d[0..n_keys] from keys sorted ascending (fdx_rekey's seg_off: rows of key k at
+ * [seg_off_d[k], seg_off_d[k+1])), one pass over the keys; keys outside [0, n_keys) never put an
+ * offset outside [0, n]. */
+int fdx_segment_offsets_sorted(const int32_t *sorted_keys_d, int64_t n, int64_t n_keys, int64_t *seg_off_d,
+                               void *stream);
 
 /* Stable argsort of int64 keys (e.g. TX_DATETIME ns): perm_d[j] = input row at sorted
  * position j, ties keep input order.  Used when a caller's frame is not in time order

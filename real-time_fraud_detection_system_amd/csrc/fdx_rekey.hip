@@ -669,7 +669,7 @@ extern "C" size_t fdx_rekey_payload_workspace_size(int64_t n, int32_t key_bits, 
 static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
                          const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
                          uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
-                         size_t workspace_bytes, void *stream);
+                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d = nullptr);
 
 extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
                                  const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
@@ -689,10 +689,34 @@ extern "C" int fdx_rekey_payload_checked(const int32_t *keys_d, int64_t n, int32
                          pay1_out_d, bad_d, workspace_d, workspace_bytes, stream);
 }
 
+extern "C" int fdx_rekey_payload_keys(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                                      const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d,
+                                      int32_t *perm_d, int32_t *sorted_keys_d, uint64_t *pay0_out_d,
+                                      uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d, size_t workspace_bytes,
+                                      void *stream) {
+    FDX_REQUIRE(n == 0 || sorted_keys_d, "null sorted_keys_d");
+    FDX_REQUIRE(((uintptr_t)sorted_keys_d & 15) == 0, "sorted_keys_d must be 16-byte aligned");
+    return rekey_payload(keys_d, n, key_bits, n_keys, flag_d, pay0_d, pay1_d, perm_d, nullptr, pay0_out_d,
+                         pay1_out_d, bad_d, workspace_d, workspace_bytes, stream, sorted_keys_d);
+}
+
+extern "C" int fdx_segment_offsets_sorted(const int32_t *sorted_keys_d, int64_t n, int64_t n_keys, int64_t *seg_off_d,
+                                          void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(n_keys >= 1 && n_keys < (int64_t)INT32_MAX, "n_keys out of range");
+    FDX_REQUIRE(seg_off_d && (n == 0 || sorted_keys_d), "null pointer");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
+        return FDX_OK;
+    }
+    return seg_offsets(reinterpret_cast<const uint32_t *>(sorted_keys_d), n, n_keys, seg_off_d, st);
+}
+
 static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
                          const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
                          uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
-                         size_t workspace_bytes, void *stream) {
+                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d) {
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     FDX_REQUIRE(key_bits >= 1 && key_bits <= 31, "key_bits must be in [1, 31]");
     FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
@@ -716,10 +740,15 @@ static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int
     const uint64_t *pin[2] = {pay0_d, pay1_d};
     uint64_t *pout[2] = {pay0_out_d, pay1_out_d};
     const uint32_t *sorted = nullptr;
-    int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, nullptr,
+    uint32_t *kout = reinterpret_cast<uint32_t *>(sorted_keys_d);
+    int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, kout,
                                   reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted, pw, flag_d, pin, pout,
                                   (uint64_t)n_keys, bad_d);
     if (rc) return rc;
+    if (kout && sorted != kout) {  // (no radix pass: the input order is the sorted one)
+        hipLaunchKernelGGL(k_copy_u32, dim3(stream_grid(n, 256)), dim3(256), 0, st, sorted, kout, n);
+        FDX_LAUNCHED("k_copy_u32");
+    }
     if (seg_off_d) return seg_offsets(sorted, n, n_keys, seg_off_d, st);
     return FDX_OK;
 }

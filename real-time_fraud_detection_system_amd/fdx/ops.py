@@ -124,13 +124,17 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
 
 def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
                   flag: torch.Tensor | None = None, stream=None, seg_off: bool = True, bad: torch.Tensor | None = None,
-                  alloc=None):
+                  alloc=None, keys_out: torch.Tensor | None = None):
     """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
     grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
     bad (int32 device scalar): receives the number of keys outside [0, n_keys), counted in the
     first radix pass (fdx_rekey_payload_checked; see KeyRangeCheck.from_count).
-    -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False), pay0 grouped | None,
-    pay1 grouped | None).  alloc: see Arena (outputs "perm", "seg", "pay0", "pay1", scratch "rekey_ws")."""
+    keys_out (int32 [n], 16-byte aligned): receives the sorted keys instead of seg_off being
+    derived (fdx_rekey_payload_keys; segment_offsets_sorted derives it later, so that another
+    re-key sharing the scratch may start in between).
+    -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False or keys_out), pay0 grouped |
+    None, pay1 grouped | None).  alloc: see Arena (outputs "perm", "seg", "pay0", "pay1", scratch
+    "rekey_ws")."""
     _dev(keys, torch.int32, "keys")
     n = keys.numel()
     dev = keys.device
@@ -145,13 +149,22 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
     kb = max(key_bits_for(n_keys), 1)
     A = alloc or _fresh(dev)
     perm = A("perm", n, torch.int32)
-    seg = A("seg", n_keys + 1, torch.int64) if seg_off else None
+    seg = A("seg", n_keys + 1, torch.int64) if seg_off and keys_out is None else None
     o0 = A("pay0", n, pay0.dtype) if pay0 is not None else None
     o1 = A("pay1", n, pay1.dtype) if pay1 is not None else None
     L = _lib.load()
     ws = A("rekey_ws", max(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), 1),
            torch.uint8)
-    if bad is not None:
+    if keys_out is not None:
+        _dev(keys_out, torch.int32, "keys_out")
+        if keys_out.numel() < n:
+            raise FdxError(f"keys_out holds {keys_out.numel()} keys, {n} needed")
+        if bad is not None:
+            _dev(bad, torch.int32, "bad")
+        check(L.fdx_rekey_payload_keys(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm),
+                                       _ptr(keys_out), _ptr(o0), _ptr(o1), _ptr(bad), _ptr(ws), ws.numel(), _s(stream)),
+              "fdx_rekey_payload_keys")
+    elif bad is not None:
         _dev(bad, torch.int32, "bad")
         check(L.fdx_rekey_payload_checked(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1),
                                           _ptr(perm), _ptr(seg), _ptr(o0), _ptr(o1), _ptr(bad), _ptr(ws), ws.numel(),
@@ -160,6 +173,18 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
         check(L.fdx_rekey_payload(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm),
                                   _ptr(seg), _ptr(o0), _ptr(o1), _ptr(ws), ws.numel(), _s(stream)), "fdx_rekey_payload")
     return perm, seg, o0, o1
+
+
+def segment_offsets_sorted(sorted_keys: torch.Tensor, n_keys: int, stream=None, alloc=None, n: int | None = None):
+    """seg_off int64 [n_keys + 1] from keys sorted ascending (the first n of sorted_keys; rekey's
+    seg_off), one pass (fdx_segment_offsets_sorted).  alloc: see Arena (output "seg")."""
+    _dev(sorted_keys, torch.int32, "sorted_keys")
+    n = sorted_keys.numel() if n is None else int(n)
+    A = alloc or _fresh(sorted_keys.device)
+    seg = A("seg", int(n_keys) + 1, torch.int64)
+    check(_lib.load().fdx_segment_offsets_sorted(_ptr(sorted_keys), n, int(n_keys), _ptr(seg), _s(stream)),
+          "fdx_segment_offsets_sorted")
+    return seg
 
 
 def key_map(keys: torch.Tensor, op: int, param: int, stream=None) -> torch.Tensor:

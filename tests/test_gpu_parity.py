@@ -100,6 +100,35 @@ def test_rekey_sorted_keys_unaligned_output(dev):
     np.testing.assert_array_equal(seg.cpu().numpy(), np.r_[0, np.cumsum(np.bincount(keys, minlength=n_keys))])
 
 
+@pytest.mark.parametrize("n,n_keys", [(0, 5), (1, 1), (5000, 1), (100_000, 50_000), (300_001, 100_000)])
+def test_rekey_payload_sorted_keys_then_offsets(dev, n, n_keys):
+    """fdx_rekey_payload_keys (the fused step's customer re-key: sorted keys to the caller's
+    buffer, no offsets) + fdx_segment_offsets_sorted == fdx_rekey_payload with offsets: perm,
+    payload, offsets; the id-range count too."""
+    rng = np.random.default_rng(n + 3 * n_keys)
+    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
+    ts = rng.integers(0, 1 << 60, size=n, dtype=np.int64)
+    amt = rng.random(n)
+    args = (T(keys, torch.int32, dev), n_keys, T(ts, torch.int64, dev), T(amt, torch.float64, dev))
+    p0, s0, t0, a0 = ops.rekey_payload(*args)
+    sk = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    bad = torch.full((1,), 9, dtype=torch.int32, device=dev)
+    p1, s1, t1, a1 = ops.rekey_payload(*args, keys_out=sk, bad=bad)
+    assert s1 is None
+    seg = ops.segment_offsets_sorted(sk, n_keys, n=n)
+    ref = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(p1.cpu().numpy(), ref)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
+    np.testing.assert_array_equal(sk[:n].cpu().numpy(), keys[ref])
+    np.testing.assert_array_equal(seg.cpu().numpy(), s0.cpu().numpy())
+    np.testing.assert_array_equal(t1.cpu().numpy(), t0.cpu().numpy())
+    np.testing.assert_array_equal(a1.cpu().numpy(), a0.cpu().numpy())
+    assert int(bad.item()) == 0
+    if n:  # a misaligned keys_out is refused
+        with pytest.raises(ops.FdxError):
+            ops.rekey_payload(*args, keys_out=torch.empty(n + 1, dtype=torch.int32, device=dev)[1:])
+
+
 def test_argsort_i64_and_perm_ops(dev):
     rng = np.random.default_rng(3)
     k = rng.integers(-(1 << 62), 1 << 62, size=200_001, dtype=np.int64)
