@@ -274,6 +274,19 @@ int fdx_rekey_payload_keys(const int32_t *keys_d, int64_t n, int32_t key_bits, i
                            const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int32_t *sorted_keys_d,
                            uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
                            size_t workspace_bytes, void *stream);
+/* The first radix pass's scanned digit table of a payload re-key, computed ahead of it (on
+ * another stream, e.g. while a re-key that shares the workspace still runs): hist0_d
+ * (fdx_rekey_hist0_size bytes, the caller's, not the workspace) also receives the id-range count
+ * into bad_d (optional, zeroed by the call) -- the check fdx_rekey_payload_checked does in that
+ * pass.  fdx_rekey_payload_hist0 is fdx_rekey_payload whose first pass goes straight to its
+ * scatter with that table; keys_d must be unchanged in between. */
+size_t fdx_rekey_hist0_size(int64_t n, int32_t key_bits);
+int fdx_rekey_hist0(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, void *hist0_d,
+                    size_t hist0_bytes, int32_t *bad_d, void *stream);
+int fdx_rekey_payload_hist0(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
+                            const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
+                            uint64_t *pay0_out_d, uint64_t *pay1_out_d, const void *hist0_d, void *workspace_d,
+                            size_t workspace_bytes, void *stream);
 /* seg_off_d[0..n_keys] from keys sorted ascending (fdx_rekey's seg_off: rows of key k at
  * [seg_off_d[k], seg_off_d[k+1])), one pass over the keys; keys outside [0, n_keys) never put an
  * offset outside [0, n]. */

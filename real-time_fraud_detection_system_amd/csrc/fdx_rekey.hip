@@ -553,18 +553,45 @@ void launch_scatter(const K *kin, const uint32_t *vin, int64_t n, int shift, K f
                        flip, tiles, hist, kout, vout, flag_in, pin[0], pin[1], pout[0], pout[1]);
 }
 
+// The digit schedule of a `bits`-bit key: passes, and how many leading passes take 9 bits.
+// 9-bit digits only where they save a pass (17- and 18-bit keys: 2 passes, not 3), and then
+// only as many as the key needs: 17 bits = 9 + 8 -- an 8-bit pass writes runs of ~16 keys
+// per digit and 4,096-key tile (a 9-bit pass ~8: twice the partial lines)
+void digit_plan(int bits, int *passes_out, int *n9_out) {
+    const int p8 = (bits + kRadixBits - 1) / kRadixBits, p9 = (bits + 8) / 9;
+    const int passes = std::min(p8, p9);
+    *passes_out = passes;
+    *n9_out = p9 < p8 ? std::max(0, bits - kRadixBits * passes) : 0;
+}
+
+// The first pass's per-tile digit table, scanned (what its scatter reads), into hist / part.
+template <typename K>
+int pass0_table(const K *keys, int64_t n, int bits, K flip, uint32_t *hist, uint32_t *part, uint64_t key_limit,
+                int32_t *bad, hipStream_t st) {
+    int passes, n9;
+    digit_plan(bits, &passes, &n9);
+    const int64_t tiles = ceil_div(n, kTile);
+    const int dbits = n9 > 0 ? 9 : kRadixBits;
+    if (dbits == 9)
+        hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, keys, n, 0, flip, tiles,
+                           hist, key_limit, bad);
+    else
+        hipLaunchKernelGGL((k_radix_hist<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, keys, n, 0, flip,
+                           tiles, hist, key_limit, bad);
+    FDX_LAUNCHED("k_radix_hist");
+    return exclusive_scan(hist, tiles * ((int64_t)1 << dbits), part, st);
+}
+
+// hist0 != nullptr: the first pass's scanned table, computed beforehand by pass0_table (e.g. on
+// another stream, while something else runs) -- the pass goes straight to its scatter.
 template <typename K>
 int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t *vals_out,
                const SortWs<K> &w, hipStream_t st, const K **sorted, int pw = 0, const uint8_t *flag_in = nullptr,
                const uint64_t *const *pay_in = nullptr, uint64_t *const *pay_out = nullptr, uint64_t key_limit = 0,
-               int32_t *bad = nullptr) {
+               int32_t *bad = nullptr, const uint32_t *hist0 = nullptr) {
     const int64_t tiles = ceil_div(n, kTile);
-    // 9-bit digits only where they save a pass (17- and 18-bit keys: 2 passes, not 3), and then
-    // only as many as the key needs: 17 bits = 9 + 8 -- an 8-bit pass writes runs of ~16 keys
-    // per digit and 4,096-key tile (a 9-bit pass ~8: twice the partial lines)
-    const int p8 = (bits + kRadixBits - 1) / kRadixBits, p9 = (bits + 8) / 9;
-    const int passes = std::min(p8, p9);
-    const int n9 = p9 < p8 ? std::max(0, bits - kRadixBits * passes) : 0;  // leading 9-bit passes
+    int passes, n9;
+    digit_plan(bits, &passes, &n9);
     const K *kin = keys;
     const uint32_t *vin = nullptr;  // identity on the first pass
     const uint64_t *pin[2] = {pw > 0 ? pay_in[0] : nullptr, pw > 1 ? pay_in[1] : nullptr};
@@ -590,18 +617,21 @@ int radix_sort(const K *keys, int64_t n, int bits, K flip, K *keys_out, uint32_t
         uint64_t *pout[2] = {nullptr, nullptr};
         for (int q = 0; q < pw; ++q) pout[q] = last ? pay_out[q] : w.q[q][p & 1];
         int32_t *bad_p = p == 0 ? bad : nullptr;
-        if (dbits == 9)
-            hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift, flip,
-                               tiles, w.hist, key_limit, bad_p);
-        else
-            hipLaunchKernelGGL((k_radix_hist<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n,
-                               shift, flip, tiles, w.hist, key_limit, bad_p);
-        FDX_LAUNCHED("k_radix_hist");
-        int rc = exclusive_scan(w.hist, tiles * ((int64_t)1 << dbits), w.part, st);
-        if (rc) return rc;
+        const uint32_t *htab = p == 0 && hist0 ? hist0 : w.hist;
+        if (htab == w.hist) {
+            if (dbits == 9)
+                hipLaunchKernelGGL((k_radix_hist<K, 9>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n, shift,
+                                   flip, tiles, w.hist, key_limit, bad_p);
+            else
+                hipLaunchKernelGGL((k_radix_hist<K, kRadixBits>), dim3((unsigned)tiles), dim3(kBlock), 0, st, kin, n,
+                                   shift, flip, tiles, w.hist, key_limit, bad_p);
+            FDX_LAUNCHED("k_radix_hist");
+            int rc = exclusive_scan(w.hist, tiles * ((int64_t)1 << dbits), w.part, st);
+            if (rc) return rc;
+        }
         const uint8_t *fl = p == 0 ? flag_in : nullptr;
 #define FDX_SCATTER(B, PWV) \
-    launch_scatter<K, B, PWV>(kin, vin, n, shift, flip, tiles, w.hist, kout, vout, fl, pin, pout, st)
+    launch_scatter<K, B, PWV>(kin, vin, n, shift, flip, tiles, htab, kout, vout, fl, pin, pout, st)
         if (dbits == 9) {
             if (pw == 2) FDX_SCATTER(9, 2); else if (pw == 1) FDX_SCATTER(9, 1); else FDX_SCATTER(9, 0);
         } else {
@@ -669,7 +699,8 @@ extern "C" size_t fdx_rekey_payload_workspace_size(int64_t n, int32_t key_bits, 
 static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
                          const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
                          uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
-                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d = nullptr);
+                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d = nullptr,
+                         const uint32_t *hist0_d = nullptr);
 
 extern "C" int fdx_rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
                                  const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d,
@@ -700,6 +731,44 @@ extern "C" int fdx_rekey_payload_keys(const int32_t *keys_d, int64_t n, int32_t 
                          pay1_out_d, bad_d, workspace_d, workspace_bytes, stream, sorted_keys_d);
 }
 
+extern "C" size_t fdx_rekey_hist0_size(int64_t n, int32_t key_bits) {
+    if (n < 0) n = 0;
+    int passes, n9;
+    digit_plan(key_bits, &passes, &n9);
+    const int64_t hm = std::max<int64_t>(1, ceil_div(n, kTile)) * ((int64_t)1 << (n9 > 0 ? 9 : kRadixBits));
+    return align_up(sizeof(uint32_t) * (size_t)hm) + sizeof(uint32_t) * (size_t)(scan_scratch_words(hm) + 2);
+}
+
+extern "C" int fdx_rekey_hist0(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, void *hist0_d,
+                               size_t hist0_bytes, int32_t *bad_d, void *stream) {
+    FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
+    FDX_REQUIRE(key_bits >= 1 && key_bits <= 31, "key_bits must be in [1, 31]");
+    FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
+    FDX_REQUIRE(hist0_d && (n == 0 || keys_d), "null pointer");
+    FDX_REQUIRE(hist0_bytes >= fdx_rekey_hist0_size(n, key_bits), "hist0 buffer too small");
+    hipStream_t st = as_stream(stream);
+    if (bad_d) FDX_HIP(hipMemsetAsync(bad_d, 0, sizeof(int32_t), st));
+    if (n == 0) return FDX_OK;
+    int passes, n9;
+    digit_plan(key_bits, &passes, &n9);
+    const int64_t hm = ceil_div(n, kTile) * ((int64_t)1 << (n9 > 0 ? 9 : kRadixBits));
+    uint32_t *hist = reinterpret_cast<uint32_t *>(hist0_d);
+    uint32_t *part = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(hist0_d) +
+                                                  align_up(sizeof(uint32_t) * (size_t)hm));
+    return pass0_table<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, hist, part,
+                                 (uint64_t)n_keys, bad_d, st);
+}
+
+extern "C" int fdx_rekey_payload_hist0(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys,
+                                       const uint8_t *flag_d, const uint64_t *pay0_d, const uint64_t *pay1_d,
+                                       int32_t *perm_d, int64_t *seg_off_d, uint64_t *pay0_out_d, uint64_t *pay1_out_d,
+                                       const void *hist0_d, void *workspace_d, size_t workspace_bytes, void *stream) {
+    FDX_REQUIRE(n == 0 || hist0_d, "null hist0_d");
+    return rekey_payload(keys_d, n, key_bits, n_keys, flag_d, pay0_d, pay1_d, perm_d, seg_off_d, pay0_out_d,
+                         pay1_out_d, nullptr, workspace_d, workspace_bytes, stream, nullptr,
+                         reinterpret_cast<const uint32_t *>(hist0_d));
+}
+
 extern "C" int fdx_segment_offsets_sorted(const int32_t *sorted_keys_d, int64_t n, int64_t n_keys, int64_t *seg_off_d,
                                           void *stream) {
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
@@ -716,7 +785,8 @@ extern "C" int fdx_segment_offsets_sorted(const int32_t *sorted_keys_d, int64_t 
 static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int64_t n_keys, const uint8_t *flag_d,
                          const uint64_t *pay0_d, const uint64_t *pay1_d, int32_t *perm_d, int64_t *seg_off_d,
                          uint64_t *pay0_out_d, uint64_t *pay1_out_d, int32_t *bad_d, void *workspace_d,
-                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d) {
+                         size_t workspace_bytes, void *stream, int32_t *sorted_keys_d,
+                         const uint32_t *hist0_d) {
     FDX_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "n out of range");
     FDX_REQUIRE(key_bits >= 1 && key_bits <= 31, "key_bits must be in [1, 31]");
     FDX_REQUIRE(n_keys >= 1 && n_keys <= (int64_t(1) << key_bits), "n_keys must be in [1, 2^key_bits]");
@@ -724,7 +794,7 @@ static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int
                     (pay1_d == nullptr || pay0_d != nullptr),
                 "payload inputs and outputs go together (stream 1 needs stream 0)");
     hipStream_t st = as_stream(stream);
-    if (bad_d) FDX_HIP(hipMemsetAsync(bad_d, 0, sizeof(int32_t), st));
+    if (bad_d && !hist0_d) FDX_HIP(hipMemsetAsync(bad_d, 0, sizeof(int32_t), st));  // (hist0: counted there)
     if (n == 0) {
         if (seg_off_d) FDX_HIP(hipMemsetAsync(seg_off_d, 0, sizeof(int64_t) * (n_keys + 1), st));
         return FDX_OK;
@@ -743,7 +813,7 @@ static int rekey_payload(const int32_t *keys_d, int64_t n, int32_t key_bits, int
     uint32_t *kout = reinterpret_cast<uint32_t *>(sorted_keys_d);
     int rc = radix_sort<uint32_t>(reinterpret_cast<const uint32_t *>(keys_d), n, key_bits, 0u, kout,
                                   reinterpret_cast<uint32_t *>(perm_d), w, st, &sorted, pw, flag_d, pin, pout,
-                                  (uint64_t)n_keys, bad_d);
+                                  (uint64_t)n_keys, hist0_d ? nullptr : bad_d, hist0_d);
     if (rc) return rc;
     if (kout && sorted != kout) {  // (no radix pass: the input order is the sorted one)
         hipLaunchKernelGGL(k_copy_u32, dim3(stream_grid(n, 256)), dim3(256), 0, st, sorted, kout, n);

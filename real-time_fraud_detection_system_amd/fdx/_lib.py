@@ -107,6 +107,9 @@ SIGNATURES = {
     "fdx_rekey_payload_checked": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_rekey_payload_keys": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_segment_offsets_sorted": (ctypes.c_int, [P, c_i64, c_i64, P, P]),
+    "fdx_rekey_hist0_size": (c_sz, [c_i64, c_i32]),
+    "fdx_rekey_hist0": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, c_sz, P, P]),
+    "fdx_rekey_payload_hist0": (ctypes.c_int, [P, c_i64, c_i32, c_i64, P, P, P, P, P, P, P, P, P, c_sz, P]),
     "fdx_terminal_windows_grouped": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P, P, P, P]),
     "fdx_terminal_windows_grouped_compact": (ctypes.c_int, [P, P, P, P, c_i64, c_i64, c_i64, P, c_i32, c_i32, P, P,
                                                             P]),

@@ -124,14 +124,16 @@ def rekey(keys: torch.Tensor, n_keys: int, stream=None, want_sorted_keys: bool =
 
 def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = None, pay1: torch.Tensor | None = None,
                   flag: torch.Tensor | None = None, stream=None, seg_off: bool = True, bad: torch.Tensor | None = None,
-                  alloc=None, keys_out: torch.Tensor | None = None):
+                  alloc=None, keys_out: torch.Tensor | None = None, hist0: torch.Tensor | None = None):
     """rekey that also moves up to two 8-byte columns (int64 / float64, input row order) into
     grouped order inside the radix passes; flag (uint8 per row) is packed into bit 31 of perm.
     bad (int32 device scalar): receives the number of keys outside [0, n_keys), counted in the
     first radix pass (fdx_rekey_payload_checked; see KeyRangeCheck.from_count).
     keys_out (int32 [n], 16-byte aligned): receives the sorted keys instead of seg_off being
     derived (fdx_rekey_payload_keys; segment_offsets_sorted derives it later, so that another
-    re-key sharing the scratch may start in between).
+    re-key sharing the scratch may start in between).  hist0: the first pass's table from
+    rekey_hist0 over the same keys (fdx_rekey_payload_hist0; the id-range count was taken there,
+    so bad must be None).
     -> (perm int32, seg_off int64[n_keys+1] (None with seg_off=False or keys_out), pay0 grouped |
     None, pay1 grouped | None).  alloc: see Arena (outputs "perm", "seg", "pay0", "pay1", scratch
     "rekey_ws")."""
@@ -155,7 +157,15 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
     L = _lib.load()
     ws = A("rekey_ws", max(L.fdx_rekey_payload_workspace_size(n, kb, (pay0 is not None) + (pay1 is not None)), 1),
            torch.uint8)
-    if keys_out is not None:
+    if hist0 is not None:
+        if bad is not None or keys_out is not None:
+            raise FdxError("hist0 takes neither bad (counted by rekey_hist0) nor keys_out")
+        if hist0.numel() < L.fdx_rekey_hist0_size(n, kb):
+            raise FdxError("hist0 is smaller than fdx_rekey_hist0_size")
+        check(L.fdx_rekey_payload_hist0(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm),
+                                        _ptr(seg), _ptr(o0), _ptr(o1), _ptr(hist0), _ptr(ws), ws.numel(), _s(stream)),
+              "fdx_rekey_payload_hist0")
+    elif keys_out is not None:
         _dev(keys_out, torch.int32, "keys_out")
         if keys_out.numel() < n:
             raise FdxError(f"keys_out holds {keys_out.numel()} keys, {n} needed")
@@ -173,6 +183,23 @@ def rekey_payload(keys: torch.Tensor, n_keys: int, pay0: torch.Tensor | None = N
         check(L.fdx_rekey_payload(_ptr(keys), n, kb, int(n_keys), _ptr(flag), _ptr(pay0), _ptr(pay1), _ptr(perm),
                                   _ptr(seg), _ptr(o0), _ptr(o1), _ptr(ws), ws.numel(), _s(stream)), "fdx_rekey_payload")
     return perm, seg, o0, o1
+
+
+def rekey_hist0(keys: torch.Tensor, n_keys: int, stream=None, bad: torch.Tensor | None = None, alloc=None):
+    """The first radix pass's scanned digit table of rekey_payload(keys, n_keys, ...), computed
+    ahead of it (fdx_rekey_hist0); bad (int32 device scalar, optional): the id-range count.
+    -> uint8 buffer for rekey_payload(hist0=).  alloc: see Arena (output "hist0")."""
+    _dev(keys, torch.int32, "keys")
+    n = keys.numel()
+    kb = max(key_bits_for(n_keys), 1)
+    L = _lib.load()
+    A = alloc or _fresh(keys.device)
+    h = A("hist0", max(L.fdx_rekey_hist0_size(n, kb), 1), torch.uint8)
+    if bad is not None:
+        _dev(bad, torch.int32, "bad")
+    check(L.fdx_rekey_hist0(_ptr(keys), n, kb, int(n_keys), _ptr(h), h.numel(), _ptr(bad), _s(stream)),
+          "fdx_rekey_hist0")
+    return h
 
 
 def segment_offsets_sorted(sorted_keys: torch.Tensor, n_keys: int, stream=None, alloc=None, n: int | None = None):

@@ -55,6 +55,10 @@ class FraudPipeline:
     crit_priority = 0
     side_priority = -1
     terminal_after_customer_rekey = True
+    # the terminal re-key's first histogram pass (+ scan, + the terminal id-range count) runs on
+    # the side stream at the step's start, beside the customer re-key, instead of after it on the
+    # critical chain (fdx_rekey_hist0 / fdx_rekey_payload_hist0)
+    terminal_hist_ahead = 1
     # the assembly and the forest on the terminal half's stream (the half that ends last), the NaN
     # flag cleared on the main stream beforehand (tools/step_ab.py measures it against 0)
     tail_on_side = 1
@@ -207,6 +211,11 @@ class FraudPipeline:
                 # the id range checks ride on the re-keys' first histogram pass (bad counts), read once
                 # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
                 bad = ar("bad", 2, torch.int32) if validate else None
+                th0 = None
+                if self.terminal_hist_ahead and self.terminal_after_customer_rekey:
+                    with torch.cuda.stream(side):
+                        th0 = ops.rekey_hist0(terminal, n_terminals, side, bad=bad[1:2] if validate else None,
+                                              alloc=ar.scope("th0"))
                 cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
                                                            bad=bad[0:1] if validate else None,
                                                            alloc=ar.scope("cust", rk_shared))
@@ -227,8 +236,8 @@ class FraudPipeline:
                 with torch.cuda.stream(side):
                     mk("start", side)
                     tperm, tseg, tgts, _ = ops.rekey_payload(terminal, n_terminals, ts_ns, flag=fraud, stream=side,
-                                                             bad=bad[1:2] if validate else None,
-                                                             alloc=ar.scope("term", rk_shared))
+                                                             bad=bad[1:2] if validate and th0 is None else None,
+                                                             alloc=ar.scope("term", rk_shared), hist0=th0)
                     if validate:
                         rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
                     mk("rekey_terminal", side)

@@ -129,6 +129,31 @@ def test_rekey_payload_sorted_keys_then_offsets(dev, n, n_keys):
             ops.rekey_payload(*args, keys_out=torch.empty(n + 1, dtype=torch.int32, device=dev)[1:])
 
 
+@pytest.mark.parametrize("n,n_keys", [(0, 5), (1, 1), (5000, 1), (4097, 257), (100_000, 50_000),
+                                      (300_001, 100_000), (70_000, 1 << 25)])  # 8- and 9-bit first digits
+def test_rekey_payload_with_first_table_ahead(dev, n, n_keys):
+    """fdx_rekey_hist0 (the first pass's scanned table + the id-range count, computed ahead) +
+    fdx_rekey_payload_hist0 == fdx_rekey_payload_checked: perm with the packed flag, payload,
+    offsets and the count of out-of-range ids."""
+    rng = np.random.default_rng(7 * n + n_keys)
+    keys = rng.integers(0, n_keys, size=n).astype(np.int32)
+    ts = rng.integers(0, 1 << 60, size=n, dtype=np.int64)
+    fr = (rng.random(n) < 0.2).astype(np.uint8)
+    for k in (keys, np.where(np.arange(n) % 9 == 4, -1 - keys, keys).astype(np.int32)):
+        kd = T(k, torch.int32, dev)
+        b0 = torch.full((1,), 5, dtype=torch.int32, device=dev)
+        b1 = torch.full((1,), 6, dtype=torch.int32, device=dev)
+        p0, s0, t0, _ = ops.rekey_payload(kd, n_keys, T(ts, torch.int64, dev), flag=T(fr, torch.uint8, dev), bad=b0)
+        h = ops.rekey_hist0(kd, n_keys, bad=b1)
+        p1, s1, t1, _ = ops.rekey_payload(kd, n_keys, T(ts, torch.int64, dev), flag=T(fr, torch.uint8, dev), hist0=h)
+        assert int(b1.item()) == int(b0.item()) == int(np.count_nonzero((k < 0) | (k >= n_keys)))
+        np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
+        np.testing.assert_array_equal(t1.cpu().numpy(), t0.cpu().numpy())
+        if int(b0.item()) == 0:  # (with ids out of range the offsets are unspecified: the caller raises)
+            np.testing.assert_array_equal(p1.cpu().numpy() & 0x7FFFFFFF, np.argsort(k, kind="stable"))
+            np.testing.assert_array_equal(s1.cpu().numpy(), s0.cpu().numpy())
+
+
 def test_argsort_i64_and_perm_ops(dev):
     rng = np.random.default_rng(3)
     k = rng.integers(-(1 << 62), 1 << 62, size=200_001, dtype=np.int64)
