@@ -216,6 +216,8 @@ class FraudPipeline:
                     with torch.cuda.stream(side):
                         th0 = ops.rekey_hist0(terminal, n_terminals, side, bad=bad[1:2] if validate else None,
                                               alloc=ar.scope("th0"))
+                        if validate:  # (the count's copy here too, off the terminal chain)
+                            rc_t = ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side)
                 cperm, cseg, gts, gamt = ops.rekey_payload(customer, n_customers, ts_ns, amount, stream=main,
                                                            bad=bad[0:1] if validate else None,
                                                            alloc=ar.scope("cust", rk_shared))
@@ -239,7 +241,8 @@ class FraudPipeline:
                                                              bad=bad[1:2] if validate and th0 is None else None,
                                                              alloc=ar.scope("term", rk_shared), hist0=th0)
                     if validate:
-                        rc.append(ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
+                        rc.append(rc_t if th0 is not None else
+                                  ops.KeyRangeCheck.from_count(bad[1:2], n_terminals, "terminal ids", side))
                     mk("rekey_terminal", side)
                     if compact:
                         trec = ops.terminal_windows_compact(tgts, tseg, rows=tperm, delay_days=self.delay_days,
