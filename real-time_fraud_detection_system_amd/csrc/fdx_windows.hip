@@ -207,7 +207,14 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
                                                                           int64_t n_seg, int32_t S, int64_t n_groups,
                                                                           int32_t *__restrict__ sorder,
                                                                           uint32_t *__restrict__ goff,
-                                                                          int32_t *__restrict__ status) {
+                                                                          int32_t *__restrict__ status,
+                                                                          int32_t *plan_host = nullptr) {
+    // plan_host (fdx_customer_layout_plan_async): the caller's pinned [slots, status] words, written
+    // from here at system scope -- no copy after the kernel (its blit waited ~70 us behind the
+    // terminal scatter's higher-priority blocks for a CU, r06au trace)
+    auto to_host = [&](int i, int32_t v) {
+        if (plan_host) __hip_atomic_store(plan_host + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
     __shared__ uint32_t s_h[kPlanWaves][kPlanBins];
     __shared__ int32_t s_long[kPlanMaxLong];
     __shared__ int32_t s_nlong;
@@ -263,7 +270,11 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
     __syncthreads();
     const int n_long = s_nlong;
     if (n_long > kPlanMaxLong) {  // uniform: the host falls back to the radix plan
-        if (tid == 0) *status = 1;
+        if (tid == 0) {
+            *status = 1;
+            to_host(0, 0);
+            to_host(1, 1);
+        }
         return;
     }
     // 2. exclusive prefix over (bin, wave) entries e = bin * 16 + wave, after the long segments
@@ -355,8 +366,14 @@ __global__ void __launch_bounds__(kPlanWaves * kWave) k_layout_plan_small(const 
         goff[g] = gr;
         gr += s_gs[g];
     }
-    if (tid == kT - 1) goff[n_groups] = wsum + inc;
-    if (tid == 0) *status = 0;
+    if (tid == kT - 1) {
+        goff[n_groups] = wsum + inc;
+        to_host(0, (int32_t)(wsum + inc));
+    }
+    if (tid == 0) {
+        *status = 0;
+        to_host(1, 0);
+    }
 }
 
 // one block per group: slot (t, l) <- time-order row r = cperm[seg_off[s] + t]
@@ -1891,11 +1908,20 @@ extern "C" int fdx_customer_layout_plan_async(const int64_t *seg_off_d, int64_t 
         return FDX_E_UNSUPPORTED;
     }
     int32_t *status = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + al256((size_t)n_seg * 4));
+    // pinned memory of the HIP allocator (torch's pin_memory included) maps into the device's
+    // address space: the kernel writes the two words itself; other host memory gets the copies
+    void *plan_dev = nullptr;
+    if (hipHostGetDevicePointer(&plan_dev, plan_h, 0) != hipSuccess) {
+        (void)hipGetLastError();  // (not an error of this call: the copy path follows)
+        plan_dev = nullptr;
+    }
     hipLaunchKernelGGL(k_layout_plan_small, dim3(1), dim3(kPlanWaves * kWave), 0, st, seg_off_d, n_seg, S, n_groups,
-                       sorder_d, goff_d, status);
+                       sorder_d, goff_d, status, reinterpret_cast<int32_t *>(plan_dev));
     FDX_LAUNCHED("k_layout_plan_small");
-    FDX_HIP(hipMemcpyAsync(plan_h, goff_d + n_groups, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    FDX_HIP(hipMemcpyAsync(plan_h + 1, status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (!plan_dev) {
+        FDX_HIP(hipMemcpyAsync(plan_h, goff_d + n_groups, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        FDX_HIP(hipMemcpyAsync(plan_h + 1, status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    }
     return FDX_OK;
 }
 
