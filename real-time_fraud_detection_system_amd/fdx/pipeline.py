@@ -212,7 +212,9 @@ class FraudPipeline:
                 # everything is enqueued (out-of-range ids cannot make the re-keys write out of bounds)
                 bad = ar("bad", 2, torch.int32) if validate else None
                 th0 = None
-                if self.terminal_hist_ahead and self.terminal_after_customer_rekey:
+                # (overlapped mode only: on one stream it would just run first, and the per-stage
+                # times bench.py takes in that mode would book it to the customer re-key)
+                if self.terminal_hist_ahead and self.terminal_after_customer_rekey and main is not caller:
                     with torch.cuda.stream(side):
                         th0 = ops.rekey_hist0(terminal, n_terminals, side, bad=bad[1:2] if validate else None,
                                               alloc=ar.scope("th0"))
