@@ -449,8 +449,16 @@ __global__ void k_seg_bounds4(const uint32_t *__restrict__ sk, int64_t n, int64_
     }
 }
 
+__global__ void k_zero_i64(int64_t *__restrict__ p, int64_t m) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = 0;
+}
+
 int seg_offsets(const uint32_t *sk, int64_t n, int64_t n_keys, int64_t *seg_off, hipStream_t st) {
-    FDX_HIP(hipMemsetAsync(seg_off, 0, sizeof(int64_t) * (size_t)(n_keys + 1), st));
+    // (one launch: hipMemsetAsync of the (n_keys + 1) x 8 bytes took two fill kernels, ~12 us on
+    // the terminal half's chain between its last scatter and its windows, r06ax trace)
+    hipLaunchKernelGGL(k_zero_i64, dim3(stream_grid(n_keys + 1, 256)), dim3(256), 0, st, seg_off, n_keys + 1);
+    FDX_LAUNCHED("k_zero_i64");
     if (((uintptr_t)sk & 15) == 0) {  // (the radix buffers; a caller's sorted_keys_d may not be)
         hipLaunchKernelGGL(k_seg_bounds4, dim3(stream_grid(ceil_div(n, 4), 256)), dim3(256), 0, st, sk, n, n_keys,
                            seg_off);
