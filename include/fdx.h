@@ -106,7 +106,9 @@ int fdx_customer_layout_plan(const int64_t *seg_off_d, int64_t n_seg, int32_t n_
                              void *stream);
 /* fdx_customer_layout_plan without the host synchronisation, for <= 65,536 segments (else
  * FDX_E_UNSUPPORTED): plan_h (caller-owned pinned host int32[2]) receives [slot count, status]
- * once the stream reaches them; status 1 = plan again with fdx_customer_layout_plan. */
+ * once the stream reaches them; status 1 = plan again with fdx_customer_layout_plan.  Pinned
+ * memory HIP maps into the device (hipHostMalloc, torch's pin_memory) is written by the plan
+ * kernel itself at system scope; other host memory gets two copies after it. */
 int fdx_customer_layout_plan_async(const int64_t *seg_off_d, int64_t n_seg, int32_t n_windows, int32_t *sorder_d,
                                    uint32_t *goff_d, int32_t *plan_h, void *workspace_d, size_t workspace_bytes,
                                    void *stream);
